@@ -1,0 +1,44 @@
+# Build the MI355X (gfx950) evaluator library, the synthetic-segment writer and the CPU oracle.
+# Direct hipcc/g++ invocations; `make -j8`.  Outputs land in-tree (git-ignored, shipped to the GPU box).
+HIPCC   ?= /opt/rocm/bin/hipcc
+ARCH    ?= gfx950
+ROCM    ?= /opt/rocm
+CXXFLAGS_HOST = -O3 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+HIPFLAGS = -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -munsafe-fp-atomics -Wall -Wno-unused-parameter
+
+SRC     = lakeside_amd/csrc
+OBJDIR  = build/obj
+LIB     = lakeside_amd/liblakeside_gpu.so
+SYNTH   = lakeside_amd/liblakeside_synth.so
+
+HOST_SRCS = $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
+HIP_OBJS  = $(OBJDIR)/kernels.o
+HDRS = $(wildcard $(SRC)/*.hpp) include/lakeside_gpu.h
+
+all: $(LIB) $(SYNTH)
+
+$(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(CXXFLAGS_HOST) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -c $< -o $@
+
+$(OBJDIR)/kernels.o: $(SRC)/kernels.hip $(HDRS)
+	@mkdir -p $(OBJDIR)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(LIB): $(HOST_OBJS) $(HIP_OBJS)
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+
+$(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
+	g++ -O3 -std=c++17 -fPIC -shared -pthread -Wall -o $@ tools/synth.cpp
+
+# Kernel ISA for inspection (register use, atomics, load widths)
+asm: $(SRC)/kernels.hip $(HDRS)
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o build/kernels.s
+
+clean:
+	rm -rf build $(LIB) $(SYNTH)
+
+
+.PHONY: all clean asm

@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: sealed-segment DataExpr evaluation on MI355X (BASELINE.json metric, config C2).
+
+One step = one evaluation of the query over every HBM-resident segment of this GPU's shard (scan kernel +
+finalize/compaction + result copy back to the host), i.e. one `lk_eval_pushdown` / `lk_eval_pushdown_dist`
+call.  Weak scaling: every GPU holds `--segments` segments of `--rows` rows (C2: 64 x 2^24); at N > 1 the
+request names all N x 64 segments, each rank scans its shard and the partial tables meet on rank 0 over RCCL.
+
+    python bench.py                      # N=1, C2
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port P bench.py --gpus 8
+"""
+import argparse
+import concurrent.futures as cf
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "rows/sec scanned + datapoints/sec emitted, 1B-row sealed DataExpr eval"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec (MI355X_MICROARCH.md)
+
+QUERIES = {
+    # C2 (BASELINE.json configs[1]): single :eq tag + :sum at 1m step
+    "c2": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                       "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
+               desc=":eq _cardinalhq.name=metric_07 :sum, step 1m"),
+    # C3 (configs[2]): :and/:re multi-tag predicate + :by 2-key group-by :max
+    "c3": dict(filter={"op": "and",
+                       "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
+                       "q2": {"k": "resource.service.name", "v": ["^svc-0[0-4]"], "op": "regex"}},
+               agg="max", group_bys=["resource.service.name", "resource.k8s.namespace.name"],
+               desc=":and(:eq name, :re service ^svc-0[0-4]) :by service,namespace :max, step 1m"),
+}
+
+
+def log(msg):
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--segments", type=int, default=64, help="segments per GPU")
+    ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
+    ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
+    ap.add_argument("--cpu-sample", type=int, default=2, help="segments timed on the CPU oracle (0: skip)")
+    ap.add_argument("--gen-workers", type=int, default=4)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+
+    import torch
+    import torch.distributed as dist
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd.evaluator import Engine
+
+    if world > 1:
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local_rank)
+    eng = Engine(local_rank)
+    if world > 1:
+        obj = [Engine.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        eng.comm_init(obj[0], world, rank)
+
+    # ---- segments of this rank (weak scaling: rank r owns global segments [r*S, (r+1)*S)) ----
+    S = args.segments
+    q = QUERIES[args.query]
+    total = S * world
+    mine = range(rank * S, (rank + 1) * S)
+    keys = [f"seg/{i}" for i in range(total)]
+    shard = [i // S for i in range(total)]
+
+    def gen(i):
+        return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4))
+
+    t0 = time.time()
+    bytes_loaded = 0
+    with cf.ThreadPoolExecutor(args.gen_workers) as ex:
+        for n, fut in enumerate(cf.as_completed([ex.submit(gen, i) for i in mine])):
+            i, seg = fut.result()
+            eng.put_segment_ptr(keys[i], seg.ptr, seg.size)
+            bytes_loaded += seg.size
+            seg.free()
+            if n % 8 == 7:
+                log(f"rank {rank}: {n + 1}/{S} segments generated + loaded to HBM ({time.time() - t0:.0f}s)")
+    log(f"rank {rank}: {S} segments ({bytes_loaded / 1e9:.1f} GB Parquet) resident, HBM cache "
+        f"{eng.segment_bytes / 1e9:.1f} GB, load {time.time() - t0:.0f}s")
+
+    segs = [synth.segment_request(i) for i in range(total)]
+    req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"]))
+
+    def step():
+        if world > 1:
+            return eng.eval_pushdown_dist(req, keys, shard, 10)
+        return eng.eval_pushdown(req, keys, 10, LK_MERGED)
+
+    for _ in range(args.warmup):
+        res = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    scan_ms, total_ms, alg_bytes, out_rows = [], [], 0, 0
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        scan_ms.append(res.stats["scan_ms"])
+        total_ms.append(res.stats["total_ms"])
+        alg_bytes = res.stats["algorithmic_bytes"]
+        out_rows = len(res)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        o = torch.tensor([out_rows], dtype=torch.int64)
+        dist.all_reduce(o, op=dist.ReduceOp.MAX)
+        out_rows = int(o.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    rows_total = total * args.rows
+    value = rows_total / (ms_per_step / 1e3)
+    scan_avg = sum(scan_ms) / len(scan_ms)
+    achieved = alg_bytes / (scan_avg / 1e3) / 1e9
+    log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
+        f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows")
+
+    traffic = None
+    prof = os.path.join(ROOT, "profiles", f"pmc_{args.query}.json")
+    if os.path.exists(prof):
+        with open(prof) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_sample > 0:
+        cpu = cpu_baseline(args, q, synth)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "f64",
+            "data": f"synthetic sealed Parquet (tools/synth.cpp, seed 20240101+i), {S} x {args.rows} rows per GPU",
+            "config": {"workload": f"{args.query.upper()}: {total} segments x {args.rows} rows, {q['desc']}",
+                       "segments_per_gpu": S, "rows_per_segment": args.rows, "glob_size": 10,
+                       "parallelism": f"segment-sharded x{world}" + (", RCCL table reduce" if world > 1 else "")},
+            "datapoints_per_sec": out_rows / (ms_per_step / 1e3),
+            "rows_scanned": rows_total, "output_rows": out_rows,
+            "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "algorithmic_bytes_per_launch": alg_bytes},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    eng.close()
+
+
+def cpu_baseline(args, q, synth):
+    """The CPU restatement (oracle/dataexpr.py: pyarrow decode + numpy) on a bounded sample of the same
+    workload, single-threaded.  A reported baseline, not the target."""
+    import pyarrow as pa
+    from oracle import dataexpr as dx
+    pa.set_cpu_count(1)
+    pa.set_io_thread_count(1)
+    n = args.cpu_sample
+    blobs = []
+    for i in range(n):
+        s = synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4))
+        blobs.append(s.bytes())
+        s.free()
+    keys = [f"cpu/{i}" for i in range(n)]
+    segs = [synth.segment_request(i) for i in range(n)]
+    pr = dx.parse_pushdown(json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"])))
+    t = time.perf_counter()
+    dx.evaluate_merged(pr, keys, 10, sources=blobs)
+    dt = time.perf_counter() - t
+    log(f"cpu baseline: {n} segments in {dt:.1f}s")
+    return {"value": n * args.rows / dt, "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{n} of the workload's segments ({n * args.rows} rows), same query, oracle/dataexpr.py "
+                      f"(pyarrow decode + numpy, 1 thread)"}
+
+
+if __name__ == "__main__":
+    main()

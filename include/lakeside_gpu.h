@@ -1,0 +1,92 @@
+/* lakeside_gpu.h — C ABI of the MI355X sealed-segment DataExpr evaluator.
+ *
+ * Drop-in for the worker's per-segment evaluator seam:
+ *   Commons.evaluatePushDownRequest(queryId, localParquet, pushDownRequest)
+ *     core/src/main/scala/com/cardinal/utils/Commons.scala:343-397
+ *   whose native seam is Commons.toGlobResultSet + resultSetToSource (Commons.scala:200-254, 280-341),
+ *   i.e. DuckDB's read_parquet + filter + hash GROUP BY + ORDER BY behind JDBC/JNI.
+ * The Scala side binds these symbols through JNA exactly as the reference already binds lib-trigram.so
+ * (core/src/main/scala/com/cardinal/utils/ast/queries/NLPUtils.scala:43-52); see INTEGRATION.md.
+ *
+ * Conventions: 0 = success, negative = error (message in lk_last_error(), thread-local).  Never throws or
+ * aborts across the ABI.  Inputs are borrowed for the duration of the call.  Results are owned by the
+ * library until lk_result_free.  Calls on one engine are thread-safe (serialised per engine).
+ */
+#ifndef LAKESIDE_GPU_H
+#define LAKESIDE_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct lk_engine lk_engine;   /* one per process per GPU: device, streams, HBM segment cache, RCCL comm */
+typedef struct lk_result lk_result;   /* rows of one evaluation */
+
+enum {
+  LK_OK = 0,
+  LK_ERR_ARG = -1,          /* bad argument / malformed JSON */
+  LK_ERR_UNSUPPORTED = -2,  /* query or file shape outside the implemented path */
+  LK_ERR_IO = -3,           /* file read / Parquet parse */
+  LK_ERR_DEVICE = -4,       /* HIP / RCCL failure, or no GPU */
+  LK_ERR_MEMORY = -5
+};
+
+/* Flags of lk_eval_pushdown. */
+#define LK_PER_GLOB_ROWS 1u   /* rows of every glob separately (the worker's output, S17) */
+#define LK_MERGED 2u          /* cells merged across globs as query-api does (TimeGroupedSketchAggregator, S19) */
+
+/* options_json: {"device": 0, "rank": 0, "world": 1}; NULL = defaults.
+ * Replaces DuckDbConnectionFactory (core/.../utils/DuckDbConnectionFactory.scala:76-114). */
+int lk_engine_create(const char* options_json, lk_engine** out);
+void lk_engine_destroy(lk_engine* e);
+
+/* HBM segment cache (replaces the worker's Caffeine disk cache, worker/WorkerApi.scala:53-77).
+ * lk_segment_put: register Parquet bytes under `key` (e.g. the path Commons.toParquetFilePath builds,
+ * Commons.scala:256-278) and upload them; lk_segment_load: read a local Parquet file into the cache.
+ * Re-putting an existing key replaces it. */
+int lk_segment_put(lk_engine* e, const char* key, const uint8_t* data, size_t size);
+int lk_segment_load(lk_engine* e, const char* path);
+int lk_segment_evict(lk_engine* e, const char* key);
+size_t lk_segment_count(const lk_engine* e);
+/* HBM bytes held by the cache. */
+size_t lk_segment_bytes(const lk_engine* e);
+
+/* Mirrors one Commons.evaluatePushDownRequest call (Commons.scala:343-397).
+ * push_down_json: PushDownRequest.toJson wire format (core/.../model/SegmentRequest.scala:30-60).
+ * paths[i]: cache key (or local file, loaded on a miss) of segmentRequests[i].
+ * glob_size: 10 for local Parquet, 5 for remote (Commons.scala:361); 0 = 10.
+ * flags: LK_PER_GLOB_ROWS or LK_MERGED. */
+int lk_eval_pushdown(lk_engine* e, const char* push_down_json, const char* const* paths, size_t n_paths,
+                     int glob_size, unsigned flags, lk_result** out);
+
+size_t lk_result_num_rows(const lk_result* r);
+const int64_t* lk_result_timestamps(const lk_result* r);   /* ascending (ties: glob, then group order) */
+const double* lk_result_values(const lk_result* r);
+const uint32_t* lk_result_globs(const lk_result* r);       /* glob index per row (0 when merged) */
+size_t lk_result_num_tag_columns(const lk_result* r);
+const char* lk_result_tag_name(const lk_result* r, size_t col);             /* "name", groupBys, queryTags keys */
+const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col); /* NULL => tag absent (S15) */
+/* JSON: {"scan_ms":..,"total_ms":..,"rows_scanned":..,"algorithmic_bytes":..,"tiles":..,"cells":..} */
+const char* lk_result_stats(const lk_result* r);
+void lk_result_free(lk_result* r);
+
+const char* lk_last_error(void);
+
+/* ---- multi-GPU (one process per GPU; segments sharded across ranks, partial tables merged over RCCL) ---- */
+#define LK_UNIQUE_ID_BYTES 128
+/* Fill `id` (LK_UNIQUE_ID_BYTES) on rank 0; broadcast it out of band (e.g. torch.distributed). */
+int lk_comm_unique_id(uint8_t* id);
+int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank);
+/* Like lk_eval_pushdown with LK_MERGED, but this rank evaluates only the segments whose index i has
+ * shard[i] == rank; partial tables are reduced to rank 0 over RCCL, which alone receives rows
+ * (other ranks get an empty result). shard == NULL: i % world. */
+int lk_eval_pushdown_dist(lk_engine* e, const char* push_down_json, const char* const* paths, size_t n_paths,
+                          const int32_t* shard, int glob_size, lk_result** out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LAKESIDE_GPU_H */

@@ -1,0 +1,143 @@
+// extern "C" surface of include/lakeside_gpu.h: argument checks, exception -> status translation.
+#include <cstring>
+#include <exception>
+#include <new>
+#include <string>
+
+#include "../../include/lakeside_gpu.h"
+#include "engine.hpp"
+#include "json.hpp"
+#include "plan.hpp"
+
+namespace lk {
+int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
+             unsigned flags, const int32_t* shard, bool dist, lk_result* res);
+}
+
+namespace {
+thread_local std::string t_err;
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const lk::PlanError& e) {
+    t_err = e.what();
+    return e.code;
+  } catch (const lk::JsonError& e) {
+    t_err = e.what();
+    return LK_ERR_ARG;
+  } catch (const std::bad_alloc&) {
+    t_err = "out of host memory";
+    return LK_ERR_MEMORY;
+  } catch (const std::exception& e) {
+    t_err = e.what();
+    std::string m = e.what();
+    if (m.rfind("HIP", 0) == 0 || m.find("device") != std::string::npos) return LK_ERR_DEVICE;
+    if (m.rfind("parquet", 0) == 0 || m.rfind("thrift", 0) == 0) return LK_ERR_IO;
+    return LK_ERR_ARG;
+  }
+}
+}  // namespace
+
+namespace lk {
+void set_error(const std::string& m) { t_err = m; }
+}
+
+extern "C" {
+
+const char* lk_last_error(void) { return t_err.c_str(); }
+
+int lk_engine_create(const char* options_json, lk_engine** out) {
+  if (!out) return LK_ERR_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    int dev = 0;
+    if (options_json && *options_json) {
+      lk::Json o = lk::Json::parse(options_json);
+      if (const lk::Json* d = o.get("device")) dev = int(d->as_i64());
+    }
+    auto* e = new lk_engine();
+    try {
+      e->e = std::make_unique<lk::Engine>(dev);
+    } catch (...) {
+      delete e;
+      throw;
+    }
+    *out = e;
+    return LK_OK;
+  });
+}
+
+void lk_engine_destroy(lk_engine* e) { delete e; }
+
+int lk_segment_put(lk_engine* e, const char* key, const uint8_t* data, size_t size) {
+  if (!e || !key || (!data && size)) return LK_ERR_ARG;
+  return guarded([&] { return e->e->put_segment(key, data, size); });
+}
+
+int lk_segment_load(lk_engine* e, const char* path) {
+  if (!e || !path) return LK_ERR_ARG;
+  return guarded([&] {
+    e->e->get_segment(path, true);
+    return LK_OK;
+  });
+}
+
+int lk_segment_evict(lk_engine* e, const char* key) {
+  if (!e || !key) return LK_ERR_ARG;
+  std::lock_guard<std::mutex> g(e->e->cache_mu);
+  auto it = e->e->cache.find(key);
+  if (it == e->e->cache.end()) return LK_ERR_ARG;
+  e->e->cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
+  e->e->cache.erase(it);
+  return LK_OK;
+}
+
+size_t lk_segment_count(const lk_engine* e) { return e ? e->e->cache.size() : 0; }
+size_t lk_segment_bytes(const lk_engine* e) { return e ? e->e->cache_bytes : 0; }
+
+static int eval_common(lk_engine* e, const char* json, const char* const* paths, size_t n_paths, const int32_t* shard,
+                       int glob_size, unsigned flags, bool dist, lk_result** out) {
+  if (!e || !json || !out || (n_paths && !paths)) return LK_ERR_ARG;
+  *out = nullptr;
+  return guarded([&] {
+    auto* r = new lk_result();
+    try {
+      std::lock_guard<std::mutex> g(e->e->eval_mu);
+      lk::evaluate(*e->e, json, paths, n_paths, glob_size, flags, shard, dist, r);
+    } catch (...) {
+      delete r;
+      throw;
+    }
+    *out = r;
+    return LK_OK;
+  });
+}
+
+int lk_eval_pushdown(lk_engine* e, const char* push_down_json, const char* const* paths, size_t n_paths, int glob_size,
+                     unsigned flags, lk_result** out) {
+  return eval_common(e, push_down_json, paths, n_paths, nullptr, glob_size, flags, false, out);
+}
+
+int lk_eval_pushdown_dist(lk_engine* e, const char* push_down_json, const char* const* paths, size_t n_paths,
+                          const int32_t* shard, int glob_size, lk_result** out) {
+  return eval_common(e, push_down_json, paths, n_paths, shard, glob_size, LK_MERGED, true, out);
+}
+
+size_t lk_result_num_rows(const lk_result* r) { return r ? r->ts.size() : 0; }
+const int64_t* lk_result_timestamps(const lk_result* r) { return r ? r->ts.data() : nullptr; }
+const double* lk_result_values(const lk_result* r) { return r ? r->val.data() : nullptr; }
+const uint32_t* lk_result_globs(const lk_result* r) { return r ? r->glob.data() : nullptr; }
+size_t lk_result_num_tag_columns(const lk_result* r) { return r ? r->tag_names.size() : 0; }
+const char* lk_result_tag_name(const lk_result* r, size_t col) {
+  return (r && col < r->tag_names.size()) ? r->tag_names[col].c_str() : nullptr;
+}
+const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col) {
+  if (!r || row >= r->ts.size() || col >= r->tag_names.size()) return nullptr;
+  return r->tag_vals[row * r->tag_names.size() + col];
+}
+const char* lk_result_stats(const lk_result* r) { return r ? r->stats.c_str() : nullptr; }
+void lk_result_free(lk_result* r) { delete r; }
+
+}  // extern "C"

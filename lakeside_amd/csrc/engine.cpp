@@ -1,0 +1,547 @@
+// lakeside_gpu engine: HBM segment cache, engine-global dictionaries, plan compile, evaluation, results.
+//
+// Replaces, for the hot query shape, the worker evaluator's DuckDB seam:
+//   Commons.evaluatePushDownRequest / toGlobResultSet / resultSetToSource / toDataPoint
+//   (core/src/main/scala/com/cardinal/utils/Commons.scala:200-462)
+// and the query-api cross-glob merge (core/src/main/scala/com/cardinal/eval/TimeGroupedSketchAggregator.scala:57-177).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <fstream>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <regex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/lakeside_gpu.h"
+#include "engine.hpp"
+#include "kernels.hpp"
+#include "layout.hpp"
+#include "parquet.hpp"
+#include "plan.hpp"
+#include "thrift.hpp"
+
+namespace lk {
+
+// ------------------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------------------
+struct DeviceError : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
+#define HIP_CHECK(x)                                                                          \
+  do {                                                                                        \
+    hipError_t _e = (x);                                                                      \
+    if (_e != hipSuccess)                                                                     \
+      throw DeviceError(std::string("HIP: ") + #x + ": " + hipGetErrorString(_e));            \
+  } while (0)
+
+static constexpr size_t kAlign = 256;
+static inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
+
+// ------------------------------------------------------------------------------------------------
+// engine-global dictionaries: one per column name; chunk dictionaries remap into them at load
+// ------------------------------------------------------------------------------------------------
+uint32_t GlobalDict::intern(const std::string& s) {
+  auto it = ids.find(s);
+  if (it != ids.end()) return it->second;
+  uint32_t id = uint32_t(vals.size());
+  vals.push_back(s);
+  ids.emplace(vals.back(), id);
+  return id;
+}
+
+GlobalDict& Engine::dict(const std::string& col) {
+  std::lock_guard<std::mutex> g(dict_mu);
+  auto& p = dicts[col];
+  if (!p) p = std::make_unique<GlobalDict>();
+  return *p;
+}
+
+// ------------------------------------------------------------------------------------------------
+// segment load: footer + page walk + run directories + tiles + zone maps -> HBM
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+struct PageStreams {
+  const uint8_t* defs = nullptr;
+  size_t defs_len = 0;
+  const uint8_t* vals = nullptr;
+  size_t vals_len = 0;
+  uint32_t nrows = 0;
+  int encoding = 0;
+};
+
+struct HostPage {
+  PageDesc d{};
+  uint32_t rg = 0;
+  uint32_t run_lo = 0, run_n = 0, drun_lo = 0, drun_n = 0;
+  std::vector<uint32_t> vprefix;   // nullable pages with NULLs: non-null rows before row i (size nrows+1)
+  const uint8_t* host_vals = nullptr;
+};
+
+struct Builder {
+  Engine& E;
+  const uint8_t* F;
+  size_t size;
+  Segment& S;
+  std::vector<uint8_t> stage;
+  std::vector<std::vector<HostPage>> pages;   // per column
+
+  size_t put(const uint8_t* p, size_t n) {
+    size_t off = align_up(stage.size(), 16);
+    stage.resize(off + n);
+    if (n) memcpy(stage.data() + off, p, n);
+    return off;
+  }
+};
+
+PageStreams split_page(const pq::PageHeader& h, const uint8_t* data, size_t n, bool nullable) {
+  PageStreams s;
+  if (h.type == pq::DATA_PAGE) {
+    s.nrows = uint32_t(h.num_values);
+    s.encoding = h.encoding;
+    size_t off = 0;
+    if (nullable) {
+      if (h.def_encoding != pq::RLE) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: BIT_PACKED definition levels");
+      if (n < 4) throw PlanError(LK_ERR_IO, "parquet: truncated page");
+      uint32_t L;
+      memcpy(&L, data, 4);
+      if (size_t(L) + 4 > n) throw PlanError(LK_ERR_IO, "parquet: bad def-level length");
+      s.defs = data + 4;
+      s.defs_len = L;
+      off = 4 + L;
+    }
+    s.vals = data + off;
+    s.vals_len = n - off;
+  } else {  // DATA_PAGE_V2
+    s.nrows = uint32_t(h.num_rows >= 0 ? h.num_rows : h.num_values);
+    s.encoding = h.encoding;
+    if (h.rep_len) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: repeated columns");
+    size_t off = size_t(h.rep_len);
+    if (size_t(h.def_len) + off > n) throw PlanError(LK_ERR_IO, "parquet: bad v2 level lengths");
+    if (nullable) {
+      s.defs = data + off;
+      s.defs_len = size_t(h.def_len);
+    }
+    off += size_t(h.def_len);
+    s.vals = data + off;
+    s.vals_len = n - off;
+  }
+  return s;
+}
+
+void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m) {
+  HostCol& col = B.S.cols[ci];
+  if (m.codec != 0)
+    throw PlanError(LK_ERR_UNSUPPORTED, "parquet: compressed column chunks (codec " + std::to_string(m.codec) +
+                                            ") are not supported yet");
+  int64_t start = m.data_page_offset;
+  if (m.dictionary_page_offset > 0 && m.dictionary_page_offset < start) start = m.dictionary_page_offset;
+  if (start < 4 || size_t(start) >= B.size) throw PlanError(LK_ERR_IO, "parquet: bad page offset");
+  col.compressed_bytes += uint64_t(m.total_compressed);
+  size_t pos = size_t(start);
+  int64_t seen = 0;
+  uint32_t remap_off = uint32_t(col.remap.size());
+  uint32_t dict_n = 0;
+  bool have_dict = false;
+  uint32_t first_row = 0;
+  while (seen < m.num_values) {
+    if (pos >= B.size) throw PlanError(LK_ERR_IO, "parquet: page walk ran past the file");
+    pq::PageHeader h = pq::parse_page_header(B.F + pos, B.size - pos);
+    const uint8_t* data = B.F + pos + h.header_len;
+    size_t n = size_t(h.compressed);
+    if (pos + h.header_len + n > B.size) throw PlanError(LK_ERR_IO, "parquet: page overruns the file");
+    pos += h.header_len + n;
+    if (h.type == pq::DICTIONARY_PAGE) {
+      if (!col.is_string) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: dictionary-encoded non-string column " + col.name);
+      GlobalDict& gd = B.E.dict(col.name);
+      std::lock_guard<std::mutex> g(gd.mu);
+      size_t p = 0;
+      col.remap.reserve(col.remap.size() + size_t(h.dict_num_values));
+      for (int32_t i = 0; i < h.dict_num_values; i++) {
+        if (p + 4 > n) throw PlanError(LK_ERR_IO, "parquet: truncated dictionary page");
+        uint32_t L;
+        memcpy(&L, data + p, 4);
+        p += 4;
+        if (p + L > n) throw PlanError(LK_ERR_IO, "parquet: truncated dictionary entry");
+        col.remap.push_back(gd.intern(std::string(reinterpret_cast<const char*>(data + p), L)));
+        p += L;
+      }
+      dict_n = uint32_t(h.dict_num_values);
+      have_dict = true;
+      continue;
+    }
+    if (h.type != pq::DATA_PAGE && h.type != pq::DATA_PAGE_V2) continue;   // index pages: skip
+    PageStreams st = split_page(h, data, n, col.nullable);
+    HostPage hp;
+    hp.rg = rg;
+    PageDesc& d = hp.d;
+    d.first_row = first_row;
+    d.nrows = st.nrows;
+    d.nullable = col.nullable ? 1 : 0;
+    // definition levels
+    uint32_t nvals = st.nrows;
+    if (col.nullable) {
+      auto druns = pq::hybrid_runs(st.defs, st.defs_len, 1, st.nrows);
+      std::vector<uint32_t> defv(st.nrows);
+      pq::hybrid_decode(st.defs, st.defs_len, 1, st.nrows, defv.data());
+      nvals = 0;
+      for (uint32_t v : defv) nvals += v ? 1 : 0;
+      d.has_nulls = nvals < st.nrows;
+      if (d.has_nulls) {
+        hp.vprefix.resize(st.nrows + 1);
+        uint32_t acc = 0;
+        for (uint32_t i = 0; i < st.nrows; i++) {
+          hp.vprefix[i] = acc;
+          acc += defv[i] ? 1 : 0;
+        }
+        hp.vprefix[st.nrows] = acc;
+        hp.drun_lo = uint32_t(col.runs.size());
+        for (auto& r : druns)
+          col.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
+        hp.drun_n = uint32_t(druns.size());
+        d.defs = B.put(st.defs, st.defs_len);
+        d.defs_len = uint32_t(st.defs_len);
+      }
+    }
+    d.nvals = nvals;
+    if (col.is_string) {
+      if (st.encoding != pq::RLE_DICTIONARY && st.encoding != pq::PLAIN_DICTIONARY)
+        throw PlanError(LK_ERR_UNSUPPORTED, "parquet: non-dictionary string page in column " + col.name +
+                                                " (PLAIN fallback not supported yet)");
+      if (!have_dict) throw PlanError(LK_ERR_IO, "parquet: dictionary page missing for " + col.name);
+      if (st.vals_len < 1 && nvals) throw PlanError(LK_ERR_IO, "parquet: empty dictionary-index page");
+      int bw = st.vals_len ? st.vals[0] : 0;
+      if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
+      const uint8_t* stream = st.vals_len ? st.vals + 1 : st.vals;
+      size_t slen = st.vals_len ? st.vals_len - 1 : 0;
+      auto runs = pq::hybrid_runs(stream, slen, bw, nvals);
+      // validate every index against the dictionary so a corrupt page can never index out of bounds on the GPU
+      std::vector<uint32_t> idx(nvals);
+      pq::hybrid_decode(stream, slen, bw, nvals, idx.data());
+      for (uint32_t v : idx)
+        if (v >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
+      hp.run_lo = uint32_t(col.runs.size());
+      for (auto& r : runs)
+        col.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
+      hp.run_n = uint32_t(runs.size());
+      d.kind = PAGE_DICT;
+      d.bw = uint8_t(bw);
+      d.remap = remap_off;
+      d.dict_n = dict_n;
+      d.vals = B.put(stream, slen);
+      d.vals_len = uint32_t(slen);
+    } else {
+      if (st.encoding != pq::PLAIN) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: non-PLAIN numeric page in " + col.name);
+      if (st.vals_len < size_t(nvals) * 8) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN page in " + col.name);
+      d.kind = PAGE_PLAIN64;
+      d.vals = B.put(st.vals, size_t(nvals) * 8);
+      d.vals_len = nvals * 8;
+      hp.host_vals = st.vals;
+    }
+    B.pages[ci].push_back(std::move(hp));
+    first_row += st.nrows;
+    seen += h.type == pq::DATA_PAGE ? h.num_values : st.nrows;
+  }
+  if (first_row != uint32_t(B.S.rg_rows[rg]))
+    throw PlanError(LK_ERR_IO, "parquet: column " + col.name + " row count disagrees with its row group");
+}
+
+// value index within page of row r (relative to page)
+inline uint32_t vindex(const HostPage& p, uint32_t r) { return p.vprefix.empty() ? r : p.vprefix[r]; }
+// first row (relative to page) whose value index is >= v
+inline uint32_t row_of_vindex(const HostPage& p, uint32_t v) {
+  if (p.vprefix.empty()) return v;
+  return uint32_t(std::lower_bound(p.vprefix.begin(), p.vprefix.end() - 1, v) - p.vprefix.begin());
+}
+
+// run index (within [lo, lo+n)) containing position x; runs sorted by start
+inline uint32_t run_containing(const std::vector<RunDesc>& runs, uint32_t lo, uint32_t n, uint32_t x) {
+  uint32_t a = lo, b = lo + n - 1;
+  while (a < b) {
+    uint32_t mid = (a + b + 1) / 2;
+    if (runs[mid].start <= x) a = mid;
+    else b = mid - 1;
+  }
+  return a;
+}
+
+void build_tiles(Builder& B) {
+  Segment& S = B.S;
+  const int nc = int(S.cols.size());
+  std::vector<size_t> page_cursor(nc, 0);
+  int ts_col = S.col_index(kTimestamp);
+  for (uint32_t rg = 0; rg < S.rg_rows.size(); rg++) {
+    uint32_t nrows = uint32_t(S.rg_rows[rg]);
+    uint32_t a = 0;
+    while (a < nrows) {
+      uint32_t e = std::min<uint64_t>(nrows, uint64_t(a) + TILE_ROWS);
+      // page of every column containing row a; clip e to that page's end and to the run caps
+      std::vector<size_t> pidx(nc);
+      for (int c = 0; c < nc; c++) {
+        auto& pg = B.pages[c];
+        size_t& k = page_cursor[c];
+        while (k < pg.size() && (pg[k].rg < rg || (pg[k].rg == rg && pg[k].d.first_row + pg[k].d.nrows <= a))) k++;
+        if (k >= pg.size() || pg[k].rg != rg) throw PlanError(LK_ERR_IO, "parquet: page index inconsistent");
+        pidx[c] = k;
+        const HostPage& p = pg[k];
+        e = std::min(e, p.d.first_row + p.d.nrows);
+        uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
+        if (p.d.kind == PAGE_DICT && p.run_n) {
+          uint32_t va = vindex(p, ra), ve = vindex(p, re);
+          if (ve > va) {
+            uint32_t r0 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, va);
+            uint32_t r1 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, ve - 1);
+            if (r1 - r0 + 1 > RUN_CAP) {
+              uint32_t vcut = S.cols[c].runs[r0 + RUN_CAP].start;
+              e = std::min(e, p.d.first_row + row_of_vindex(p, vcut));
+            }
+          }
+        }
+        if (p.d.has_nulls) {
+          re = e - p.d.first_row;
+          uint32_t r0 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, ra);
+          uint32_t r1 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, re - 1);
+          if (r1 - r0 + 1 > RUN_CAP) e = std::min(e, p.d.first_row + S.cols[c].runs[r0 + RUN_CAP].start);
+        }
+      }
+      if (e <= a) throw PlanError(LK_ERR_IO, "parquet: tile construction made no progress");
+      TileDesc t{};
+      t.rg = rg;
+      t.row0 = a;
+      t.nrows = e - a;
+      t.ts_min = INT64_MAX;
+      t.ts_max = INT64_MIN;
+      uint32_t tile_index = uint32_t(S.tiles.size());
+      for (int c = 0; c < nc; c++) {
+        const HostPage& p = B.pages[c][pidx[c]];
+        TileCol tc{};
+        tc.page = uint32_t(pidx[c]);
+        uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
+        uint32_t va = vindex(p, ra), ve = vindex(p, re);
+        tc.vbase = va;
+        if (p.d.kind == PAGE_DICT && p.run_n && ve > va) {
+          uint32_t r0 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, va);
+          uint32_t r1 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, ve - 1);
+          tc.run_lo = r0;
+          tc.nruns = r1 - r0 + 1;
+        }
+        if (p.d.has_nulls) {
+          uint32_t r0 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, ra);
+          uint32_t r1 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, re - 1);
+          tc.drun_lo = r0;
+          tc.ndruns = r1 - r0 + 1;
+        }
+        S.cols[c].tcols.push_back(tc);
+        if (c == ts_col && p.d.kind == PAGE_PLAIN64 && !S.cols[c].is_string) {
+          for (uint32_t v = va; v < ve; v++) {
+            int64_t x;
+            memcpy(&x, p.host_vals + size_t(v) * 8, 8);
+            t.ts_min = std::min(t.ts_min, x);
+            t.ts_max = std::max(t.ts_max, x);
+          }
+        }
+      }
+      (void)tile_index;
+      S.tiles.push_back(t);
+      a = e;
+    }
+  }
+}
+
+}  // namespace
+
+int Segment::col_index(const std::string& name) const {
+  auto it = by_name.find(name);
+  return it == by_name.end() ? -1 : it->second;
+}
+
+Segment::~Segment() {
+  if (d_data) (void)hipFree(d_data);
+  if (d_meta) (void)hipFree(d_meta);
+}
+
+std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uint8_t* F, size_t size) {
+  auto S = std::make_shared<Segment>();
+  S->key = key;
+  pq::FileMeta fm = pq::parse_footer(F, size);
+  if (fm.schema.empty()) throw PlanError(LK_ERR_IO, "parquet: empty schema");
+  for (size_t i = 1; i < fm.schema.size(); i++) {
+    const auto& e = fm.schema[i];
+    if (e.num_children > 0 || e.type < 0) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: nested schema");
+    if (e.repetition == pq::REPEATED) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: repeated column " + e.name);
+    S->all_columns.insert(e.name);
+    HostCol c;
+    c.name = e.name;
+    c.ptype = e.type;
+    c.nullable = e.repetition == pq::OPTIONAL;
+    c.is_string = e.type == pq::BYTE_ARRAY;
+    S->by_name[c.name] = int(S->cols.size());
+    S->cols.push_back(std::move(c));
+  }
+  S->num_rows = fm.num_rows;
+  for (auto& g : fm.row_groups) {
+    if (g.columns.size() != S->cols.size()) throw PlanError(LK_ERR_IO, "parquet: row group column count mismatch");
+    S->rg_rows.push_back(g.num_rows);
+  }
+  Builder B{*this, F, size, *S, {}, {}};
+  B.pages.resize(S->cols.size());
+  B.stage.reserve(size);
+  for (uint32_t rg = 0; rg < fm.row_groups.size(); rg++) {
+    for (size_t ci = 0; ci < S->cols.size(); ci++) {
+      HostCol& col = S->cols[ci];
+      // only the physical types the kernels decode are loaded; others stay "absent" for queries
+      bool supported = col.is_string || col.ptype == pq::INT64 || col.ptype == pq::DOUBLE;
+      if (!supported) continue;
+      load_column_chunk(B, int(ci), rg, fm.row_groups[rg].columns[ci]);
+    }
+  }
+  // drop columns of unsupported types from the index
+  for (size_t ci = 0; ci < S->cols.size(); ci++) {
+    HostCol& col = S->cols[ci];
+    if (!(col.is_string || col.ptype == pq::INT64 || col.ptype == pq::DOUBLE)) col.unsupported = true;
+  }
+  // unsupported columns still need page lists for tile building: give them none and skip in build_tiles
+  {
+    std::vector<HostCol> kept;
+    std::vector<std::vector<HostPage>> kept_pages;
+    S->by_name.clear();
+    for (size_t ci = 0; ci < S->cols.size(); ci++) {
+      if (S->cols[ci].unsupported) continue;
+      S->by_name[S->cols[ci].name] = int(kept.size());
+      kept.push_back(std::move(S->cols[ci]));
+      kept_pages.push_back(std::move(B.pages[ci]));
+    }
+    S->cols = std::move(kept);
+    B.pages = std::move(kept_pages);
+  }
+  if (S->num_rows > 0 && !S->cols.empty()) build_tiles(B);
+  for (size_t ci = 0; ci < S->cols.size(); ci++) {
+    auto& col = S->cols[ci];
+    for (auto& hp : B.pages[ci]) col.pages.push_back(hp.d);
+  }
+
+  // ---- upload: streams, then one metadata blob per segment ----
+  std::lock_guard<std::mutex> dg(dev_mu);
+  HIP_CHECK(hipSetDevice(device));
+  S->data_bytes = align_up(B.stage.size() + 64);
+  HIP_CHECK(hipMalloc(&S->d_data, S->data_bytes));
+  HIP_CHECK(hipMemcpy(S->d_data, B.stage.data(), B.stage.size(), hipMemcpyHostToDevice));
+  size_t meta = align_up(S->tiles.size() * sizeof(TileDesc));
+  for (auto& c : S->cols) {
+    meta += align_up(c.pages.size() * sizeof(PageDesc)) + align_up(c.runs.size() * sizeof(RunDesc)) +
+            align_up(c.tcols.size() * sizeof(TileCol)) + align_up(c.remap.size() * sizeof(uint32_t));
+  }
+  S->meta_bytes = std::max<size_t>(meta, kAlign);
+  HIP_CHECK(hipMalloc(&S->d_meta, S->meta_bytes));
+  std::vector<uint8_t> blob(S->meta_bytes, 0);
+  size_t off = 0;
+  auto place = [&](const void* src, size_t n) -> size_t {
+    size_t o = off;
+    if (n) memcpy(blob.data() + o, src, n);
+    off += align_up(n);
+    return o;
+  };
+  uint8_t* base = static_cast<uint8_t*>(S->d_meta);
+  S->d_tiles = reinterpret_cast<TileDesc*>(base + place(S->tiles.data(), S->tiles.size() * sizeof(TileDesc)));
+  for (auto& c : S->cols) {
+    c.d_pages = reinterpret_cast<PageDesc*>(base + place(c.pages.data(), c.pages.size() * sizeof(PageDesc)));
+    c.d_runs = reinterpret_cast<RunDesc*>(base + place(c.runs.data(), c.runs.size() * sizeof(RunDesc)));
+    c.d_tcols = reinterpret_cast<TileCol*>(base + place(c.tcols.data(), c.tcols.size() * sizeof(TileCol)));
+    c.d_remap = reinterpret_cast<uint32_t*>(base + place(c.remap.data(), c.remap.size() * sizeof(uint32_t)));
+    c.any_nulls = false;
+    for (auto& p : c.pages) c.any_nulls |= p.has_nulls != 0;
+  }
+  HIP_CHECK(hipMemcpy(S->d_meta, blob.data(), off, hipMemcpyHostToDevice));
+  // host copies no longer needed except what the planner reads
+  for (auto& c : S->cols) {
+    std::vector<RunDesc>().swap(c.runs);
+    std::vector<TileCol>().swap(c.tcols);
+    std::vector<uint32_t>().swap(c.remap);
+  }
+  return S;
+}
+
+int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size) {
+  auto S = build_segment(key, data, size);
+  std::lock_guard<std::mutex> g(cache_mu);
+  auto it = cache.find(key);
+  if (it != cache.end()) cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
+  cache_bytes += S->data_bytes + S->meta_bytes;
+  cache[key] = S;
+  return LK_OK;
+}
+
+std::shared_ptr<Segment> Engine::get_segment(const std::string& key, bool load_on_miss) {
+  {
+    std::lock_guard<std::mutex> g(cache_mu);
+    auto it = cache.find(key);
+    if (it != cache.end()) return it->second;
+  }
+  if (!load_on_miss) return nullptr;
+  std::ifstream f(key, std::ios::binary);
+  if (!f) throw PlanError(LK_ERR_IO, "cannot open segment " + key);
+  std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+  put_segment(key, buf.data(), buf.size());
+  std::lock_guard<std::mutex> g(cache_mu);
+  return cache[key];
+}
+
+// ------------------------------------------------------------------------------------------------
+// engine lifecycle + workspace
+// ------------------------------------------------------------------------------------------------
+Engine::Engine(int dev) : device(dev) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw DeviceError("no HIP device available");
+  if (dev < 0 || dev >= n) throw DeviceError("device index out of range");
+  HIP_CHECK(hipSetDevice(device));
+  HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+  HIP_CHECK(hipEventCreate(&ev_scan0));
+  HIP_CHECK(hipEventCreate(&ev_scan1));
+  HIP_CHECK(hipHostMalloc(&pinned, pinned_cap = 1 << 20));
+}
+
+Engine::~Engine() {
+  (void)hipSetDevice(device);
+  cache.clear();
+  for (auto& w : ws)
+    if (w.second.p) (void)hipFree(w.second.p);
+  if (pinned) (void)hipHostFree(pinned);
+  if (ev_scan0) (void)hipEventDestroy(ev_scan0);
+  if (ev_scan1) (void)hipEventDestroy(ev_scan1);
+  if (stream) (void)hipStreamDestroy(stream);
+  comm_destroy();
+}
+
+void* Engine::workspace(const std::string& name, size_t bytes) {
+  auto& w = ws[name];
+  if (w.cap < bytes) {
+    if (w.p) HIP_CHECK(hipFree(w.p));
+    w.cap = align_up(std::max(bytes, w.cap * 3 / 2), 1 << 20);
+    HIP_CHECK(hipMalloc(&w.p, w.cap));
+  }
+  return w.p;
+}
+
+void* Engine::pinned_buf(size_t bytes) {
+  if (pinned_cap < bytes) {
+    HIP_CHECK(hipHostFree(pinned));
+    pinned_cap = align_up(bytes, 1 << 20);
+    HIP_CHECK(hipHostMalloc(&pinned, pinned_cap));
+  }
+  return pinned;
+}
+
+}  // namespace lk

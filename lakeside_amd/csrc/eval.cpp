@@ -1,0 +1,607 @@
+// Query evaluation: PushDownRequest -> per-glob plan -> scan kernel -> (RCCL merge) -> finalize -> rows.
+//
+// Semantics: globs of `glob_size` segments in request order (Commons.scala:361-366);
+// per glob the column union decides nonExistentFields (Commons.scala:214-224) -> literal `false` leaves
+// (BaseExpr.scala:462-464) and dropped groupBys (338-346); a column the SQL references that no file of the
+// glob has is a DuckDB Binder Error -> empty glob (Commons.scala:249-253); window [min startTs, max endTs)
+// (Commons.scala:225-226); step of the glob head (Commons.scala:232); bucket ts - ts % step (logs/traces,
+// BaseExpr.scala:163-165) or raw ts (metrics, 376-394); sum/min/max/count ignore NULL values, a group whose
+// values are all NULL reads back 0.0 (Commons.scala:427); tags drop NULL/"null"/"" (Commons.scala:433) and
+// fall back to the glob head's queryTags (450-452).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <climits>
+#include <cmath>
+#include <cstring>
+#include <regex>
+#include <string>
+#include <vector>
+
+#include "../../include/lakeside_gpu.h"
+#include "comm.hpp"
+#include "engine.hpp"
+#include "kernels.hpp"
+#include "layout.hpp"
+#include "plan.hpp"
+
+namespace lk {
+
+#define HIP_TRY(x)                                                                              \
+  do {                                                                                          \
+    hipError_t _e = (x);                                                                        \
+    if (_e != hipSuccess)                                                                       \
+      throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+namespace {
+
+struct LeafInfo {
+  const FilterNode* node;
+  int str;      // string column index
+  int index;    // global leaf index
+};
+
+struct StrCol {
+  std::string name;
+  std::vector<const FilterNode*> leaves;
+  bool is_dim = false;
+  bool restricted = false;
+  std::vector<std::string> cand;          // restricted dims: candidate values (dim id = position)
+  uint32_t ndim = 1;
+  uint32_t dim_null = 0;
+  uint64_t stride = 0;
+  uint32_t lbase = 0, lmask = 0, hmask = 0;
+  uint32_t dict_n = 0;                    // snapshot of the global dictionary size
+  std::vector<int> dim_of_cand_null;      // restricted: candidate positions that collapse to absent
+};
+
+struct GlobInfo {
+  std::vector<int> segs;                  // request indices
+  bool skip = false;                      // Binder-error glob or no segments here
+  uint32_t leaf_false = 0;
+  int64_t win_lo = 0, win_hi = 0;
+  int64_t step = 0;
+  std::vector<std::pair<std::string, std::string>> query_tags;   // glob head's queryTags
+};
+
+bool leaf_eval(const FilterNode& f, const std::string& s, const std::regex* re) {
+  const std::string& op = f.op;
+  if (op == "eq") return s == f.v[0];
+  if (op == "!=") return s != f.v[0];
+  if (op == "in") return std::find(f.v.begin(), f.v.end(), s) != f.v.end();
+  if (op == "not_in") return std::find(f.v.begin(), f.v.end(), s) == f.v.end();
+  if (op == "has" || op == "exists") return true;
+  if (op == "regex" || op == "contains") return std::regex_search(s, *re);
+  throw PlanError(LK_ERR_UNSUPPORTED, "operator " + op);
+}
+
+void postfix(const FilterNode* n, const std::vector<LeafInfo>& leaves, std::vector<uint8_t>& prog) {
+  switch (n->kind) {
+    case FilterNode::LEAF:
+      for (auto& l : leaves)
+        if (l.node == n) { prog.push_back(uint8_t(l.index)); return; }
+      throw PlanError(LK_ERR_ARG, "internal: leaf not numbered");
+    case FilterNode::AND:
+    case FilterNode::OR:
+      postfix(n->a.get(), leaves, prog);
+      postfix(n->b.get(), leaves, prog);
+      prog.push_back(n->kind == FilterNode::AND ? OP_AND : OP_OR);
+      return;
+    case FilterNode::NOT:
+      postfix(n->a.get(), leaves, prog);
+      prog.push_back(OP_NOT);
+      return;
+  }
+}
+
+void collect_leaves(const FilterNode* n, std::vector<const FilterNode*>& out) {
+  if (n->kind == FilterNode::LEAF) out.push_back(n);
+  else {
+    collect_leaves(n->a.get(), out);
+    if (n->b) collect_leaves(n->b.get(), out);
+  }
+}
+
+bool null_like(const std::string& s) { return s.empty() || s == "null"; }
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
+             unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
+  auto t_start = std::chrono::steady_clock::now();
+  Request R = parse_request(json);
+  const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
+  if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
+  if (glob_size <= 0) glob_size = 10;
+  if (n_paths != R.segments.size()) throw PlanError(LK_ERR_ARG, "paths must match segmentRequests");
+
+  // ---- shape gate ----
+  if (R.is_tag_query || !R.has_chart) throw PlanError(LK_ERR_UNSUPPORTED, "tag / exemplar queries are not on the hot path");
+  if (R.field_chart || R.has_extract || R.has_compute)
+    throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute / field charts are not on the hot path");
+  if (R.dataset != "logs" && R.dataset != "traces" && R.dataset != "metrics")
+    throw PlanError(LK_ERR_ARG, "Invalid dataset: " + R.dataset);
+  int agg;
+  if (R.aggregation == "sum") agg = AGG_SUM;
+  else if (R.aggregation == "min") agg = AGG_MIN;
+  else if (R.aggregation == "max") agg = AGG_MAX;
+  else if (R.aggregation == "count") agg = AGG_COUNT;
+  else if (R.aggregation == "avg") agg = AGG_AVG;
+  else throw PlanError(LK_ERR_UNSUPPORTED, "aggregation " + R.aggregation + " (sketch path) is not on the hot path");
+  if (agg == AGG_AVG && !per_glob_rows)
+    throw PlanError(LK_ERR_UNSUPPORTED, "avg is split into sum+count before the merge (QueryEngineV2.scala:280-283)");
+  if (dist && per_glob_rows) throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
+  const bool metrics = R.dataset == "metrics";
+  const std::string vcol = value_column(R);
+
+  std::vector<const FilterNode*> all_leaves;
+  collect_leaves(R.filter.get(), all_leaves);
+  for (auto* l : all_leaves) {
+    if (l->extracted || l->computed) throw PlanError(LK_ERR_UNSUPPORTED, "extracted/computed filter fields");
+    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
+    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; })) {
+      if (l->op == "gt" || l->op == "ge" || l->op == "lt" || l->op == "le")
+        throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves are not on the hot path yet");
+      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
+    }
+  }
+
+  // no segments: the worker answers one sentinel row (Commons.scala:393-396)
+  if (R.segments.empty()) {
+    if (per_glob_rows) {
+      res->ts.push_back(-1);
+      res->val.push_back(-1.0);
+      res->glob.push_back(0);
+    }
+    res->stats = "{\"scan_ms\":0,\"total_ms\":0,\"rows_scanned\":0,\"algorithmic_bytes\":0,\"tiles\":0,\"cells\":0}";
+    return LK_OK;
+  }
+
+  // ---- string columns: name first, then leaf keys, then groupBys ----
+  std::vector<StrCol> strs;
+  auto str_index = [&](const std::string& name) -> int {
+    for (size_t i = 0; i < strs.size(); i++)
+      if (strs[i].name == name) return int(i);
+    strs.push_back(StrCol{});
+    strs.back().name = name;
+    return int(strs.size() - 1);
+  };
+  str_index(kName);
+  for (auto* l : all_leaves) strs[str_index(l->k)].leaves.push_back(l);
+  std::vector<std::string> gbs;
+  for (auto& g : R.group_bys)
+    if (std::find(gbs.begin(), gbs.end(), g) == gbs.end()) gbs.push_back(g);
+  for (auto& g : gbs) str_index(g);
+  if (strs.size() > size_t(MAXSTR)) throw PlanError(LK_ERR_UNSUPPORTED, "too many string columns in one query");
+  if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
+  if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& s) { return s.name == kTimestamp || s.name == vcol; }) != strs.end())
+    throw PlanError(LK_ERR_UNSUPPORTED, "filters / groupBys on the timestamp or value column");
+  std::vector<LeafInfo> leaves;
+  for (size_t s = 0; s < strs.size(); s++) {
+    StrCol& sc = strs[s];
+    if (sc.leaves.size() > size_t(LEAF_BITS)) throw PlanError(LK_ERR_UNSUPPORTED, "too many leaves on one column");
+    sc.lbase = uint32_t(leaves.size());
+    for (size_t j = 0; j < sc.leaves.size(); j++) {
+      uint32_t idx = uint32_t(leaves.size());
+      leaves.push_back(LeafInfo{sc.leaves[j], int(s), int(idx)});
+      sc.lmask |= 1u << idx;
+      if (sc.leaves[j]->op == "has" || sc.leaves[j]->op == "exists") sc.hmask |= 1u << idx;
+    }
+  }
+  std::vector<uint8_t> prog;
+  postfix(R.filter.get(), leaves, prog);
+  if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
+
+  // ---- segments: which ones this process evaluates ----
+  const int world = dist ? comm_world(E) : 1;
+  const int rank = dist ? comm_rank(E) : 0;
+  std::vector<char> mine(n_paths, 1);
+  if (dist)
+    for (size_t i = 0; i < n_paths; i++) mine[i] = (shard ? shard[i] : int32_t(i % size_t(world))) == rank;
+  std::vector<std::shared_ptr<Segment>> segs(n_paths);
+  for (size_t i = 0; i < n_paths; i++)
+    if (mine[i]) segs[i] = E.get_segment(paths[i], true);
+
+  // ---- globs ----
+  const std::set<std::string> fset = field_set(R);
+  std::vector<std::string> probe_cols(fset.begin(), fset.end());   // columns whose existence matters
+  for (auto& k : std::vector<std::string>{kTimestamp, kName, vcol})
+    if (std::find(probe_cols.begin(), probe_cols.end(), k) == probe_cols.end()) probe_cols.push_back(k);
+  for (auto* l : all_leaves)
+    if (std::find(probe_cols.begin(), probe_cols.end(), l->k) == probe_cols.end()) probe_cols.push_back(l->k);
+  std::vector<GlobInfo> globs;
+  for (size_t i = 0; i < n_paths; i += size_t(glob_size)) {
+    GlobInfo g;
+    for (size_t j = i; j < std::min(n_paths, i + size_t(glob_size)); j++) g.segs.push_back(int(j));
+    globs.push_back(std::move(g));
+  }
+  // union of columns per glob (over the probe columns), and "value column may be NULL"
+  const size_t np = probe_cols.size();
+  std::vector<uint8_t> exists(globs.size() * np + 1, 0);
+  for (size_t gi = 0; gi < globs.size(); gi++)
+    for (int si : globs[gi].segs) {
+      if (!segs[si]) continue;
+      for (size_t k = 0; k < np; k++)
+        if (segs[si]->all_columns.count(probe_cols[k])) exists[gi * np + k] = 1;
+      int vc = segs[si]->col_index(vcol);
+      if (vc < 0 || segs[si]->cols[vc].any_nulls || segs[si]->cols[vc].nullable) exists.back() = 1;
+    }
+  if (dist) comm_allreduce_max_u8(E, exists.data(), exists.size());   // every rank sees every glob's union
+  const bool value_nulls = exists.back() != 0;
+  auto glob_has = [&](size_t gi, const std::string& c) {
+    size_t k = size_t(std::find(probe_cols.begin(), probe_cols.end(), c) - probe_cols.begin());
+    return exists[gi * np + k] != 0;
+  };
+  int64_t step = -1;
+  for (size_t gi = 0; gi < globs.size(); gi++) {
+    GlobInfo& g = globs[gi];
+    const SegmentReq& head = R.segments[g.segs[0]];
+    g.step = head.step;
+    g.query_tags = head.query_tags;
+    g.win_lo = INT64_MAX;
+    g.win_hi = INT64_MIN;
+    for (int si : g.segs) {
+      g.win_lo = std::min(g.win_lo, R.segments[si].start_ts);
+      g.win_hi = std::max(g.win_hi, R.segments[si].end_ts);
+    }
+    // nonExistentFields (Commons.scala:224) -> leaves compiled to `false`
+    std::set<std::string> nonexist;
+    for (auto& f : fset)
+      if (!glob_has(gi, f)) nonexist.insert(f);
+    for (auto& l : leaves)
+      if (nonexist.count(l.node->k)) g.leaf_false |= 1u << l.index;
+    // Binder Error: referenced column absent from the whole glob
+    if (!glob_has(gi, kTimestamp) || !glob_has(gi, kName) || !glob_has(gi, vcol)) g.skip = true;
+    for (auto& l : leaves)
+      if (!nonexist.count(l.node->k) && !glob_has(gi, l.node->k)) g.skip = true;
+    if (g.step <= 0) throw PlanError(LK_ERR_ARG, "stepInMillis must be positive");
+    if (step < 0) step = g.step;
+    else if (g.step != step) throw PlanError(LK_ERR_UNSUPPORTED, "globs with different steps");
+  }
+
+  // ---- group dimensions ----
+  const bool merged = !per_glob_rows;
+  for (size_t s = 0; s < strs.size(); s++) {
+    StrCol& sc = strs[s];
+    sc.is_dim = (s == 0) || std::find(gbs.begin(), gbs.end(), sc.name) != gbs.end();
+    GlobalDict& gd = E.dict(sc.name);
+    {
+      std::lock_guard<std::mutex> g(gd.mu);
+      sc.dict_n = uint32_t(gd.vals.size());
+    }
+    if (!sc.is_dim) continue;
+    if (restricted_values(R.filter.get(), sc.name, sc.cand)) {
+      sc.restricted = true;
+      sc.ndim = uint32_t(sc.cand.size()) + 1;     // + absent
+      sc.dim_null = uint32_t(sc.cand.size());
+    } else {
+      if (dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed group-by over an unrestricted column (round 1)");
+      if (sc.dict_n + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
+      sc.ndim = sc.dict_n + 1;
+      sc.dim_null = sc.dict_n;
+    }
+  }
+  uint64_t ngroups = 1;
+  for (int s = int(strs.size()) - 1; s >= 0; s--) {
+    if (!strs[s].is_dim) continue;
+    strs[s].stride = ngroups;
+    ngroups *= strs[s].ndim;
+    if (ngroups > (1ull << 40)) throw PlanError(LK_ERR_UNSUPPORTED, "group space too large");
+  }
+
+  // ---- lookup tables: global id -> leaf bits << 24 | dim id ----
+  std::vector<std::vector<uint32_t>> tabs(strs.size());
+  std::vector<char> need_tab(strs.size(), 0);
+  for (size_t s = 0; s < strs.size(); s++) {
+    StrCol& sc = strs[s];
+    GlobalDict& gd = E.dict(sc.name);
+    std::lock_guard<std::mutex> g(gd.mu);
+    bool null_like_present = gd.ids.count("null") || gd.ids.count("");
+    need_tab[s] = !sc.leaves.empty() || sc.restricted || (sc.is_dim && merged && null_like_present) ||
+                  (!sc.is_dim && sc.leaves.empty());
+    if (!need_tab[s]) continue;
+    std::vector<std::regex> res(sc.leaves.size());
+    for (size_t j = 0; j < sc.leaves.size(); j++) {
+      const FilterNode* l = sc.leaves[j];
+      if (l->op == "regex" || l->op == "contains") {
+        std::string pat = l->op == "contains" ? ".*" + l->v[0] + ".*" : l->v[0];
+        try {
+          res[j] = std::regex(pat, std::regex::ECMAScript | std::regex::icase | std::regex::optimize);
+        } catch (const std::regex_error& e) {
+          throw PlanError(LK_ERR_UNSUPPORTED, "regex '" + pat + "': " + e.what());
+        }
+      }
+    }
+    auto& tab = tabs[s];
+    tab.resize(std::max<uint32_t>(sc.dict_n, 1));
+    for (uint32_t gid = 0; gid < sc.dict_n; gid++) {
+      const std::string& v = gd.vals[gid];
+      uint32_t bits = 0;
+      for (size_t j = 0; j < sc.leaves.size(); j++)
+        if (leaf_eval(*sc.leaves[j], v, &res[j])) bits |= 1u << j;
+      uint32_t dim = 0;
+      if (sc.is_dim) {
+        if (sc.restricted) {
+          auto it = std::find(sc.cand.begin(), sc.cand.end(), v);
+          dim = it == sc.cand.end() ? sc.dim_null : uint32_t(it - sc.cand.begin());
+          if (merged && null_like(v)) dim = sc.dim_null;
+        } else {
+          dim = (merged && null_like(v)) ? sc.dim_null : gid;
+        }
+      }
+      tab[gid] = (bits << 24) | dim;
+    }
+  }
+
+  // ---- bucket space ----
+  int64_t min_lo = INT64_MAX, max_hi = INT64_MIN;
+  for (auto& g : globs) {
+    if (g.skip) continue;
+    min_lo = std::min(min_lo, g.win_lo);
+    max_hi = std::max(max_hi, g.win_hi);
+  }
+  int64_t bucket_base = 0;
+  uint64_t nbuckets = 0;
+  if (min_lo < max_hi) {
+    if (metrics) bucket_base = min_lo;
+    else bucket_base = min_lo - min_lo % step;
+    int64_t last = max_hi - 1;
+    int64_t last_b = metrics ? last : last - last % step;
+    nbuckets = uint64_t((last_b - bucket_base) / step + 1);
+  }
+  const bool per_glob_cells = per_glob_rows || ((agg == AGG_MIN || agg == AGG_MAX) && value_nulls);
+  const uint32_t nslots = per_glob_cells ? uint32_t(globs.size()) : 1u;
+  const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
+  if (ncells > (1ull << 28)) throw PlanError(LK_ERR_UNSUPPORTED, "aggregation table too large (" + std::to_string(ncells) + " cells)");
+
+  // ---- per-segment query descriptors ----
+  std::vector<QSeg> qsegs;
+  std::vector<uint32_t> seg_begin;
+  uint32_t total_tiles = 0;
+  uint64_t rows_scanned = 0, alg_bytes = 0;
+  for (size_t gi = 0; gi < globs.size() && nbuckets; gi++) {
+    const GlobInfo& g = globs[gi];
+    if (g.skip) continue;
+    for (int si : g.segs) {
+      if (!segs[si]) continue;
+      const Segment& S = *segs[si];
+      rows_scanned += uint64_t(S.num_rows);
+      QSeg q{};
+      q.base = S.d_data;
+      q.tiles = S.d_tiles;
+      q.ntiles = uint32_t(S.tiles.size());
+      q.glob_slot = per_glob_cells ? uint32_t(gi) : 0;
+      q.leaf_false = g.leaf_false;
+      q.win_lo = g.win_lo;
+      q.win_hi = g.win_hi;
+      auto bind = [&](int qc, const std::string& name, bool want_string) {
+        int c = S.col_index(name);
+        if (c < 0) {
+          if (S.all_columns.count(name))
+            throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has a physical type the kernels do not decode");
+          return;
+        }
+        const HostCol& hc = S.cols[c];
+        if (want_string != hc.is_string)
+          throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
+        if (qc == 0 && hc.ptype != 2) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
+        if (qc == 1 && hc.ptype != 5) throw PlanError(LK_ERR_UNSUPPORTED, "value column must be DOUBLE");
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
+        alg_bytes += hc.compressed_bytes;
+      };
+      bind(0, kTimestamp, false);
+      if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
+      bind(1, vcol, false);
+      for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      q.tile_begin = total_tiles;
+      seg_begin.push_back(total_tiles);
+      total_tiles += q.ntiles;
+      qsegs.push_back(q);
+    }
+  }
+
+  // ---- device: upload, zero table, scan ----
+  std::lock_guard<std::mutex> dev_guard(E.dev_mu);
+  HIP_TRY(hipSetDevice(E.device));
+  hipStream_t st = E.stream;
+  QParams P{};
+  P.nsegs = uint32_t(qsegs.size());
+  P.total_tiles = total_tiles;
+  P.nstr = uint32_t(strs.size());
+  P.nleaves = uint32_t(leaves.size());
+  P.nprog = uint32_t(prog.size());
+  P.metrics = metrics ? 1 : 0;
+  P.step = step > 0 ? step : 1;
+  P.bucket_base = bucket_base;
+  P.nbuckets = nbuckets;
+  P.ngroups = ngroups;
+  P.ncells = ncells;
+  for (size_t s = 0; s < strs.size(); s++) {
+    P.dim_null[s] = strs[s].dim_null;
+    P.dim_stride[s] = strs[s].is_dim ? strs[s].stride : 0;
+    P.str_lbase[s] = strs[s].lbase;
+    P.str_lmask[s] = strs[s].lmask;
+    P.str_hmask[s] = strs[s].hmask;
+  }
+  memcpy(P.prog, prog.data(), prog.size());
+
+  // staging layout in one pinned buffer + one device workspace
+  size_t off = 0;
+  auto reserve = [&](size_t n) { size_t o = (off + 255) / 256 * 256; off = o + n; return o; };
+  const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
+  const size_t o_begin = reserve(seg_begin.size() * sizeof(uint32_t));
+  std::vector<size_t> o_tab(strs.size());
+  for (size_t s = 0; s < strs.size(); s++) o_tab[s] = need_tab[s] ? reserve(tabs[s].size() * 4) : 0;
+  const size_t o_flags = reserve(sizeof(uint32_t) * 4);
+  std::vector<uint32_t> name_rank;
+  const bool collapse = merged && gbs.empty();
+  if (collapse && strs[0].is_dim) {
+    // "tags of the first input" (TimeGroupedSketchAggregator.scala:57-60) is arrival-order dependent in the
+    // reference; we pick the smallest name string among the merged cells, deterministically.
+    std::vector<std::pair<std::string, uint32_t>> order;
+    GlobalDict& gd = E.dict(kName);
+    std::lock_guard<std::mutex> g(gd.mu);
+    for (uint32_t d = 0; d < strs[0].ndim; d++) {
+      std::string v = d == strs[0].dim_null ? std::string("\xff\xff") :
+                      (strs[0].restricted ? strs[0].cand[d] : gd.vals[d]);
+      order.emplace_back(v, d);
+    }
+    std::sort(order.begin(), order.end());
+    name_rank.assign(strs[0].ndim, 0);
+    for (uint32_t r = 0; r < order.size(); r++) name_rank[order[r].second] = r;
+  }
+  const size_t o_rank = reserve(name_rank.size() * 4);
+  const size_t stage_bytes = off;
+  uint8_t* hbuf = static_cast<uint8_t*>(E.pinned_buf(stage_bytes));
+  uint8_t* dbuf = static_cast<uint8_t*>(E.workspace("query", stage_bytes));
+  for (auto& q : qsegs) (void)q;
+  memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
+  memcpy(hbuf + o_begin, seg_begin.data(), seg_begin.size() * sizeof(uint32_t));
+  for (size_t s = 0; s < strs.size(); s++)
+    if (need_tab[s]) {
+      memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
+      P.strtab[s] = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
+    }
+  memset(hbuf + o_flags, 0, 16);
+  if (!name_rank.empty()) memcpy(hbuf + o_rank, name_rank.data(), name_rank.size() * 4);
+  HIP_TRY(hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st));
+  P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
+  P.flags = reinterpret_cast<uint32_t*>(dbuf + o_flags);
+  const uint32_t* d_seg_begin = reinterpret_cast<const uint32_t*>(dbuf + o_begin);
+
+  // aggregation table (SoA)
+  const size_t nc = size_t(std::max<uint64_t>(ncells, 1));
+  uint8_t* tb = static_cast<uint8_t*>(E.workspace("table", nc * 8 * 5 + 4 * 256));
+  P.rows = reinterpret_cast<unsigned long long*>(tb);
+  P.cnt = reinterpret_cast<unsigned long long*>(tb + nc * 8);
+  P.hi = reinterpret_cast<double*>(tb + nc * 16);
+  P.lo = reinterpret_cast<double*>(tb + nc * 24);
+  P.ext = reinterpret_cast<unsigned long long*>(tb + nc * 32);
+  const int kagg = agg == AGG_AVG ? AGG_SUM : agg;
+  HIP_TRY(hipMemsetAsync(tb, 0, nc * 16, st));
+  if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + nc * 16, 0, nc * 16, st));
+  if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, nc * 8, st));
+  if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, nc * 8, st));
+  HIP_TRY(hipEventRecord(E.ev_scan0, st));
+  if (ncells) HIP_TRY(launch_scan(P, d_seg_begin, kagg, st));
+  HIP_TRY(hipEventRecord(E.ev_scan1, st));
+
+  // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
+  if (dist) comm_reduce_table(E, P, kagg, nc);
+  const bool emit = !dist || rank == 0;
+
+  // ---- finalize + compaction ----
+  FParams F{};
+  F.rows = P.rows;
+  F.cnt = P.cnt;
+  F.hi = P.hi;
+  F.lo = P.lo;
+  F.ext = P.ext;
+  F.ngroups = ngroups;
+  F.nbuckets = nbuckets;
+  F.nglob_slots = nslots;
+  F.agg = agg;
+  F.per_glob = per_glob_rows ? 1 : 0;
+  F.collapse = collapse ? 1 : 0;
+  F.name_stride = strs[0].stride ? strs[0].stride : 1;
+  F.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
+  F.bucket_base = bucket_base;
+  F.step = P.step;
+  F.nkeys = ncells == 0 ? 0 : (per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups));
+  uint32_t nfb = finalize_blocks(F.nkeys);
+  const size_t nk = size_t(std::max<uint64_t>(F.nkeys, 1));
+  uint8_t* ob = static_cast<uint8_t*>(E.workspace("out", nk * (8 + 8 + 8 + 4) + (nfb + 1) * 4 + 1024));
+  int64_t* d_ts = reinterpret_cast<int64_t*>(ob);
+  double* d_val = reinterpret_cast<double*>(ob + nk * 8);
+  unsigned long long* d_gid = reinterpret_cast<unsigned long long*>(ob + nk * 16);
+  uint32_t* d_glob = reinterpret_cast<uint32_t*>(ob + nk * 24);
+  uint32_t* d_counts = reinterpret_cast<uint32_t*>(ob + nk * 28);
+  uint32_t nrows_out = 0;
+  uint32_t hflags = 0;
+  if (emit && F.nkeys) {
+    HIP_TRY(launch_finalize(F, d_counts, d_ts, d_val, d_gid, d_glob, st));
+    HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipMemcpyAsync(&hflags, P.flags, 4, hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  if (hflags & FLAG_METRICS_UNALIGNED)
+    throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
+  if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
+  std::vector<unsigned long long> gid(nrows_out);
+  res->ts.resize(nrows_out);
+  res->val.resize(nrows_out);
+  res->glob.resize(nrows_out);
+  if (nrows_out) {
+    HIP_TRY(hipMemcpyAsync(res->ts.data(), d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->val.data(), d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(gid.data(), d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->glob.data(), d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+  }
+  float scan_ms = 0;
+  HIP_TRY(hipEventElapsedTime(&scan_ms, E.ev_scan0, E.ev_scan1));
+
+  // ---- tags: "name", groupBys (as written), then queryTags keys (rows whose own tags are all absent) ----
+  std::vector<int> col_str;   // tag column -> string column index
+  res->tag_names.push_back("name");
+  col_str.push_back(0);
+  for (auto& g : R.group_bys) {
+    res->tag_names.push_back(g);
+    col_str.push_back(str_index(g));
+  }
+  const size_t nreg = res->tag_names.size();
+  std::vector<std::string> qt_keys;
+  for (auto& g : globs)
+    for (auto& kv : g.query_tags)
+      if (std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
+  for (auto& k : qt_keys) res->tag_names.push_back(k);
+  const size_t ncol = res->tag_names.size();
+  res->tag_vals.assign(size_t(nrows_out) * ncol, nullptr);
+  std::vector<GlobalDict*> gds(strs.size());
+  std::vector<std::unique_lock<std::mutex>> locks;
+  for (size_t s = 0; s < strs.size(); s++) {
+    gds[s] = &E.dict(strs[s].name);
+    locks.emplace_back(gds[s]->mu);
+  }
+  for (uint32_t r = 0; r < nrows_out; r++) {
+    bool any = false;
+    for (size_t c = 0; c < nreg; c++) {
+      const StrCol& sc = strs[col_str[c]];
+      uint32_t d = uint32_t((gid[r] / sc.stride) % sc.ndim);
+      const std::string* v = nullptr;
+      if (d != sc.dim_null) v = sc.restricted ? &sc.cand[d] : &gds[col_str[c]]->vals[d];
+      if (v && !null_like(*v)) {
+        if (sc.restricted) {
+          res->owned.push_back(*v);
+          v = &res->owned.back();
+        }
+        res->tag_vals[size_t(r) * ncol + c] = v->c_str();
+        any = true;
+      }
+    }
+    if (!any) {   // Commons.scala:450-452: empty tags -> the glob head's queryTags
+      const GlobInfo& g = globs[per_glob_rows ? res->glob[r] : 0];
+      for (auto& kv : g.query_tags) {
+        size_t c = nreg + size_t(std::find(qt_keys.begin(), qt_keys.end(), kv.first) - qt_keys.begin());
+        res->owned.push_back(kv.second);
+        res->tag_vals[size_t(r) * ncol + c] = res->owned.back().c_str();
+      }
+    }
+  }
+  char buf[512];
+  snprintf(buf, sizeof(buf),
+           "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"rows_scanned\":%llu,\"algorithmic_bytes\":%llu,\"tiles\":%u,"
+           "\"cells\":%llu,\"segments\":%zu}",
+           double(scan_ms), ms_since(t_start), (unsigned long long)rows_scanned, (unsigned long long)alg_bytes,
+           total_tiles, (unsigned long long)ncells, qsegs.size());
+  res->stats = buf;
+  return LK_OK;
+}
+
+}  // namespace lk

@@ -1,0 +1,39 @@
+// Host-visible interface of the HIP kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "layout.hpp"
+
+namespace lk {
+
+struct FParams {
+  const unsigned long long* rows;
+  const unsigned long long* cnt;
+  const double* hi;
+  const double* lo;
+  const unsigned long long* ext;
+  unsigned long long nkeys;        // output key space
+  unsigned long long ngroups;
+  unsigned long long nbuckets;
+  unsigned long long name_stride;  // group-id stride of the name dimension (most significant)
+  const uint32_t* name_rank;       // name dim id -> rank in string order (merged + collapse), or null
+  uint32_t nglob_slots;
+  int agg;                         // Agg, or 4 = avg
+  int per_glob;                    // 1: one output row per (glob, bucket, group) cell
+  int collapse;                    // merged without groupBys: one row per bucket (S19)
+  int64_t bucket_base;
+  int64_t step;
+};
+
+constexpr int AGG_AVG = 4;
+
+hipError_t launch_merge_dd(double* hi, double* lo, const double* parts, int world, size_t nc, hipStream_t stream);
+hipError_t launch_scan(const QParams& P, const uint32_t* d_seg_begin, int agg, hipStream_t stream);
+uint32_t finalize_blocks(unsigned long long nkeys);
+// d_counts must hold finalize_blocks(nkeys) + 1 entries; the row total lands in d_counts[nblocks].
+hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
+                           uint32_t* glob, hipStream_t stream);
+
+}  // namespace lk

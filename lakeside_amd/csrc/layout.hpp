@@ -1,0 +1,130 @@
+// Data layout shared by the host engine and the HIP kernels.
+//
+// HBM-resident segment (loaded once, reused by every query; the worker's disk cache becomes an HBM cache):
+//   bytes    : the sealed Parquet file, verbatim (page headers included, never read by the GPU)
+//   pages    : one PageDesc per data page of every column chunk (where its value / def-level streams start)
+//   runs     : RunDesc per run of every hybrid RLE/bit-packed stream (dictionary indices, def levels)
+//   tiles    : TileDesc per tile = a row range inside one row group and inside one page of every column,
+//              small enough that each column's runs over the tile fit the kernel's LDS staging (RUN_CAP)
+//   tcols    : TileCol per (column, tile): the page and the run windows of that column over the tile
+//   remap    : per dictionary-encoded column chunk, local dictionary index -> engine-global value id
+//
+// Per query the host uploads one QSeg per segment (which columns the query reads, the glob it belongs to,
+// forced-false leaves) and, per string column, a table global id -> (leaf bits << 24 | group-dim id).
+#pragma once
+#include <cstdint>
+
+namespace lk {
+
+constexpr int MAXQCOL = 8;      // query columns: 0 = timestamp, 1 = aggregated value, 2.. = string columns
+constexpr int MAXSTR = 6;       // string columns per query (name + filter keys + groupBys)
+constexpr int MAXLEAF = 16;     // filter leaves
+constexpr int MAXPROG = 48;     // postfix filter program length
+constexpr int LEAF_BITS = 8;    // leaf bits per string column in the packed lookup value
+constexpr uint32_t DIM_MASK = 0x00ffffffu;   // group-dim id bits of the packed lookup value
+constexpr uint32_t TILE_ROWS = 65536;        // max rows per tile
+constexpr uint32_t RUN_CAP = 64;             // max runs of one stream of one column inside a tile
+
+enum PageKind : uint8_t { PAGE_PLAIN64 = 1, PAGE_DICT = 2 };
+
+struct PageDesc {           // 48 B
+  uint64_t vals;            // byte offset (from segment base) of the value stream: PLAIN data, or dictionary
+                            //   indices' hybrid data (after the bit-width byte)
+  uint64_t defs;            // byte offset of the definition-level hybrid stream (0 if the column is REQUIRED)
+  uint32_t first_row;       // first row of the page within its row group
+  uint32_t nrows;
+  uint32_t nvals;           // non-null values stored in the page
+  uint32_t remap;           // offset (elements) of the chunk's dictionary remap in the segment remap array
+  uint32_t dict_n;          // dictionary size of the chunk
+  uint32_t vals_len;        // bytes of the value stream
+  uint32_t defs_len;        // bytes of the def-level stream
+  uint8_t bw;               // dictionary index bit width
+  uint8_t kind;             // PageKind
+  uint8_t nullable;         // has a def-level stream
+  uint8_t has_nulls;        // at least one NULL row in this page
+};
+
+struct RunDesc {            // 16 B; one run of a hybrid RLE/bit-packed stream
+  uint32_t start;           // first value index (value stream) / row (def stream), relative to the page
+  uint32_t off_lit;         // bit 31: literal (bit-packed) run; bits 0..30: byte offset from stream start
+  uint32_t value;           // RLE run: the repeated value
+  uint32_t count;           // values covered
+};
+
+struct TileDesc {           // 32 B
+  uint32_t rg;              // row group
+  uint32_t row0;            // first row (within the row group)
+  uint32_t nrows;
+  uint32_t pad;
+  int64_t ts_min;           // zone map of the timestamp column over the tile (INT64_MAX/MIN if no value)
+  int64_t ts_max;
+};
+
+struct TileCol {            // 24 B
+  uint32_t page;            // index into the segment's page array
+  uint32_t run_lo;          // first value-stream run overlapping the tile (index into the run array)
+  uint32_t nruns;
+  uint32_t drun_lo;         // first def-stream run overlapping the tile
+  uint32_t ndruns;
+  uint32_t vbase;           // value index (within the page) of the tile's first non-null row
+};
+
+struct QCol {               // one query column in one segment
+  const PageDesc* pages;
+  const RunDesc* runs;
+  const TileCol* tcols;     // per tile
+  const uint32_t* remap;
+  uint32_t present;         // 0: column absent from this segment (all NULL)
+  uint32_t pad;
+};
+
+struct QSeg {
+  const uint8_t* base;
+  const TileDesc* tiles;
+  uint32_t tile_begin;      // prefix sum of tiles over the query's segments
+  uint32_t ntiles;
+  uint32_t glob_slot;       // glob index in the cell space (0 when globs are merged in the table)
+  uint32_t leaf_false;      // leaves compiled to literal `false` for this segment's glob (BaseExpr.scala:462)
+  int64_t win_lo;           // glob window [min startTs, max endTs) (Commons.scala:225-226)
+  int64_t win_hi;
+  QCol cols[MAXQCOL];
+};
+
+enum Agg : int { AGG_SUM = 0, AGG_MIN = 1, AGG_MAX = 2, AGG_COUNT = 3 };
+enum Op : uint8_t { OP_AND = 0x80, OP_OR = 0x81, OP_NOT = 0x82, OP_TRUE = 0x83 };   // < 0x80: push leaf
+
+struct QParams {
+  const QSeg* segs;
+  uint32_t nsegs;
+  uint32_t total_tiles;
+  uint32_t nstr;            // string columns (query cols 2 .. 2+nstr)
+  uint32_t nleaves;
+  uint32_t nprog;
+  int32_t metrics;          // 1: bucket = raw timestamp (BaseExpr.scala:391); 0: ts - ts % step (163-165)
+  int64_t step;
+  int64_t bucket_base;      // step-aligned origin of bucket 0
+  uint64_t nbuckets;
+  uint64_t ngroups;
+  uint64_t ncells;
+  // per string column
+  const uint32_t* strtab[MAXSTR];   // global id -> (leaf bits << 24) | dim id; null: identity dim, no leaves
+  uint32_t dim_null[MAXSTR];        // dim id of NULL / absent
+  uint64_t dim_stride[MAXSTR];      // 0: not a group dimension
+  // leaves: the leaves of string column s are the contiguous leaf indices lbase[s] .. (lmask[s] bits);
+  // bit i of the column's packed leaf bits is leaf lbase[s] + i
+  uint32_t str_lbase[MAXSTR];
+  uint32_t str_lmask[MAXSTR];       // global leaf-index mask of the column's leaves
+  uint32_t str_hmask[MAXSTR];       // of those, `has`/`exists` leaves (IS NOT NULL: FALSE on NULL, never NULL)
+  uint8_t prog[MAXPROG];
+  // aggregation table (structure of arrays, ncells each)
+  unsigned long long* rows;         // rows that passed the filter (cell existence)
+  unsigned long long* cnt;          // non-NULL values
+  double* hi;                       // sum = hi + lo (compensated)
+  double* lo;
+  unsigned long long* ext;          // min/max as order-preserving u64
+  uint32_t* flags;                  // error / diagnostic flags
+};
+
+enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u };
+
+}  // namespace lk

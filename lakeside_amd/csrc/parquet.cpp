@@ -1,0 +1,259 @@
+#include "parquet.hpp"
+
+#include <algorithm>
+#include <cstring>
+#include <stdexcept>
+
+#include "thrift.hpp"
+
+namespace lk {
+namespace pq {
+
+static void parse_schema_element(TReader& r, SchemaElement& e) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 1: e.type = int(r.zigzag()); break;
+      case 3: e.repetition = int(r.zigzag()); break;
+      case 4: e.name = r.binary(); break;
+      case 5: e.num_children = int(r.zigzag()); break;
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+}
+
+static void parse_statistics(TReader& r, ColumnMeta& m) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    if (id == 3) m.null_count = r.zigzag();
+    else r.skip(t);
+  }
+  r.struct_end();
+}
+
+static void parse_column_meta(TReader& r, ColumnMeta& m) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 1: m.type = int(r.zigzag()); break;
+      case 3: {
+        uint8_t et; uint32_t n;
+        r.list_begin(et, n);
+        for (uint32_t i = 0; i < n; i++) m.path.push_back(r.binary());
+        break;
+      }
+      case 4: m.codec = int(r.zigzag()); break;
+      case 5: m.num_values = r.zigzag(); break;
+      case 6: m.total_uncompressed = r.zigzag(); break;
+      case 7: m.total_compressed = r.zigzag(); break;
+      case 9: m.data_page_offset = r.zigzag(); break;
+      case 11: m.dictionary_page_offset = r.zigzag(); break;
+      case 12: parse_statistics(r, m); break;
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+}
+
+static void parse_column_chunk(TReader& r, ColumnMeta& m) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  bool have_meta = false;
+  while (r.field(id, t)) {
+    if (id == 3) { parse_column_meta(r, m); have_meta = true; }
+    else if (id == 1) { r.binary(); throw std::runtime_error("parquet: external column chunks are not supported"); }
+    else r.skip(t);
+  }
+  r.struct_end();
+  if (!have_meta) throw std::runtime_error("parquet: column chunk without meta_data");
+}
+
+static void parse_row_group(TReader& r, RowGroupMeta& g) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    if (id == 1) {
+      uint8_t et; uint32_t n;
+      r.list_begin(et, n);
+      g.columns.resize(n);
+      for (uint32_t i = 0; i < n; i++) parse_column_chunk(r, g.columns[i]);
+    } else if (id == 3) {
+      g.num_rows = r.zigzag();
+    } else {
+      r.skip(t);
+    }
+  }
+  r.struct_end();
+}
+
+FileMeta parse_footer(const uint8_t* file, size_t size) {
+  if (size < 12 || memcmp(file, "PAR1", 4) != 0 || memcmp(file + size - 4, "PAR1", 4) != 0)
+    throw std::runtime_error("parquet: missing PAR1 magic");
+  uint32_t flen;
+  memcpy(&flen, file + size - 8, 4);
+  if (size_t(flen) + 12 > size) throw std::runtime_error("parquet: bad footer length");
+  TReader r(file + size - 8 - flen, flen);
+  FileMeta fm;
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 2: {
+        uint8_t et; uint32_t n;
+        r.list_begin(et, n);
+        fm.schema.resize(n);
+        for (uint32_t i = 0; i < n; i++) parse_schema_element(r, fm.schema[i]);
+        break;
+      }
+      case 3: fm.num_rows = r.zigzag(); break;
+      case 4: {
+        uint8_t et; uint32_t n;
+        r.list_begin(et, n);
+        fm.row_groups.resize(n);
+        for (uint32_t i = 0; i < n; i++) parse_row_group(r, fm.row_groups[i]);
+        break;
+      }
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+  return fm;
+}
+
+static void parse_data_page_header(TReader& r, PageHeader& h) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 1: h.num_values = int32_t(r.zigzag()); break;
+      case 2: h.encoding = int(r.zigzag()); break;
+      case 3: h.def_encoding = int(r.zigzag()); break;
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+}
+
+static void parse_data_page_header_v2(TReader& r, PageHeader& h) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 1: h.num_values = int32_t(r.zigzag()); break;
+      case 2: h.num_nulls = int32_t(r.zigzag()); break;
+      case 3: h.num_rows = int32_t(r.zigzag()); break;
+      case 4: h.encoding = int(r.zigzag()); break;
+      case 5: h.def_len = int32_t(r.zigzag()); break;
+      case 6: h.rep_len = int32_t(r.zigzag()); break;
+      case 7: h.v2_compressed = r.bool_val(t); break;
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+}
+
+static void parse_dictionary_page_header(TReader& r, PageHeader& h) {
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    if (id == 1) h.dict_num_values = int32_t(r.zigzag());
+    else if (id == 2) h.encoding = int(r.zigzag());
+    else r.skip(t);
+  }
+  r.struct_end();
+}
+
+PageHeader parse_page_header(const uint8_t* p, size_t n) {
+  TReader r(p, n);
+  PageHeader h;
+  r.struct_begin();
+  int16_t id; uint8_t t;
+  while (r.field(id, t)) {
+    switch (id) {
+      case 1: h.type = int(r.zigzag()); break;
+      case 2: h.uncompressed = int32_t(r.zigzag()); break;
+      case 3: h.compressed = int32_t(r.zigzag()); break;
+      case 5: parse_data_page_header(r, h); break;
+      case 7: parse_dictionary_page_header(r, h); break;
+      case 8: parse_data_page_header_v2(r, h); break;
+      default: r.skip(t);
+    }
+  }
+  r.struct_end();
+  h.header_len = r.consumed();
+  return h;
+}
+
+static inline uint64_t read_varint(const uint8_t*& p, const uint8_t* end) {
+  uint64_t v = 0;
+  for (int s = 0; s < 64; s += 7) {
+    if (p >= end) throw std::runtime_error("parquet: truncated hybrid run header");
+    uint8_t b = *p++;
+    v |= uint64_t(b & 0x7f) << s;
+    if (!(b & 0x80)) return v;
+  }
+  throw std::runtime_error("parquet: bad varint");
+}
+
+std::vector<HRun> hybrid_runs(const uint8_t* p, size_t len, int bw, uint32_t nvalues) {
+  std::vector<HRun> runs;
+  const uint8_t* s = p;
+  const uint8_t* end = p + len;
+  uint32_t v = 0;
+  const int vbytes = (bw + 7) / 8;
+  while (v < nvalues) {
+    uint64_t h = read_varint(s, end);
+    HRun r{};
+    r.start = v;
+    if (h & 1) {
+      uint64_t groups = h >> 1;
+      uint64_t bytes = groups * uint64_t(bw);
+      if (uint64_t(end - s) < bytes) throw std::runtime_error("parquet: truncated bit-packed run");
+      uint64_t cnt = groups * 8;
+      if (cnt == 0) continue;
+      r.literal = true;
+      r.off = uint32_t(s - p);
+      r.count = uint32_t(std::min<uint64_t>(cnt, nvalues - v));
+      s += bytes;
+    } else {
+      uint64_t cnt = h >> 1;
+      if (end - s < vbytes) throw std::runtime_error("parquet: truncated RLE run");
+      uint32_t val = 0;
+      for (int i = 0; i < vbytes; i++) val |= uint32_t(s[i]) << (8 * i);
+      s += vbytes;
+      if (cnt == 0) continue;
+      r.literal = false;
+      r.value = val;
+      r.count = uint32_t(std::min<uint64_t>(cnt, nvalues - v));
+    }
+    v += r.count;
+    runs.push_back(r);
+  }
+  return runs;
+}
+
+void hybrid_decode(const uint8_t* p, size_t len, int bw, uint32_t nvalues, uint32_t* out) {
+  auto runs = hybrid_runs(p, len, bw, nvalues);
+  const uint64_t mask = bw >= 32 ? 0xffffffffull : ((1ull << bw) - 1);
+  for (const auto& r : runs) {
+    if (!r.literal) {
+      for (uint32_t i = 0; i < r.count; i++) out[r.start + i] = r.value;
+    } else {
+      const uint8_t* d = p + r.off;
+      for (uint32_t i = 0; i < r.count; i++) {
+        uint64_t bit = uint64_t(i) * bw;
+        uint64_t w = 0;
+        size_t b0 = bit >> 3;
+        for (int k = 0; k < 8 && d + b0 + k < p + len; k++) w |= uint64_t(d[b0 + k]) << (8 * k);
+        out[r.start + i] = uint32_t((w >> (bit & 7)) & mask);
+      }
+    }
+  }
+}
+
+}  // namespace pq
+}  // namespace lk

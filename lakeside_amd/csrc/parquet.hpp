@@ -1,0 +1,86 @@
+// Parquet footer / page-header parsing and hybrid RLE/bit-packed run directories (host side).
+//
+// The GPU never parses Thrift: at segment load the host walks the footer and every page header once,
+// records where each page's definition-level and value streams start, and splits each hybrid stream into
+// runs.  Those run directories let a GPU tile start decoding at any row without replaying the stream.
+#pragma once
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace lk {
+namespace pq {
+
+enum PhysType { BOOLEAN = 0, INT32 = 1, INT64 = 2, INT96 = 3, FLOAT = 4, DOUBLE = 5, BYTE_ARRAY = 6, FIXED_LEN = 7 };
+enum Encoding { PLAIN = 0, PLAIN_DICTIONARY = 2, RLE = 3, BIT_PACKED = 4, RLE_DICTIONARY = 8 };
+enum PageType { DATA_PAGE = 0, INDEX_PAGE = 1, DICTIONARY_PAGE = 2, DATA_PAGE_V2 = 3 };
+enum Repetition { REQUIRED = 0, OPTIONAL = 1, REPEATED = 2 };
+
+struct SchemaElement {
+  int type = -1;
+  int repetition = REQUIRED;
+  int num_children = 0;
+  std::string name;
+};
+
+struct ColumnMeta {
+  int type = -1;
+  int codec = 0;
+  std::vector<std::string> path;
+  int64_t num_values = 0;
+  int64_t total_uncompressed = 0;
+  int64_t total_compressed = 0;
+  int64_t data_page_offset = 0;
+  int64_t dictionary_page_offset = -1;
+  int64_t null_count = -1;
+};
+
+struct RowGroupMeta {
+  std::vector<ColumnMeta> columns;
+  int64_t num_rows = 0;
+};
+
+struct FileMeta {
+  std::vector<SchemaElement> schema;
+  std::vector<RowGroupMeta> row_groups;
+  int64_t num_rows = 0;
+};
+
+struct PageHeader {
+  int type = -1;
+  int32_t uncompressed = 0;
+  int32_t compressed = 0;
+  size_t header_len = 0;
+  // DATA_PAGE (v1) / DATA_PAGE_V2
+  int32_t num_values = 0;
+  int encoding = 0;
+  int def_encoding = RLE;
+  int32_t num_nulls = -1;   // v2 only
+  int32_t num_rows = -1;    // v2 only
+  int32_t def_len = 0;      // v2 only
+  int32_t rep_len = 0;      // v2 only
+  bool v2_compressed = true;
+  // DICTIONARY_PAGE
+  int32_t dict_num_values = 0;
+};
+
+// Throws lk::ThriftError / std::runtime_error on malformed input.
+FileMeta parse_footer(const uint8_t* file, size_t size);
+PageHeader parse_page_header(const uint8_t* p, size_t n);
+
+// One run of a hybrid RLE/bit-packed stream.
+struct HRun {
+  uint32_t start;   // first value index of the run (relative to the stream)
+  uint32_t count;   // number of values the run covers (literal runs are clipped to the stream's size)
+  uint32_t off;     // literal: byte offset of the packed data from the stream start; RLE: unused
+  uint32_t value;   // RLE: the repeated value; literal: unused
+  bool literal;
+};
+
+// Split a hybrid stream of `nvalues` values at bit width `bw` into runs. `len` bounds the bytes.
+std::vector<HRun> hybrid_runs(const uint8_t* p, size_t len, int bw, uint32_t nvalues);
+// Decode the whole stream (host reference; used for zone maps and validity counts).
+void hybrid_decode(const uint8_t* p, size_t len, int bw, uint32_t nvalues, uint32_t* out);
+
+}  // namespace pq
+}  // namespace lk

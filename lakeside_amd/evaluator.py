@@ -1,0 +1,152 @@
+"""Host-side mirror of the worker's per-segment evaluator over the HIP engine.
+
+``evaluate_push_down_request`` mirrors ``Commons.evaluatePushDownRequest(queryId, localParquet,
+pushDownRequest)`` (core/src/main/scala/com/cardinal/utils/Commons.scala:343-397): same arguments, globs
+of 10 (local) or 5 (remote) segments, rows ascending by timestamp per glob, errors swallowed into an empty
+result as the reference does (Commons.scala:249-253, 338-340).  ``Engine`` is the lower-level API that
+raises ``LakesideError`` instead.
+"""
+import ctypes
+import json
+import logging
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import LK_MERGED, LK_PER_GLOB_ROWS, LakesideError, check
+
+log = logging.getLogger("lakeside_amd")
+
+Row = Tuple[int, float, Dict[str, str]]
+
+
+class Result:
+    """Rows of one evaluation (copied out of the library result)."""
+
+    def __init__(self, handle):
+        L = _lib.lib()
+        n = L.lk_result_num_rows(handle)
+        self.ts = np.ctypeslib.as_array(L.lk_result_timestamps(handle), (n,)).copy() if n else np.zeros(0, np.int64)
+        self.values = np.ctypeslib.as_array(L.lk_result_values(handle), (n,)).copy() if n else np.zeros(0)
+        self.globs = np.ctypeslib.as_array(L.lk_result_globs(handle), (n,)).copy() if n else np.zeros(0, np.uint32)
+        ncol = L.lk_result_num_tag_columns(handle)
+        self.tag_names = [L.lk_result_tag_name(handle, c).decode() for c in range(ncol)]
+        self._tags = []
+        for r in range(n):
+            t = {}
+            for c in range(ncol):
+                v = L.lk_result_tag_value(handle, r, c)
+                if v is not None:
+                    t[self.tag_names[c]] = v.decode()
+            self._tags.append(t)
+        self.stats = json.loads(L.lk_result_stats(handle).decode())
+
+    def __len__(self):
+        return len(self.ts)
+
+    def rows(self) -> List[Row]:
+        return [(int(t), float(v), g) for t, v, g in zip(self.ts, self.values, self._tags)]
+
+    def per_glob(self, nglobs: int) -> List[List[Row]]:
+        out: List[List[Row]] = [[] for _ in range(nglobs)]
+        for t, v, g, tags in zip(self.ts, self.values, self.globs, self._tags):
+            out[int(g)].append((int(t), float(v), tags))
+        return out
+
+
+class Engine:
+    """One per process per GPU: HIP device, stream, HBM segment cache, optional RCCL communicator."""
+
+    def __init__(self, device: int = 0):
+        L = _lib.lib()
+        h = ctypes.c_void_p()
+        check(L.lk_engine_create(json.dumps({"device": device}).encode(), ctypes.byref(h)))
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            _lib.lib().lk_engine_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- HBM segment cache ----
+    def put_segment(self, key: str, data) -> None:
+        buf = (ctypes.c_uint8 * len(data)).from_buffer_copy(data) if not isinstance(data, ctypes.Array) else data
+        check(_lib.lib().lk_segment_put(self._h, key.encode(), ctypes.cast(buf, ctypes.c_void_p), len(data)))
+
+    def put_segment_ptr(self, key: str, ptr, size: int) -> None:
+        check(_lib.lib().lk_segment_put(self._h, key.encode(), ptr, size))
+
+    def load_segment(self, path: str) -> None:
+        check(_lib.lib().lk_segment_load(self._h, path.encode()))
+
+    def evict(self, key: str) -> None:
+        check(_lib.lib().lk_segment_evict(self._h, key.encode()))
+
+    @property
+    def segment_count(self) -> int:
+        return int(_lib.lib().lk_segment_count(self._h))
+
+    @property
+    def segment_bytes(self) -> int:
+        return int(_lib.lib().lk_segment_bytes(self._h))
+
+    # ---- evaluation ----
+    def eval_pushdown(self, request_json: str, paths: Sequence[str], glob_size: int = 10,
+                      flags: int = LK_PER_GLOB_ROWS) -> Result:
+        L = _lib.lib()
+        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        h = ctypes.c_void_p()
+        check(L.lk_eval_pushdown(self._h, request_json.encode(), arr, len(paths), glob_size, flags, ctypes.byref(h)))
+        try:
+            return Result(h)
+        finally:
+            L.lk_result_free(h)
+
+    # ---- multi-GPU ----
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = (ctypes.c_uint8 * _lib.LK_UNIQUE_ID_BYTES)()
+        check(_lib.lib().lk_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, uid: bytes, world: int, rank: int) -> None:
+        buf = (ctypes.c_uint8 * _lib.LK_UNIQUE_ID_BYTES).from_buffer_copy(uid)
+        check(_lib.lib().lk_comm_init(self._h, buf, world, rank))
+
+    def eval_pushdown_dist(self, request_json: str, paths: Sequence[str], shard: Optional[Sequence[int]] = None,
+                           glob_size: int = 10) -> Result:
+        L = _lib.lib()
+        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        sh = (ctypes.c_int32 * len(paths))(*shard) if shard is not None else None
+        h = ctypes.c_void_p()
+        check(L.lk_eval_pushdown_dist(self._h, request_json.encode(), arr, len(paths), sh, glob_size,
+                                      ctypes.byref(h)))
+        try:
+            return Result(h)
+        finally:
+            L.lk_result_free(h)
+
+
+def evaluate_push_down_request(engine: Engine, query_id: str, local_parquet: bool, push_down_request: str,
+                               paths: Sequence[str]) -> List[List[Row]]:
+    """Commons.evaluatePushDownRequest (Commons.scala:343-397): per-glob rows; a failing glob/request
+    yields no rows (Commons.scala:249-253) and is logged; no segments -> one sentinel row ts=-1."""
+    glob_size = 10 if local_parquet else 5
+    nglobs = max(1, (len(paths) + glob_size - 1) // glob_size)
+    try:
+        res = engine.eval_pushdown(push_down_request, paths, glob_size, LK_PER_GLOB_ROWS)
+    except LakesideError as e:
+        log.error("[%s] Error in reading glob: %s", query_id, e)
+        return [[] for _ in range(nglobs)]
+    return res.per_glob(nglobs)
+
+
+__all__ = ["Engine", "Result", "LakesideError", "evaluate_push_down_request", "LK_MERGED", "LK_PER_GLOB_ROWS"]

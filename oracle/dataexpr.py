@@ -1,0 +1,567 @@
+"""CPU restatement of lakeside's sealed-segment DataExpr evaluation (TEST INFRASTRUCTURE ONLY).
+
+This module is the parity oracle.  Only ``tests/``, ``__graft_entry__.smoke()`` and
+``bench.py``'s ``cpu_baseline`` leg may import it, and only as the checker: the product path
+(``lakeside_amd``) never routes through it.
+
+Pinning.  The reference's arithmetic runs inside DuckDB 1.3.2 (``org.duckdb:duckdb_jdbc:1.3.2.0``,
+``ext.gradle:24``), which is neither vendored nor installed; the reference is Scala/JVM and cannot run
+here.  The reference pins no numeric result.  What IS pinned:
+  * the plan: ``oracle/sqlplan.py`` restates ``BaseExpr.generateSql`` and is checked against the exact
+    SQL strings of ``query-api/src/test/scala/com/cardinal/queryapi/utils/ASTUtilsBaseExprTest.scala``;
+  * the numbers: this numpy restatement is cross-checked, fixture by fixture, against that generated SQL
+    executed by an independent SQL engine (SQLite, ``oracle/sqlplan.py::run_sql``).
+Counts/min/max are exact; sums are the correctly rounded sum (``math.fsum``), which is the
+order-independent target the reference's parallel DuckDB sum approximates.
+
+Semantics follow SURVEY.md Appendix A (S1-S22); each function cites the reference file:line it restates.
+"""
+from __future__ import annotations
+
+import json
+import math
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+TIMESTAMP = "_cardinalhq.timestamp"   # core/.../utils/Commons.scala:55
+VALUE = "_cardinalhq.value"           # Commons.scala:57
+NAME = "_cardinalhq.name"             # Commons.scala:47
+LOGS, TRACES, METRICS = "logs", "traces", "metrics"  # Commons.scala:48-50
+
+# Operator vocabulary, core/.../logs/LogCommons.scala:21-44
+EXISTS, NOT_EQUALS, REGEX, IN, NOT_IN, CONTAINS = "exists", "!=", "regex", "in", "not_in", "contains"
+EQ, HAS, GT, GE, LT, LE = "eq", "has", "gt", "ge", "lt", "le"
+SUM, MIN, MAX, COUNT, AVG = "sum", "min", "max", "count", "avg"
+
+
+# ----------------------------------------------------------------------------------------------
+# Model + JSON parsing (ASTUtils.scala:124-137, 222-229, 276-417; SegmentRequest.scala:45-98)
+# ----------------------------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Filter:
+    k: str
+    v: Tuple[str, ...]
+    op: str
+    extracted: bool = False
+    computed: bool = False
+    dataType: str = "string"
+
+
+@dataclass(frozen=True)
+class BinaryClause:
+    q1: Any
+    q2: Any
+    op: str
+
+
+@dataclass(frozen=True)
+class NotClause:
+    inner: Any
+
+
+@dataclass
+class ChartOptions:
+    aggregation: str = SUM
+    groupBys: List[str] = field(default_factory=list)
+    type: str = "count"
+    rollup: Optional[str] = None
+    fieldName: Optional[str] = None
+    fieldType: Optional[str] = None
+
+
+@dataclass
+class BaseExpr:
+    id: str
+    dataset: str
+    filter: Any
+    chart: Optional[ChartOptions]
+    extract: Any = None
+    compute: Any = None
+
+
+@dataclass
+class SegmentRequest:
+    hour: str
+    dateInt: str
+    segmentId: str
+    sealedStatus: bool
+    dataset: str
+    queryTags: Dict[str, Any]
+    stepInMillis: int
+    customerId: str
+    collectorId: str
+    bucketName: str
+    cName: str
+    startTs: int
+    endTs: int
+
+
+@dataclass
+class PushDownRequest:
+    baseExpr: BaseExpr
+    segmentRequests: List[SegmentRequest]
+    reverseSort: bool = False
+    isTagQuery: bool = False
+    processor: Optional[dict] = None
+
+
+def _basic_filter(node: dict) -> Filter:
+    """ASTUtils.toBasicFilter (ASTUtils.scala:276-288)."""
+    if node.get("k") is None:
+        raise ValueError("No `k` provided in filter!")
+    op = node.get("op")
+    if op is None:
+        raise ValueError("No op provided for filter!")
+    values = tuple(node.get("v") or [])
+    if not values and op != EXISTS:
+        raise ValueError(f"No value for key = {node['k']} provided in filter!")
+    return Filter(k=node["k"], v=values, op=op, extracted=bool(node.get("extracted", False)),
+                  computed=bool(node.get("computed", False)), dataType=node.get("dataType", "string"))
+
+
+def _binary_clause(node: dict):
+    """ASTUtils.toBinaryClauseFromFilterJsonNode (ASTUtils.scala:379-404): every non-textual member of
+    the object (JSON order) is a child; children fold left-associatively."""
+    op = node.get("op")
+    if op is None:
+        raise ValueError("No `op` provided in binary query clause!")
+    clauses = [handle_filter(v) for v in node.values() if not isinstance(v, str)]
+    if len(clauses) < 2:
+        raise ValueError("Atleast two clauses required in a binary clause!")
+    acc = clauses[0]
+    for c in clauses[1:]:
+        acc = BinaryClause(acc, c, op)
+    return acc
+
+
+def handle_filter(node: dict):
+    """ASTUtils.handleFilter (ASTUtils.scala:406-417)."""
+    if "not" in node and node["not"] is not None:
+        return NotClause(handle_filter(node["not"]))
+    if node.get("k") is not None:
+        return _basic_filter(node)
+    return _binary_clause(node)
+
+
+def to_base_expr(node: dict, id_: Optional[str] = None) -> BaseExpr:
+    """ASTUtils.toBaseExpr (ASTUtils.scala:290-377)."""
+    chart = None
+    if node.get("chart") is not None:
+        c = node["chart"]
+        gb = c.get("groupBys")
+        agg = c.get("aggregation")
+        chart = ChartOptions(aggregation=agg if isinstance(agg, str) else SUM,
+                             groupBys=list(gb) if isinstance(gb, list) else [],
+                             type=c.get("type", "count"), rollup=c.get("rollup"),
+                             fieldName=c.get("fieldName"), fieldType=c.get("fieldType"))
+    if node.get("filter") is None:
+        raise ValueError("No filter provided!")
+    return BaseExpr(id=id_ if id_ is not None else node.get("id", "_"),
+                    dataset=node.get("dataset", METRICS), filter=handle_filter(node["filter"]),
+                    chart=chart, extract=node.get("extract"), compute=node.get("compute"))
+
+
+def parse_pushdown(text: str) -> PushDownRequest:
+    """PushDownRequest.fromJson (SegmentRequest.scala:45-60)."""
+    p = json.loads(text)
+    be = to_base_expr(p["baseExpr"])
+    segs = []
+    for s in p["segmentRequests"]:
+        segs.append(SegmentRequest(hour=str(s.get("hour", "")), dateInt=str(s.get("dateInt", "")),
+                                   segmentId=str(s.get("segmentId", "")),
+                                   sealedStatus=bool(s.get("sealedStatus", True)),
+                                   dataset=s.get("dataset", be.dataset), queryTags=s.get("queryTags") or {},
+                                   stepInMillis=int(s["stepInMillis"]), customerId=s.get("customerId", ""),
+                                   collectorId=s.get("collectorId", ""), bucketName=s.get("bucketName", ""),
+                                   cName=s.get("cName", ""), startTs=int(s["startTs"]), endTs=int(s["endTs"])))
+    return PushDownRequest(baseExpr=be, segmentRequests=segs, reverseSort=bool(p.get("reverseSort", False)),
+                           isTagQuery=bool(p.get("isTagQuery", False)), processor=p.get("processor"))
+
+
+# ----------------------------------------------------------------------------------------------
+# Plan helpers
+# ----------------------------------------------------------------------------------------------
+def filter_field_set(q) -> set:
+    """BaseExpr.filterFieldSet (BaseExpr.scala:652-663).  NOTE: a NotClause contributes nothing
+    (the reference's match has no NotClause case), so a field used only under `not` is never put in
+    nonExistentFields and compiles to a column reference even when absent."""
+    if isinstance(q, Filter):
+        return {q.k}
+    if isinstance(q, BinaryClause):
+        return filter_field_set(q.q1) | filter_field_set(q.q2)
+    return set()
+
+
+def field_set(be: BaseExpr) -> set:
+    """BaseExpr.fieldSet (BaseExpr.scala:648-650)."""
+    return filter_field_set(be.filter) | set(be.chart.groupBys if be.chart else [])
+
+
+def exact_tags(q) -> Dict[str, Any]:
+    """BaseExpr.queryTags/exactTags (BaseExpr.scala:623-646)."""
+    out: Dict[str, Any] = {}
+    if isinstance(q, Filter):
+        if q.op == EQ:
+            out[q.k] = q.v[0]
+        elif q.op == IN:
+            out[q.k] = list(q.v)
+    elif isinstance(q, BinaryClause) and q.op == "and":
+        out.update(exact_tags(q.q1))
+        out.update(exact_tags(q.q2))
+    return out
+
+
+def value_column(be: BaseExpr) -> str:
+    """Aggregated column: logs/traces `_cardinalhq.value` (BaseExpr.scala:349-351);
+    metrics `rollup_<rollup|sum>` (BaseExpr.scala:376-394)."""
+    if be.dataset == METRICS:
+        return "rollup_" + ((be.chart.rollup if be.chart else None) or SUM)
+    return VALUE
+
+
+def check_hot_path(pr: PushDownRequest) -> None:
+    """Raise for query shapes outside the hot path."""
+    be = pr.baseExpr
+    if pr.isTagQuery or be.chart is None:
+        raise NotImplementedError("tag/exemplar queries are outside the hot path")
+    agg = be.chart.aggregation
+    if agg not in (SUM, MIN, MAX, COUNT, AVG):
+        raise NotImplementedError(f"aggregation {agg} (sketch path) is outside the hot path")
+    if be.chart.fieldName is not None or be.extract is not None or be.compute is not None:
+        raise NotImplementedError("extract/compute/field charts are outside the hot path")
+    if be.dataset not in (LOGS, TRACES, METRICS):
+        raise ValueError(f"Invalid dataset: {be.dataset}")
+
+    def walk(q):
+        if isinstance(q, Filter):
+            if q.extracted or q.computed:
+                raise NotImplementedError("extracted/computed filter fields are outside the hot path")
+            if q.op in (GT, GE, LT, LE):
+                raise NotImplementedError("numeric comparisons are not on the hot path yet")
+            if q.op not in (EQ, NOT_EQUALS, IN, NOT_IN, REGEX, CONTAINS, HAS, EXISTS):
+                raise ValueError(f"Invalid operator {q.op}")
+        elif isinstance(q, BinaryClause):
+            if q.op not in ("and", "or"):
+                raise ValueError(f"unknown binary op {q.op}")
+            walk(q.q1)
+            walk(q.q2)
+        else:
+            walk(q.inner)
+    walk(be.filter)
+
+
+# ----------------------------------------------------------------------------------------------
+# Regex: DuckDB regexp_matches(l, p, 'i') = RE2 partial match, case-insensitive (BaseExpr.scala:485-501)
+# ----------------------------------------------------------------------------------------------
+def re2_search(values: Sequence[Optional[str]], pattern: str) -> List[Optional[bool]]:
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    return pc.match_substring_regex(pa.array(list(values), type=pa.string()), pattern,
+                                    ignore_case=True).to_pylist()
+
+
+# ----------------------------------------------------------------------------------------------
+# Glob evaluation (Commons.toGlobResultSet 200-254 + generateSql semantics, BaseExpr.scala:319-513)
+# ----------------------------------------------------------------------------------------------
+class _Col:
+    """A string column of a glob: dictionary codes (-1 = NULL) plus the dictionary."""
+
+    def __init__(self, codes: np.ndarray, dictionary: List[str]):
+        self.codes = codes
+        self.dictionary = dictionary
+
+
+def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[str], sources=None):
+    """union_by_name=True read of the glob (Commons.scala:210-213): a column missing from a file is NULL
+    for that file's rows.  Returns (union column names, numeric arrays + validity, string columns)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    union: List[str] = []
+    tables = []
+    for i, p in enumerate(paths):
+        src = p if sources is None else pa.BufferReader(sources[i])
+        pf = pq.ParquetFile(src)
+        names = pf.schema_arrow.names
+        for n in names:
+            if n not in union:
+                union.append(n)
+        want = [c for c in list(numeric) + list(strings) if c in names]
+        tables.append((pf.read(columns=want, use_threads=True), pf.metadata.num_rows))
+    nums = {}
+    for c in numeric:
+        parts, valid = [], []
+        for t, n in tables:
+            if c in t.column_names:
+                a = t.column(c).combine_chunks() if t.num_rows else pa.array([], pa.float64())
+                arr = a.to_numpy(zero_copy_only=False)
+                v = np.asarray(a.is_valid().to_numpy(zero_copy_only=False), dtype=bool) if a.null_count else \
+                    np.ones(n, dtype=bool)
+                arr = np.where(v, arr, 0) if a.null_count else arr
+                parts.append(np.asarray(arr))
+                valid.append(v)
+            else:
+                parts.append(np.zeros(n, dtype=np.float64))
+                valid.append(np.zeros(n, dtype=bool))
+        nums[c] = (np.concatenate(parts) if parts else np.zeros(0), np.concatenate(valid) if valid else
+                   np.zeros(0, dtype=bool))
+    strs = {}
+    for c in strings:
+        vocab: Dict[str, int] = {}
+        parts = []
+        for t, n in tables:
+            if c in t.column_names:
+                a = t.column(c).combine_chunks()
+                if pa.types.is_dictionary(a.type):
+                    a = a.cast(a.type.value_type)
+                d = a.dictionary_encode()
+                local = d.dictionary.to_pylist()
+                remap = np.array([vocab.setdefault(s, len(vocab)) for s in local] + [-1], dtype=np.int64)
+                idx = d.indices.to_numpy(zero_copy_only=False)
+                idx = np.where(np.asarray(d.indices.is_valid().to_numpy(zero_copy_only=False), dtype=bool),
+                               idx, len(local)).astype(np.int64) if d.indices.null_count else \
+                    np.asarray(idx, dtype=np.int64)
+                parts.append(remap[idx])
+            else:
+                parts.append(np.full(n, -1, dtype=np.int64))
+        inv = [None] * len(vocab)
+        for s, i in vocab.items():
+            inv[i] = s
+        strs[c] = _Col(np.concatenate(parts) if parts else np.zeros(0, dtype=np.int64), inv)
+    return union, nums, strs
+
+
+def _leaf(f: Filter, col: Optional[_Col], nonexistent: set, n: int):
+    """One filter leaf under SQL three-valued logic -> (is_true, is_false) masks.
+    Leaf compile: BaseExpr.scala:461-504; NULL semantics: SURVEY.md Appendix A S7."""
+    if f.k in nonexistent:                       # BaseExpr.scala:462-464 -> literal `false`
+        return np.zeros(n, bool), np.ones(n, bool)
+    if col is None:                              # absent column referenced only under NOT: all NULL
+        codes, dictionary = np.full(n, -1, np.int64), []
+    else:
+        codes, dictionary = col.codes, col.dictionary
+    notnull = codes >= 0
+    if f.op in (HAS, EXISTS):                    # IS NOT NULL never yields NULL
+        return notnull.copy(), ~notnull
+    if f.op == EQ:
+        hit = [s == f.v[0] for s in dictionary]
+    elif f.op == NOT_EQUALS:
+        hit = [s != f.v[0] for s in dictionary]
+    elif f.op == IN:
+        hit = [s in f.v for s in dictionary]
+    elif f.op == NOT_IN:
+        hit = [s not in f.v for s in dictionary]
+    elif f.op == REGEX:
+        hit = [bool(b) for b in re2_search(dictionary, f.v[0])] if dictionary else []
+    elif f.op == CONTAINS:
+        hit = [bool(b) for b in re2_search(dictionary, ".*" + f.v[0] + ".*")] if dictionary else []
+    else:
+        raise NotImplementedError(f.op)
+    lut = np.array(list(hit) + [False], dtype=bool)
+    h = lut[np.where(notnull, codes, len(hit))]
+    return h & notnull, (~h) & notnull
+
+
+def _eval_filter(q, cols: Dict[str, _Col], nonexistent: set, n: int):
+    """Kleene AND/OR/NOT over (is_true, is_false) masks (BaseExpr.scala:505-511)."""
+    if isinstance(q, Filter):
+        return _leaf(q, cols.get(q.k), nonexistent, n)
+    if isinstance(q, NotClause):
+        t, f = _eval_filter(q.inner, cols, nonexistent, n)
+        return f, t
+    t1, f1 = _eval_filter(q.q1, cols, nonexistent, n)
+    t2, f2 = _eval_filter(q.q2, cols, nonexistent, n)
+    if q.op == "and":
+        return t1 & t2, f1 | f2
+    return t1 | t2, f1 & f2
+
+
+def _leaf_columns(q) -> List[str]:
+    if isinstance(q, Filter):
+        return [q.k]
+    if isinstance(q, NotClause):
+        return _leaf_columns(q.inner)
+    return _leaf_columns(q.q1) + _leaf_columns(q.q2)
+
+
+@dataclass
+class Cell:
+    """One (bucket, tags) aggregate cell: raw aggregation state, exact."""
+    ts: int
+    tags: Dict[str, str]
+    rows: int = 0
+    count: int = 0
+    values: Optional[np.ndarray] = None      # non-null values (for exact sum)
+    vmin: float = math.inf
+    vmax: float = -math.inf
+
+    def agg_value(self, agg: str) -> float:
+        """SQL aggregate of the cell, NULL -> 0.0 via JDBC getDouble (Commons.scala:427)."""
+        if agg == COUNT:
+            return float(self.count)
+        if self.count == 0:
+            return 0.0
+        if agg == SUM:
+            return exact_sum(self.values)
+        if agg == MIN:
+            return self.vmin
+        if agg == MAX:
+            return self.vmax
+        if agg == AVG:
+            return exact_sum(self.values) / self.count
+        raise NotImplementedError(agg)
+
+
+def exact_sum(v: np.ndarray) -> float:
+    """Correctly rounded sum; NaN/Inf follow IEEE."""
+    if v is None or len(v) == 0:
+        return 0.0
+    if not np.all(np.isfinite(v)):
+        return float(np.sum(v))
+    return math.fsum(v.tolist())
+
+
+def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str], sources=None):
+    """Rows of ONE glob = one DuckDB query (Commons.toGlobResultSet, Commons.scala:200-254, then
+    resultSetToSource/toDataPoint 280-341, 399-462).  Returns list of (ts, value, tags) in ascending ts
+    order (ties ordered by tags for determinism; the reference's tie order is arbitrary, S17)."""
+    be = pr.baseExpr
+    chart = be.chart
+    segs = [pr.segmentRequests[i] for i in seg_idx]
+    vcol = value_column(be)
+    fs = field_set(be)
+    strings = sorted(set(_leaf_columns(be.filter)) | set(chart.groupBys) | {NAME})
+    union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
+    nonexistent = fs - set(union)                                   # Commons.scala:224
+    # Columns the generated SQL references but that no file of the glob has: DuckDB raises a Binder
+    # Error, which Commons.toGlobResultSet turns into an empty result (Commons.scala:249-253).  This
+    # happens for a field used only under `not` (not in fieldSet), and for ts/name/value columns.
+    referenced = (set(_leaf_columns(be.filter)) - nonexistent) | {TIMESTAMP, NAME, vcol}
+    if not referenced <= set(union):
+        return []
+    start = min(s.startTs for s in segs)                            # Commons.scala:225-226
+    end = max(s.endTs for s in segs)
+    step = segs[0].stepInMillis                                     # Commons.scala:232 (glob head)
+    ts, ts_valid = nums[TIMESTAMP]
+    ts = ts.astype(np.int64)
+    n = len(ts)
+    win = ts_valid & (ts >= start) & (ts < end)                     # BaseExpr.scala:159-161
+    t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    keep = win & t
+    if be.dataset == METRICS:
+        bucket = ts                                                  # BaseExpr.scala:391-394
+    else:
+        bucket = ts - np.fmod(ts, step)                              # BaseExpr.scala:163-165 (fmod)
+    gcols = [g for g in chart.groupBys if g not in nonexistent]      # BaseExpr.scala:338-346 (S12)
+    keycols = [("name", strs[NAME])] + [(g, strs[g]) for g in gcols]
+    vals, vvalid = nums[vcol]
+    idx = np.nonzero(keep)[0]
+    if len(idx) == 0:
+        return []
+    key = np.stack([bucket[idx]] + [c.codes[idx] for _, c in keycols], axis=1)
+    order = np.lexsort(key.T[::-1])
+    key = key[order]
+    idx = idx[order]
+    brk = np.nonzero(np.any(key[1:] != key[:-1], axis=1))[0] + 1
+    starts = np.concatenate([[0], brk])
+    ends = np.concatenate([brk, [len(idx)]])
+    qtags = {k: (v if isinstance(v, str) else str(v)) for k, v in segs[0].queryTags.items()}
+    out = []
+    for s, e in zip(starts, ends):
+        rows = idx[s:e]
+        ok = vvalid[rows]
+        v = vals[rows][ok].astype(np.float64)
+        cell = Cell(ts=int(key[s, 0]), tags={}, rows=len(rows), count=int(ok.sum()), values=v)
+        if len(v):
+            cell.vmin = float(_sql_min(v))
+            cell.vmax = float(_sql_max(v))
+        tags = {}
+        for j, (name, c) in enumerate(keycols):
+            code = key[s, j + 1]
+            if code >= 0:
+                sv = c.dictionary[code]
+                if sv is not None and sv != "null" and sv != "":   # Commons.scala:433 (S15)
+                    tags[name] = sv
+        if not tags:
+            tags = dict(qtags)                                        # Commons.scala:450-452
+        cell.tags = tags
+        out.append(cell)
+    out.sort(key=lambda c: (c.ts, sorted(c.tags.items()), c.agg_value(chart.aggregation)))
+    return out
+
+
+def _sql_min(v):
+    """DuckDB orders NaN above every other double: min ignores NaN unless all are NaN."""
+    nn = v[~np.isnan(v)]
+    return np.min(nn) if len(nn) else np.nan
+
+
+def _sql_max(v):
+    return np.nan if np.any(np.isnan(v)) else np.max(v)
+
+
+def globs_of(pr: PushDownRequest, glob_size: int) -> List[List[int]]:
+    """Segments chunked in request order (Commons.scala:361-366)."""
+    n = len(pr.segmentRequests)
+    return [list(range(i, min(n, i + glob_size))) for i in range(0, n, glob_size)]
+
+
+def evaluate_glob_cells(pr: PushDownRequest, glob_size: int, paths: Sequence[str], sources=None):
+    """Cells (with their raw non-NULL values) of every glob."""
+    check_hot_path(pr)
+    out = []
+    for g in globs_of(pr, glob_size):
+        out.append(evaluate_glob(pr, g, [paths[i] for i in g], None if sources is None else [sources[i] for i in g]))
+    return out
+
+
+def evaluate_per_glob(pr: PushDownRequest, paths: Sequence[str], glob_size: int = 10, sources=None):
+    """Worker level (S17): list over globs of the glob's rows [(ts, value, tags)]."""
+    agg = pr.baseExpr.chart.aggregation
+    return [[(c.ts, c.agg_value(agg), c.tags) for c in cells]
+            for cells in evaluate_glob_cells(pr, glob_size, paths, sources)]
+
+
+def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, Dict[str, str]]]:
+    """query-api merge (S19): TimeGroupedSketchAggregator (TimeGroupedSketchAggregator.scala:57-114,
+    148-170).  Cells merge by exact timestamp; with groupBys by the full tag map, otherwise all cells of a
+    timestamp merge into one.  sum/count add, min/max by min/max of the per-glob values (a glob cell whose
+    values are all NULL contributes its JDBC 0.0, Commons.scala:427).
+
+    Order-dependent details of the reference are pinned to a deterministic choice:
+      * sums: the correctly rounded sum of every underlying value (the reference adds per-glob DuckDB sums
+        in arrival order; SURVEY.md Appendix A S14 makes the correctly rounded sum the parity target);
+      * without groupBys the merged row takes "the first input's" tags (TimeGroupedSketchAggregator.scala:
+        57-60, arrival order); we take the smallest tag map."""
+    agg = pr.baseExpr.chart.aggregation
+    if agg == AVG:
+        raise NotImplementedError("avg is split into sum+count before the merge (QueryEngineV2.scala:280-283)")
+    has_gb = bool(pr.baseExpr.chart.groupBys)
+    merged: Dict[Any, list] = {}
+    for cells in glob_cells:
+        for c in cells:
+            k = (c.ts, tuple(sorted(c.tags.items()))) if has_gb else c.ts
+            merged.setdefault(k, []).append(c)
+    out = []
+    for k, cs in merged.items():
+        tags = min((c.tags for c in cs), key=lambda t: sorted(t.items()))
+        if agg == SUM:
+            val = exact_sum(np.concatenate([c.values for c in cs]))
+        elif agg == COUNT:
+            val = float(sum(c.count for c in cs))
+        elif agg == MIN:
+            val = min(c.agg_value(MIN) for c in cs)
+        else:
+            val = max(c.agg_value(MAX) for c in cs)
+        out.append((cs[0].ts, val, tags))
+    out.sort(key=lambda r: (r[0], sorted(r[2].items()), r[1]))
+    return out
+
+
+def evaluate_merged(pr: PushDownRequest, paths: Sequence[str], glob_size: int = 10, sources=None):
+    return merge_glob_cells(pr, evaluate_glob_cells(pr, glob_size, paths, sources))
+
+
+def rows_to_jsonable(rows):
+    return [[int(ts), float(v).hex(), dict(sorted(tags.items()))] for ts, v, tags in rows]

@@ -1,0 +1,149 @@
+"""Parity of the HIP path (through the C ABI) with the oracle and the committed golden rows (MI355X)."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+
+from tests.parity import assert_rows_equal, from_jsonable
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+pytestmark = pytest.mark.gpu
+
+
+def _cases():
+    with open(os.path.join(GOLDEN, "cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def golden_engine(engine):
+    for c in _cases():
+        for p in c["segments"]:
+            path = os.path.join(GOLDEN, p)
+            if not _cached(engine, path):
+                engine.load_segment(path)
+    return engine
+
+
+_loaded = set()
+
+
+def _cached(engine, path):
+    if path in _loaded:
+        return True
+    _loaded.add(path)
+    return False
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: c["name"])
+def test_golden_per_glob(golden_engine, case):
+    from lakeside_amd import LK_PER_GLOB_ROWS
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    res = golden_engine.eval_pushdown(json.dumps(case["request"]), paths, case["glob_size"], LK_PER_GLOB_ROWS)
+    agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+    got = res.per_glob(len(case["expected_per_glob"]))
+    for gi, (g, w) in enumerate(zip(got, case["expected_per_glob"])):
+        assert_rows_equal(g, from_jsonable(w), agg, f"{case['name']} glob {gi}")
+
+
+@pytest.mark.parametrize("case", [c for c in _cases() if c["expected_merged"] is not None],
+                         ids=lambda c: c["name"])
+def test_golden_merged(golden_engine, case):
+    from lakeside_amd import LK_MERGED
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    res = golden_engine.eval_pushdown(json.dumps(case["request"]), paths, case["glob_size"], LK_MERGED)
+    agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+    assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, case["name"])
+
+
+def test_no_segments_sentinel(engine):
+    from lakeside_amd.evaluator import evaluate_push_down_request
+    req = {"baseExpr": {"id": "A", "dataset": "logs", "filter": {"k": "_cardinalhq.name", "v": ["x"], "op": "eq"},
+                        "chart": {"aggregation": "sum", "groupBys": []}},
+           "segmentRequests": [], "reverseSort": False, "isTagQuery": False}
+    rows = evaluate_push_down_request(engine, "q", True, json.dumps(req), [])
+    assert rows == [[(-1, -1.0, {})]]
+
+
+def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys, step=60000, glob_size=10):
+    """Synthetic segments written by tools/synth.cpp, evaluated by the GPU and by the oracle on the same bytes."""
+    import pyarrow as pa  # noqa: F401
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    keys, blobs, segs = [], [], []
+    for i in range(nseg):
+        s = synth.make_segment(synth.segment_spec(i, rows=rows, value_mode=value_mode, null_frac=null_frac,
+                                                  rg_rows=1 << 18, page_rows=1 << 15))
+        key = f"synth/{rows}/{value_mode}/{null_frac}/{i}"
+        engine.put_segment_ptr(key, s.ptr, s.size)
+        blobs.append(s.bytes())
+        s.free()
+        keys.append(key)
+        segs.append(synth.segment_request(i, step=step))
+    req = json.dumps(synth.pushdown(filt, segs, agg, group_bys))
+    pr = dx.parse_pushdown(req)
+    cells = dx.evaluate_glob_cells(pr, glob_size, keys, sources=blobs)
+    want_pg = [[(c.ts, c.agg_value(agg), c.tags) for c in cs] for cs in cells]
+    got = engine.eval_pushdown(req, keys, glob_size, LK_PER_GLOB_ROWS).per_glob(len(want_pg))
+    for gi, (g, w) in enumerate(zip(got, want_pg)):
+        assert_rows_equal(g, w, agg, f"glob {gi}")
+    if agg != "avg":
+        merged = engine.eval_pushdown(req, keys, glob_size, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "merged")
+        return merged
+    return None
+
+
+def test_c1_shape_eq_sum(engine):
+    """C1: 1 segment x 2^20 rows, :eq name :sum, 1m step (bit-exact on integer values)."""
+    from lakeside_amd import synth
+    res = _synth_case(engine, 1, 1 << 20, 0, 0.0, synth.leaf(synth.NAME, "eq", "metric_07"), "sum", [])
+    assert len(res) == 60
+
+
+def test_real_values_sum_within_one_ulp(engine):
+    from lakeside_amd import synth
+    _synth_case(engine, 3, 1 << 19, 1, 0.0, synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "sum", [])
+
+
+def test_c3_shape_and_regex_by2_max_with_nulls(engine):
+    from lakeside_amd import synth
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"),
+            "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
+    _synth_case(engine, 4, 1 << 19, 1, 0.05, filt, "max", [synth.SERVICE, synth.NAMESPACE])
+
+
+def test_groupby_count_min_with_nulls(engine):
+    from lakeside_amd import synth
+    filt = {"op": "or", "q1": {"not": synth.leaf(synth.SERVICE, "eq", "svc-001")},
+            "q2": synth.leaf(synth.NAMESPACE, "in", "ns-01")}
+    _synth_case(engine, 2, 1 << 18, 1, 0.05, filt, "count", [synth.NAMESPACE], step=300000)
+    _synth_case(engine, 2, 1 << 18, 1, 0.05, filt, "min", [synth.NAMESPACE], step=10000)
+
+
+def test_full_size_properties(engine):
+    """At a BASELINE-sized segment (2^24 rows): counts are exact, every row lands in one bucket, and the
+    per-name counts over all buckets add up to the rows of the segment (no row lost or double counted)."""
+    from lakeside_amd import LK_MERGED
+    from lakeside_amd import synth
+    s = synth.make_segment(synth.segment_spec(0, rows=1 << 24))
+    engine.put_segment_ptr("synth/full/0", s.ptr, s.size)
+    s.free()
+    seg = synth.segment_request(0)
+    names = [f"metric_{i:02d}" for i in range(16)]
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "in", *names), [seg], "count", [synth.NAME]))
+    res = engine.eval_pushdown(req, ["synth/full/0"], 10, LK_MERGED)
+    assert len(res) == 60 * 16
+    assert int(res.values.sum()) == 1 << 24
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_03"), [seg], "count", []))
+    part = engine.eval_pushdown(req, ["synth/full/0"], 10, LK_MERGED)
+    by_ts = {}
+    for t, v, tags in res.rows():
+        if tags["name"] == "metric_03":
+            by_ts[t] = v
+    assert {t: v for t, v, _ in part.rows()} == by_ts
