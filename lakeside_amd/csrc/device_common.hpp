@@ -1,0 +1,135 @@
+// Device helpers shared by the HIP kernels (included by kernels.hip only).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "kernels.hpp"
+#include "layout.hpp"
+
+namespace lk {
+
+constexpr int BLOCK = 256;
+constexpr int RPT = 4;                 // row slots decoded together in phase 1
+constexpr int SLOTS = 8;               // row slots per thread per sub-tile
+constexpr int SUBT = BLOCK * SLOTS;    // rows per sub-tile (2048)
+constexpr int HCAP = 512;              // LDS hash entries
+constexpr int HPROBE = 16;
+constexpr int LUT_CAP = 256;           // LDS lookup entries per string column
+constexpr unsigned long long EMPTY = ~0ull;
+constexpr uint32_t OOB = 0x80000000u;  // buffer offset past num_records: no memory access, reads 0
+
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+
+struct LRun {                          // LDS copy of a RunDesc (12 B)
+  uint32_t start, off_lit, value;
+};
+
+__device__ __forceinline__ unsigned long long dbl_order(double d) {
+  unsigned long long u = (unsigned long long)__double_as_longlong(d);
+  if (d != d) u = 0x7ff8000000000000ull;     // NaN sorts above +inf (DuckDB orders NaN greatest)
+  return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
+}
+__device__ __forceinline__ double order_dbl(unsigned long long o) {
+  unsigned long long u = (o >> 63) ? (o & 0x7fffffffffffffffull) : ~o;
+  return __longlong_as_double((long long)u);
+}
+__device__ __forceinline__ void two_sum(double a, double b, double& s, double& e) {
+  s = a + b;
+  double bb = s - a;
+  e = (a - (s - bb)) + (b - bb);
+}
+
+// ---- wave-uniform values: readfirstlane puts them in SGPRs so branches on them stay scalar ----
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ const uint8_t* uni_ptr(const uint8_t* p) {
+  uint64_t v = reinterpret_cast<uint64_t>(p);
+  uint64_t lo = uni(uint32_t(v)), hi = uni(uint32_t(v >> 32));
+  return reinterpret_cast<const uint8_t*>((hi << 32) | lo);
+}
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint8_t* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc((void*)uni_ptr(base), (short)0, int(uni(bytes)), 0x00020000);
+}
+
+// Branch-free run lookup over at most RUN_CAP (64) staged runs: last run whose start <= v.
+__device__ __forceinline__ int find_run64(const LRun* runs, int n, uint32_t v) {
+  int lo = 0;
+#pragma unroll
+  for (int step = 32; step >= 1; step >>= 1) {
+    const int m = lo + step;
+    const uint32_t st = runs[m < n ? m : n - 1].start;
+    lo = (m < n && st <= v) ? m : lo;
+  }
+  return lo;
+}
+
+// Branch-free hybrid RLE/bit-packed value read through a buffer descriptor over the stream: RLE runs read the
+// stream's first dword (harmless) and select the run value, so no lane branches around the load.
+__device__ __forceinline__ uint32_t hybrid_get_buf(__amdgpu_buffer_rsrc_t rs, const LRun& r, uint32_t v, int bw) {
+  const bool lit = (r.off_lit & 0x80000000u) != 0;
+  const uint32_t bit = lit ? (v - r.start) * uint32_t(bw) : 0u;
+  const uint32_t byte = (lit ? (r.off_lit & 0x7fffffffu) : 0u) + (bit >> 3);
+  const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, byte & ~3u, 0, 0);
+  uint64_t x = ((uint64_t)w.y << 32) | w.x;
+  x >>= ((byte & 3u) * 8u + (bit & 7u));
+  const uint32_t mask = bw >= 32 ? 0xffffffffu : ((1u << bw) - 1u);
+  return lit ? (uint32_t(x) & mask) : r.value;
+}
+
+struct Acc {                           // one aggregation cell's partial state
+  unsigned long long key;
+  uint32_t rows, cnt;
+  double hi, lo;                       // SUM: compensated sum
+  unsigned long long ext;              // MIN/MAX: ordered bits
+};
+
+template <int AGG>
+__device__ __forceinline__ void acc_add(Acc& a, bool vvalid, double v) {
+  a.rows += 1;
+  if (!vvalid) return;
+  a.cnt += 1;
+  if (AGG == AGG_SUM) {
+    double s, e;
+    two_sum(a.hi, v, s, e);
+    a.hi = s;
+    a.lo += e;
+  } else if (AGG == AGG_MIN) {
+    unsigned long long o = dbl_order(v);
+    a.ext = o < a.ext ? o : a.ext;
+  } else if (AGG == AGG_MAX) {
+    unsigned long long o = dbl_order(v);
+    a.ext = o > a.ext ? o : a.ext;
+  }
+}
+
+template <int AGG>
+__device__ __forceinline__ void acc_reset(Acc& a, unsigned long long key) {
+  a.key = key;
+  a.rows = 0;
+  a.cnt = 0;
+  a.hi = 0.0;
+  a.lo = 0.0;
+  a.ext = (AGG == AGG_MIN) ? ~0ull : 0ull;
+}
+
+// Merge a partial cell into the global table (device-scope atomics).
+template <int AGG>
+__device__ __forceinline__ void global_merge(const QParams& P, unsigned long long cell, uint32_t rows,
+                                             uint32_t cnt, double hi, double lo, unsigned long long ext) {
+  if (rows == 0) return;
+  atomicAdd(&P.rows[cell], (unsigned long long)rows);
+  if (cnt == 0) return;
+  atomicAdd(&P.cnt[cell], (unsigned long long)cnt);
+  if (AGG == AGG_SUM) {
+    double old = atomicAdd(&P.hi[cell], hi);   // returning atomic: old is exact -> TwoSum recovers the error
+    double s, e;
+    two_sum(old, hi, s, e);
+    atomicAdd(&P.lo[cell], lo + e);
+  } else if (AGG == AGG_MIN) {
+    atomicMin(&P.ext[cell], ext);
+  } else if (AGG == AGG_MAX) {
+    atomicMax(&P.ext[cell], ext);
+  }
+}
+
+}  // namespace lk

@@ -332,6 +332,16 @@ void build_tiles(Builder& B) {
         uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
         uint32_t va = vindex(p, ra), ve = vindex(p, re);
         tc.vbase = va;
+        tc.vals = p.d.vals;
+        tc.defs = p.d.defs;
+        tc.vals_len = p.d.vals_len;
+        tc.defs_len = p.d.defs_len;
+        tc.row_in_page = ra;
+        tc.remap = p.d.remap;
+        tc.dict_n = p.d.dict_n;
+        tc.bw = p.d.bw;
+        tc.kind = p.d.kind;
+        tc.has_nulls = p.d.has_nulls;
         if (p.d.kind == PAGE_DICT && p.run_n && ve > va) {
           uint32_t r0 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, va);
           uint32_t r1 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, ve - 1);

@@ -267,6 +267,11 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
 
   // ---- group dimensions ----
   const bool merged = !per_glob_rows;
+  // Merged min/max over values that can be NULL: NULL, "null" and "" group values stay apart in the table
+  // (each is its own DuckDB group, and an all-NULL group reads back 0.0); they collapse after per-glob
+  // finalization (rekey_minmax).  Everywhere else they can share a cell.
+  const bool min_max_nulls = (agg == AGG_MIN || agg == AGG_MAX) && value_nulls;
+  const bool collapse_in_table = merged && !min_max_nulls;
   for (size_t s = 0; s < strs.size(); s++) {
     StrCol& sc = strs[s];
     sc.is_dim = (s == 0) || std::find(gbs.begin(), gbs.end(), sc.name) != gbs.end();
@@ -303,7 +308,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     GlobalDict& gd = E.dict(sc.name);
     std::lock_guard<std::mutex> g(gd.mu);
     bool null_like_present = gd.ids.count("null") || gd.ids.count("");
-    need_tab[s] = !sc.leaves.empty() || sc.restricted || (sc.is_dim && merged && null_like_present) ||
+    need_tab[s] = !sc.leaves.empty() || sc.restricted || (sc.is_dim && collapse_in_table && null_like_present) ||
                   (!sc.is_dim && sc.leaves.empty());
     if (!need_tab[s]) continue;
     std::vector<std::regex> res(sc.leaves.size());
@@ -330,9 +335,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
         if (sc.restricted) {
           auto it = std::find(sc.cand.begin(), sc.cand.end(), v);
           dim = it == sc.cand.end() ? sc.dim_null : uint32_t(it - sc.cand.begin());
-          if (merged && null_like(v)) dim = sc.dim_null;
+          if (collapse_in_table && null_like(v)) dim = sc.dim_null;
         } else {
-          dim = (merged && null_like(v)) ? sc.dim_null : gid;
+          dim = (collapse_in_table && null_like(v)) ? sc.dim_null : gid;
         }
       }
       tab[gid] = (bits << 24) | dim;
@@ -355,7 +360,27 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     int64_t last_b = metrics ? last : last - last % step;
     nbuckets = uint64_t((last_b - bucket_base) / step + 1);
   }
-  const bool per_glob_cells = per_glob_rows || ((agg == AGG_MIN || agg == AGG_MAX) && value_nulls);
+  const bool per_glob_cells = per_glob_rows || min_max_nulls;
+  // dims whose null-like values must be folded after per-glob finalization
+  std::vector<std::vector<uint32_t>> fold_maps(strs.size());
+  bool rekey = false;
+  if (merged && min_max_nulls && !gbs.empty()) {
+    for (size_t s = 0; s < strs.size(); s++) {
+      StrCol& sc = strs[s];
+      if (!sc.is_dim) continue;
+      GlobalDict& gd = E.dict(sc.name);
+      std::lock_guard<std::mutex> g(gd.mu);
+      std::vector<uint32_t> m(sc.ndim);
+      bool any = false;
+      for (uint32_t d = 0; d < sc.ndim; d++) {
+        m[d] = d;
+        if (d == sc.dim_null) continue;
+        const std::string& v = sc.restricted ? sc.cand[d] : gd.vals[d];
+        if (null_like(v)) { m[d] = sc.dim_null; any = true; }
+      }
+      if (any) { fold_maps[s] = std::move(m); rekey = true; }
+    }
+  }
   const uint32_t nslots = per_glob_cells ? uint32_t(globs.size()) : 1u;
   const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
   if (ncells > (1ull << 28)) throw PlanError(LK_ERR_UNSUPPORTED, "aggregation table too large (" + std::to_string(ncells) + " cells)");
@@ -406,6 +431,41 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     }
   }
 
+  if (seg_begin.size() > 65535) throw PlanError(LK_ERR_UNSUPPORTED, "more than 65535 segments in one evaluation");
+  uint32_t max_tiles = 0;
+  for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
+  // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
+  std::vector<uint32_t> truth;
+  if (leaves.size() <= size_t(TT_MAX_LEAVES)) {
+    const uint32_t L = uint32_t(leaves.size());
+    truth.assign(((1u << (2 * L)) + 31) / 32, 0u);
+    for (uint32_t idx = 0; idx < (1u << (2 * L)); idx++) {
+      const uint32_t T = idx & ((1u << L) - 1), F = idx >> L;
+      uint64_t st = 0, sf = 0;
+      for (uint8_t op : prog) {
+        if (op < 0x80) {
+          st = (st << 1) | ((T >> op) & 1u);
+          sf = (sf << 1) | ((F >> op) & 1u);
+        } else if (op == OP_NOT) {
+          uint64_t t1 = st & 1, f1 = sf & 1;
+          st = (st & ~1ull) | f1;
+          sf = (sf & ~1ull) | t1;
+        } else {
+          uint64_t t2 = st & 1, f2 = sf & 1;
+          st >>= 1;
+          sf >>= 1;
+          uint64_t t1 = st & 1, f1 = sf & 1;
+          uint64_t tt = op == OP_AND ? (t1 & t2) : (t1 | t2);
+          uint64_t ff = op == OP_AND ? (f1 | f2) : (f1 & f2);
+          st = (st & ~1ull) | tt;
+          sf = (sf & ~1ull) | ff;
+        }
+      }
+      if (st & 1) truth[idx >> 5] |= 1u << (idx & 31);
+    }
+  }
+  if (total_tiles >= (1u << 31)) throw PlanError(LK_ERR_UNSUPPORTED, "too many tiles");
+
   // ---- device: upload, zero table, scan ----
   std::lock_guard<std::mutex> dev_guard(E.dev_mu);
   HIP_TRY(hipSetDevice(E.device));
@@ -413,6 +473,10 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   QParams P{};
   P.nsegs = uint32_t(qsegs.size());
   P.total_tiles = total_tiles;
+  P.max_tiles = max_tiles;
+  P.fast_div = (step > 0 && step < (int64_t(1) << 31) && nbuckets &&
+                max_hi - bucket_base < (int64_t(1) << 32)) ? 1 : 0;
+  P.inv_step = 1.0 / double(step > 0 ? step : 1);
   P.nstr = uint32_t(strs.size());
   P.nleaves = uint32_t(leaves.size());
   P.nprog = uint32_t(prog.size());
@@ -422,35 +486,43 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   P.nbuckets = nbuckets;
   P.ngroups = ngroups;
   P.ncells = ncells;
+  std::vector<StrParam> strp(strs.size());
   for (size_t s = 0; s < strs.size(); s++) {
-    P.dim_null[s] = strs[s].dim_null;
-    P.dim_stride[s] = strs[s].is_dim ? strs[s].stride : 0;
-    P.str_lbase[s] = strs[s].lbase;
-    P.str_lmask[s] = strs[s].lmask;
-    P.str_hmask[s] = strs[s].hmask;
+    strp[s].dim_null = strs[s].dim_null;
+    strp[s].dim_stride = strs[s].is_dim ? uint32_t(strs[s].stride) : 0u;
+    strp[s].lbase = strs[s].lbase;
+    strp[s].lmask = strs[s].lmask;
+    strp[s].hmask = strs[s].hmask;
   }
   memcpy(P.prog, prog.data(), prog.size());
+  if (const char* ab = getenv("LK_ABLATE")) P.ablate = uint32_t(atoi(ab));   // diagnostics only
 
   // staging layout in one pinned buffer + one device workspace
   size_t off = 0;
   auto reserve = [&](size_t n) { size_t o = (off + 255) / 256 * 256; off = o + n; return o; };
   const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
-  const size_t o_begin = reserve(seg_begin.size() * sizeof(uint32_t));
+  const size_t o_truth = reserve(truth.size() * 4);
   std::vector<size_t> o_tab(strs.size());
   for (size_t s = 0; s < strs.size(); s++) o_tab[s] = need_tab[s] ? reserve(tabs[s].size() * 4) : 0;
   const size_t o_flags = reserve(sizeof(uint32_t) * 4);
+  const size_t o_strp = reserve(strp.size() * sizeof(StrParam));
   std::vector<uint32_t> name_rank;
   const bool collapse = merged && gbs.empty();
   if (collapse && strs[0].is_dim) {
     // "tags of the first input" (TimeGroupedSketchAggregator.scala:57-60) is arrival-order dependent in the
     // reference; we pick the smallest name string among the merged cells, deterministically.
-    std::vector<std::pair<std::string, uint32_t>> order;
+    // Order = the row's resulting tag map as a sorted (key, value) list: {"name": v}, or the first glob's
+    // queryTags when the name is NULL / "null" / "" (Commons.scala:433, 450-452).
+    using TagList = std::vector<std::pair<std::string, std::string>>;
+    TagList qt = globs[0].query_tags;
+    std::sort(qt.begin(), qt.end());
+    std::vector<std::pair<TagList, uint32_t>> order;
     GlobalDict& gd = E.dict(kName);
     std::lock_guard<std::mutex> g(gd.mu);
     for (uint32_t d = 0; d < strs[0].ndim; d++) {
-      std::string v = d == strs[0].dim_null ? std::string("\xff\xff") :
-                      (strs[0].restricted ? strs[0].cand[d] : gd.vals[d]);
-      order.emplace_back(v, d);
+      const std::string* v = d == strs[0].dim_null ? nullptr : (strs[0].restricted ? &strs[0].cand[d] : &gd.vals[d]);
+      if (v && !null_like(*v)) order.emplace_back(TagList{{"name", *v}}, d);
+      else order.emplace_back(qt, d);
     }
     std::sort(order.begin(), order.end());
     name_rank.assign(strs[0].ndim, 0);
@@ -462,18 +534,20 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   uint8_t* dbuf = static_cast<uint8_t*>(E.workspace("query", stage_bytes));
   for (auto& q : qsegs) (void)q;
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
-  memcpy(hbuf + o_begin, seg_begin.data(), seg_begin.size() * sizeof(uint32_t));
+  if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
   for (size_t s = 0; s < strs.size(); s++)
     if (need_tab[s]) {
       memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
-      P.strtab[s] = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
+      strp[s].strtab = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
     }
+  memcpy(hbuf + o_strp, strp.data(), strp.size() * sizeof(StrParam));
   memset(hbuf + o_flags, 0, 16);
   if (!name_rank.empty()) memcpy(hbuf + o_rank, name_rank.data(), name_rank.size() * 4);
   HIP_TRY(hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st));
   P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
   P.flags = reinterpret_cast<uint32_t*>(dbuf + o_flags);
-  const uint32_t* d_seg_begin = reinterpret_cast<const uint32_t*>(dbuf + o_begin);
+  P.truth = truth.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_truth);
+  P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
 
   // aggregation table (SoA)
   const size_t nc = size_t(std::max<uint64_t>(ncells, 1));
@@ -489,23 +563,87 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, nc * 8, st));
   if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, nc * 8, st));
   HIP_TRY(hipEventRecord(E.ev_scan0, st));
-  if (ncells) HIP_TRY(launch_scan(P, d_seg_begin, kagg, st));
+  const size_t nstamp = size_t(P.max_tiles) * P.nsegs * 4;
+  if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
+    P.stamps = static_cast<unsigned long long*>(E.workspace("stamps", nstamp * 8));
+    HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
+  }
+  if (ncells) HIP_TRY(launch_scan(P, kagg, st));
+  if (P.stamps) {
+    std::vector<unsigned long long> h(nstamp);
+    HIP_TRY(hipMemcpyAsync(h.data(), P.stamps, nstamp * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    double s[4] = {0, 0, 0, 0};
+    size_t n = 0;
+    for (size_t i = 0; i < nstamp; i += 4) {
+      if (!h[i + 3]) continue;
+      for (int k = 0; k < 4; k++) s[k] += double(h[i + k]);
+      n++;
+    }
+    if (n)
+      fprintf(stderr, "[lk stamps] blocks=%zu mean cycles: prologue=%.0f phase1=%.0f phase2=%.0f total=%.0f\n", n,
+              s[0] / n, s[1] / n, s[2] / n, s[3] / n);
+  }
   HIP_TRY(hipEventRecord(E.ev_scan1, st));
 
   // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
   if (dist) comm_reduce_table(E, P, kagg, nc);
   const bool emit = !dist || rank == 0;
 
-  // ---- finalize + compaction ----
+  // ---- merged min/max with NULL-able values: fold null-like group values per glob-cell SQL value ----
   FParams F{};
   F.rows = P.rows;
   F.cnt = P.cnt;
   F.hi = P.hi;
   F.lo = P.lo;
   F.ext = P.ext;
+  uint32_t fslots = nslots;
+  if (rekey && emit && ncells) {
+    const size_t n2 = size_t(nbuckets * ngroups);
+    uint8_t* t2 = static_cast<uint8_t*>(E.workspace("table2", n2 * 24 + 256));
+    RParams RP{};
+    RP.in_rows = P.rows;
+    RP.in_cnt = P.cnt;
+    RP.in_ext = P.ext;
+    RP.ncells_in = ncells;
+    RP.out_rows = reinterpret_cast<unsigned long long*>(t2);
+    RP.out_cnt = reinterpret_cast<unsigned long long*>(t2 + n2 * 8);
+    RP.out_ext = reinterpret_cast<unsigned long long*>(t2 + n2 * 16);
+    RP.nbuckets = nbuckets;
+    RP.ngroups = ngroups;
+    RP.agg = kagg;
+    size_t moff = 0;
+    std::vector<uint32_t> flat;
+    std::vector<size_t> map_off(strs.size(), SIZE_MAX);
+    for (size_t s = 0; s < strs.size(); s++)
+      if (!fold_maps[s].empty()) {
+        map_off[s] = flat.size();
+        flat.insert(flat.end(), fold_maps[s].begin(), fold_maps[s].end());
+      }
+    uint32_t* dmaps = static_cast<uint32_t*>(E.workspace("foldmaps", flat.size() * 4 + 16));
+    HIP_TRY(hipMemcpyAsync(dmaps, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, st));
+    for (size_t s = 0; s < strs.size(); s++) {
+      if (!strs[s].is_dim) continue;
+      RP.stride[RP.ndims] = strs[s].stride;
+      RP.ndim[RP.ndims] = strs[s].ndim;
+      RP.map[RP.ndims] = map_off[s] == SIZE_MAX ? nullptr : dmaps + map_off[s];
+      RP.ndims++;
+    }
+    (void)moff;
+    HIP_TRY(hipMemsetAsync(t2, 0, n2 * 16, st));
+    HIP_TRY(hipMemsetAsync(RP.out_ext, kagg == AGG_MIN ? 0xff : 0, n2 * 8, st));
+    HIP_TRY(launch_rekey_minmax(RP, st));
+    HIP_TRY(hipStreamSynchronize(st));   // flat / maps staging is host memory owned by this frame
+    F.rows = RP.out_rows;
+    F.cnt = RP.out_cnt;
+    F.ext = RP.out_ext;
+    fslots = 1;
+  }
+
+  // ---- finalize + compaction ----
   F.ngroups = ngroups;
   F.nbuckets = nbuckets;
-  F.nglob_slots = nslots;
+  F.nglob_slots = fslots;
   F.agg = agg;
   F.per_glob = per_glob_rows ? 1 : 0;
   F.collapse = collapse ? 1 : 0;

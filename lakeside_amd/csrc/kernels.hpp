@@ -29,8 +29,27 @@ struct FParams {
 
 constexpr int AGG_AVG = 4;
 
+struct RParams {                   // rekey_minmax: per-glob uncollapsed table -> merged collapsed table
+  const unsigned long long* in_rows;
+  const unsigned long long* in_cnt;
+  const unsigned long long* in_ext;
+  unsigned long long ncells_in;
+  unsigned long long* out_rows;
+  unsigned long long* out_cnt;
+  unsigned long long* out_ext;
+  unsigned long long nbuckets;
+  unsigned long long ngroups;
+  int ndims;
+  int agg;
+  unsigned long long stride[MAXSTR];
+  unsigned long long ndim[MAXSTR];
+  const uint32_t* map[MAXSTR];     // dim id -> collapsed dim id (null: identity)
+};
+
+hipError_t launch_rekey_minmax(const RParams& R, hipStream_t stream);
+
 hipError_t launch_merge_dd(double* hi, double* lo, const double* parts, int world, size_t nc, hipStream_t stream);
-hipError_t launch_scan(const QParams& P, const uint32_t* d_seg_begin, int agg, hipStream_t stream);
+hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
 uint32_t finalize_blocks(unsigned long long nkeys);
 // d_counts must hold finalize_blocks(nkeys) + 1 entries; the row total lands in d_counts[nblocks].
 hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,

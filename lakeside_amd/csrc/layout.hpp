@@ -60,14 +60,26 @@ struct TileDesc {           // 32 B
   int64_t ts_max;
 };
 
-struct TileCol {            // 24 B
-  uint32_t page;            // index into the segment's page array
+struct TileCol {            // 64 B: everything the kernel needs about one column over one tile
+  uint64_t vals;            // byte offset (segment base) of the page's value stream
+  uint64_t defs;            // byte offset of the page's def-level stream
+  uint32_t vals_len;
+  uint32_t defs_len;
+  uint32_t row_in_page;     // first row of the tile within its page
+  uint32_t vbase;           // value index (within the page) of the tile's first non-null row
   uint32_t run_lo;          // first value-stream run overlapping the tile (index into the run array)
   uint32_t nruns;
   uint32_t drun_lo;         // first def-stream run overlapping the tile
   uint32_t ndruns;
-  uint32_t vbase;           // value index (within the page) of the tile's first non-null row
+  uint32_t remap;           // offset of the chunk's dictionary remap
+  uint32_t dict_n;          // dictionary size of the chunk
+  uint8_t bw;               // dictionary index bit width
+  uint8_t kind;             // PageKind
+  uint8_t has_nulls;        // the page has at least one NULL
+  uint8_t pad0;
+  uint32_t page;            // index into the segment's page array (host bookkeeping)
 };
+static_assert(sizeof(TileCol) == 64, "TileCol layout");
 
 struct QCol {               // one query column in one segment
   const PageDesc* pages;
@@ -81,8 +93,8 @@ struct QCol {               // one query column in one segment
 struct QSeg {
   const uint8_t* base;
   const TileDesc* tiles;
-  uint32_t tile_begin;      // prefix sum of tiles over the query's segments
-  uint32_t ntiles;
+  uint32_t tile_begin;      // prefix sum of tiles over the query's segments (stats only)
+  uint32_t ntiles;          // grid.x covers the largest segment; blocks past ntiles exit
   uint32_t glob_slot;       // glob index in the cell space (0 when globs are merged in the table)
   uint32_t leaf_false;      // leaves compiled to literal `false` for this segment's glob (BaseExpr.scala:462)
   int64_t win_lo;           // glob window [min startTs, max endTs) (Commons.scala:225-226)
@@ -93,10 +105,27 @@ struct QSeg {
 enum Agg : int { AGG_SUM = 0, AGG_MIN = 1, AGG_MAX = 2, AGG_COUNT = 3 };
 enum Op : uint8_t { OP_AND = 0x80, OP_OR = 0x81, OP_NOT = 0x82, OP_TRUE = 0x83 };   // < 0x80: push leaf
 
+constexpr int TT_MAX_LEAVES = 6;   // filters with <= 6 leaves run as a truth table (4^6 bits)
+
+struct StrParam {           // per string column of a query (device array; read inside the column loop)
+  const uint32_t* strtab;   // global id -> (leaf bits << 24) | dim id; null: identity dim, no leaves
+  uint32_t dim_null;        // dim id of NULL / absent
+  uint32_t dim_stride;      // 0: not a group dimension
+  uint32_t lbase;           // first leaf index of this column
+  uint32_t lmask;           // leaf-index mask of its leaves
+  uint32_t hmask;           // its `has`/`exists` leaves
+  uint32_t pad;
+};
+
 struct QParams {
   const QSeg* segs;
   uint32_t nsegs;
   uint32_t total_tiles;
+  uint32_t max_tiles;       // grid.x
+  const uint32_t* truth;    // filter truth table: bit (T | F << nleaves) = row passes; null: interpret prog
+  int32_t fast_div;         // 1: (ts - bucket_base) fits 32 bits for every window -> 32-bit bucket division
+  double inv_step;          // 1.0 / step
+  const StrParam* strp;     // [nstr]
   uint32_t nstr;            // string columns (query cols 2 .. 2+nstr)
   uint32_t nleaves;
   uint32_t nprog;
@@ -106,15 +135,6 @@ struct QParams {
   uint64_t nbuckets;
   uint64_t ngroups;
   uint64_t ncells;
-  // per string column
-  const uint32_t* strtab[MAXSTR];   // global id -> (leaf bits << 24) | dim id; null: identity dim, no leaves
-  uint32_t dim_null[MAXSTR];        // dim id of NULL / absent
-  uint64_t dim_stride[MAXSTR];      // 0: not a group dimension
-  // leaves: the leaves of string column s are the contiguous leaf indices lbase[s] .. (lmask[s] bits);
-  // bit i of the column's packed leaf bits is leaf lbase[s] + i
-  uint32_t str_lbase[MAXSTR];
-  uint32_t str_lmask[MAXSTR];       // global leaf-index mask of the column's leaves
-  uint32_t str_hmask[MAXSTR];       // of those, `has`/`exists` leaves (IS NOT NULL: FALSE on NULL, never NULL)
   uint8_t prog[MAXPROG];
   // aggregation table (structure of arrays, ncells each)
   unsigned long long* rows;         // rows that passed the filter (cell existence)
@@ -123,6 +143,8 @@ struct QParams {
   double* lo;
   unsigned long long* ext;          // min/max as order-preserving u64
   uint32_t* flags;                  // error / diagnostic flags
+  uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
+  unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
 };
 
 enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u };
