@@ -3,21 +3,29 @@
 // grid (tile, segment); one 256-thread workgroup per tile (a row range inside one page of every column).
 //   prologue: every fact about the tile's columns (stream pointers, run windows, value bases, flags) is read
 //     once and staged in LDS together with the run windows, small dictionaries' lookup values (dictionary index
-//     -> leaf bits | group-dim id) and the filter truth table;
-//   per 2048-row sub-tile (thread owns rows j*256 + tid, j < 8: every 64-row group is one wave, contiguous)
-//   phase 1, one string column at a time: definition levels (ballot + popcount + LDS prefix -> value index),
-//     dictionary indices (branch-free buffer loads, all 8 in flight, run lookup in LDS), folded into the row's
-//     leaf T/F bits and group id held in registers; then the truth table (Kleene logic precomputed on the host)
-//     gives the pass bitmap (one ballot per 64 rows) and the group ids, both to LDS;
-//   phase 2: every timestamp/value load of the sub-tile is issued before the first use; non-passing lanes use
-//     an out-of-range buffer offset, which the hardware drops (late materialization without branches); bucket
-//     by exact 32-bit reciprocal division; accumulate in a per-thread register cell (time-sorted rows hit it),
-//     spilling to an LDS hash table (LDS atomics; sums as compensated hi/lo via returning-atomic TwoSum);
+//     -> leaf bits | group-dim id) and the filter truth table.
+//   Per 2048-row sub-tile:
+//   1. definition levels of every nullable column, run-major: thread i unpacks the byte of rows 8i..8i+7
+//      (one bit-packed byte, or the RLE value) into an LDS validity bitmap; one wave per column turns the
+//      bitmap into per-64-row prefix counts (value index of every row);
+//   2. string columns, one at a time, value-major: thread i unpacks the 8 dictionary indices 8i..8i+7 of the
+//      sub-tile's values from one bit-packed group (one or two dword loads, shifts) and writes their lookup
+//      values to LDS; then every row (k-major: row j*256 + tid) folds its value into leaf T/F bits and its
+//      group id, in registers;
+//   3. the filter's truth table (Kleene logic precomputed on the host) gives the pass bit of every row
+//      (one ballot per 64 rows); passing rows are compacted, in row order, into an LDS list;
+//   4. streaming: timestamps and values are loaded only for listed rows, all loads of a thread issued before
+//      the first use; bucket by exact 32-bit reciprocal division; accumulate in a per-thread register cell
+//      (time-sorted rows hit it), spilling to an LDS hash table (LDS atomics; sums as compensated hi/lo with a
+//      returning-atomic TwoSum).
 //   tile end: LDS cells -> global table with device atomics (count/min/max exact, sums within 1 ulp).
 #pragma once
 #include "device_common.hpp"
 
 namespace lk {
+
+constexpr int WORDS = SUBT / 64;         // 64-row groups per sub-tile (32)
+constexpr int PS = 4;                    // listed rows per thread loaded together in phase 4
 
 struct ColHot {                          // one column over one tile, staged once per tile
   const uint8_t* vals;                   // value stream (absolute)
@@ -30,7 +38,7 @@ struct ColHot {                          // one column over one tile, staged onc
 
 template <int NSTR>
 struct Lds {
-  LRun pool[(2 + NSTR) * 2 * RUN_CAP];   // run windows: [column][value runs | def runs]
+  LRun pool[(2 + NSTR) * 2 * (RUN_CAP + 1)];   // run windows: [column][value runs | def runs], + sentinel
   uint32_t lut[NSTR][LUT_CAP];
   uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
   unsigned long long hkey[HCAP];
@@ -38,12 +46,14 @@ struct Lds {
   uint32_t hcnt[HCAP];
   double hhi[HCAP];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
   double hlo[HCAP];
-  unsigned long long passw[SUBT / 64];   // phase 1 -> 2: predicate bitmap of the sub-tile
-  uint32_t gidl[SUBT];                   // phase 1 -> 2: group id per row
-  unsigned long long nvw[2][SUBT / 64];  // timestamp / value validity bits (nullable pages)
-  uint32_t npre[2][SUBT / 64];           // their exclusive prefix (+ running base)
-  uint32_t wsum[2 + NSTR][BLOCK / 64];   // per-wave valid counts (string def-level prefix)
-  uint32_t vrun[2 + NSTR];               // running non-null count since the tile start (nullable pages)
+  uint32_t pk[SUBT];                     // decoded lookup values of one string column (value-major); after the
+                                         //   last column's fold: the group id of every row (phases 3-4)
+  uint16_t list[SUBT];                   // passing rows, in row order
+  unsigned long long passw[WORDS];       // pass bitmap
+  uint32_t ppre[WORDS + 1];              // its exclusive prefix (+ total)
+  unsigned long long nv[2 + NSTR][WORDS];  // validity bitmaps (nullable columns)
+  uint32_t npre[2 + NSTR][WORDS + 1];    // their exclusive prefix within the sub-tile (+ total)
+  uint32_t vrun[2 + NSTR];               // non-null values of the column before this sub-tile (tile-relative)
   ColHot hot[2 + NSTR];                  // per-tile column state
   StrParam sp[NSTR];                     // per-query string column parameters
   int64_t win_lo, win_hi;
@@ -76,30 +86,6 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const 
     h = (h + 1) & (HCAP - 1);
   }
   global_merge<AGG>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
-}
-
-// Value index (relative to the tile's first non-null row) of this thread's row in one slice of a nullable
-// string column: non-null rows before it in the tile.  Wave part: ballot + popcount; block part: LDS; the
-// running count since the tile start lives in L.vrun[c] (read between the barriers, advanced by thread 0 after
-// the second one, so the next slice's reads are ordered behind the write).
-template <int NSTR>
-__device__ __forceinline__ uint32_t block_prefix(Lds<NSTR>& L, int c, bool valid) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  unsigned long long m = __ballot(valid);
-  uint32_t pre = __popcll(m & ((1ull << lane) - 1ull));
-  if (lane == 0) L.wsum[c][wave] = __popcll(m);
-  __syncthreads();
-  uint32_t base = 0, total = 0;
-#pragma unroll
-  for (int w = 0; w < BLOCK / 64; w++) {
-    uint32_t s = L.wsum[c][w];
-    base += (w < wave) ? s : 0;
-    total += s;
-  }
-  const uint32_t run = L.vrun[c];
-  __syncthreads();
-  if (threadIdx.x == 0) L.vrun[c] = run + total;
-  return run + base + pre;
 }
 
 // Kleene evaluation of the postfix program (filters with more than TT_MAX_LEAVES leaves).
@@ -137,10 +123,47 @@ __device__ __forceinline__ const T* uptr(const T* p) {
   return reinterpret_cast<const T*>(uni_ptr(reinterpret_cast<const uint8_t*>(p)));
 }
 
+// 8 consecutive values [v, v+8) of a hybrid stream (runs staged in LDS, `n` runs + sentinel), bit width
+// bw <= 8: one bit-packed group (bw bytes) or the RLE value; other cases fall back to per-value reads.
+__device__ __forceinline__ void hybrid_get8(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
+                                            uint32_t out[8]) {
+  const int ri = find_run64(runs, n, v);
+  const LRun r = runs[ri];
+  const uint32_t end = runs[ri + 1].start;   // sentinel past the last run
+  const bool lit = (r.off_lit & 0x80000000u) != 0;
+  const bool whole = v + 8 <= end;
+  if (whole && !lit) {
+#pragma unroll
+    for (int e = 0; e < 8; e++) out[e] = r.value;
+    return;
+  }
+  if (whole && bw <= 8) {
+    // 8 values = 8*bw <= 64 bits starting at bit `bit`; the 96 bits from the enclosing dword cover them
+    const uint32_t bit = (v - r.start) * uint32_t(bw);
+    const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
+    const uint32_t al = byte & ~3u;
+    const v2u w01 = __builtin_amdgcn_raw_buffer_load_b64(rs, al, 0, 0);
+    const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 8, 0, 0);
+    const uint32_t sh = (byte & 3u) * 8u + (bit & 7u);                       // <= 31
+    const uint64_t lo = ((uint64_t)w01.y << 32) | w01.x;
+    const uint64_t x = sh ? ((lo >> sh) | ((uint64_t)w2 << (64 - sh))) : lo;
+    const uint32_t mask = (1u << bw) - 1u;
+#pragma unroll
+    for (int e = 0; e < 8; e++) out[e] = uint32_t(x >> (e * bw)) & mask;
+    return;
+  }
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const uint32_t ve = v + e;
+    out[e] = hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, bw);
+  }
+}
+
 template <int AGG, int NSTR>
 __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
+  constexpr int PSTRIDE = 2 * (RUN_CAP + 1);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const unsigned long long lane_lt = (1ull << lane) - 1ull;
@@ -190,16 +213,18 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
     if (!uni(L.hot[c].present)) continue;
     const TileCol* tc = Sp->cols[c].tcols + t;
     const RunDesc* runs = Sp->cols[c].runs;
-    LRun* vp = L.pool + c * 2 * RUN_CAP;
+    LRun* vp = L.pool + c * PSTRIDE;
     const uint32_t nr = uni(L.hot[c].nruns), nd = uni(L.hot[c].ndruns);
     const uint32_t rlo = tc->run_lo, dlo = tc->drun_lo;
     for (uint32_t i = tid; i < nr; i += BLOCK) {
       const RunDesc r = runs[rlo + i];
       vp[i] = LRun{r.start, r.off_lit, r.value};
+      if (i == nr - 1) vp[nr] = LRun{r.start + r.count, 0u, 0u};          // sentinel: end of the last run
     }
     for (uint32_t i = tid; i < nd; i += BLOCK) {
       const RunDesc r = runs[dlo + i];
-      vp[RUN_CAP + i] = LRun{r.start, r.off_lit, r.value};
+      vp[RUN_CAP + 1 + i] = LRun{r.start, r.off_lit, r.value};
+      if (i == nd - 1) vp[RUN_CAP + 1 + nd] = LRun{r.start + r.count, 0u, 0u};
     }
   }
 #pragma unroll
@@ -234,93 +259,119 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
   unsigned long long st_pro = stamp ? __builtin_amdgcn_s_memtime() : 0, st_p1 = 0, st_p2 = 0, st_mark = st_pro;
 
   for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
-    // ============ phase 1: one string column at a time ============
-    uint32_t leafT[SLOTS], leafF[SLOTS], gid[SLOTS];
-    bool inrow[SLOTS];
+    const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
+
+    // ============ 1. validity bitmaps of nullable columns (run-major, 8 rows per thread) ============
+    bool any_nulls = false;
 #pragma unroll
-    for (int j = 0; j < SLOTS; j++) {
-      leafT[j] = 0;
-      leafF[j] = 0;
-      gid[j] = 0;
-      inrow[j] = sub + j * BLOCK + tid < tile_nrows;
+    for (int c = 0; c < NC; c++) {
+      if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
+      any_nulls = true;
+      const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
+      const LRun* druns = L.pool + c * PSTRIDE + RUN_CAP + 1;
+      const int nd = int(uni(L.hot[c].ndruns));
+      const uint32_t r0 = uni(L.hot[c].rip) + sub + 8 * tid;    // rows 8*tid .. 8*tid+7 of the sub-tile
+      uint32_t bits = 0;
+      if (8 * uint32_t(tid) < nsub) {
+        uint32_t d[8];
+        hybrid_get8(drs, druns, nd, r0, 1, d);
+#pragma unroll
+        for (int e = 0; e < 8; e++) bits |= (d[e] & 1u) << e;
+        const uint32_t left = nsub - 8 * tid;
+        if (left < 8) bits &= (1u << left) - 1u;
+      }
+      reinterpret_cast<uint8_t*>(L.nv[c])[tid] = uint8_t(bits);
     }
+    if (any_nulls) {
+      __syncthreads();
+      // per-64-row prefix counts (one wave per column; WORDS = 32 <= 64 lanes)
+      for (int c = wave; c < NC; c += BLOCK / 64) {
+        if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
+        const uint32_t cnt = lane < WORDS ? __popcll(L.nv[c][lane]) : 0u;
+        uint32_t x = cnt;
+        for (int o = 1; o < 64; o <<= 1) {
+          const uint32_t y = __shfl_up(x, o, 64);
+          if (lane >= o) x += y;
+        }
+        if (lane < WORDS) L.npre[c][lane] = x - cnt;
+        if (lane == WORDS - 1) L.npre[c][WORDS] = x;
+      }
+      __syncthreads();
+    }
+
+    // ============ 2. string columns: value-major decode to LDS, then fold per row ============
+    uint32_t leafT[SLOTS], leafF[SLOTS], gid[SLOTS];
+#pragma unroll
+    for (int j = 0; j < SLOTS; j++) leafT[j] = 0, leafF[j] = 0, gid[j] = 0;
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
-      uint32_t packed[SLOTS];
-      bool isnull[SLOTS];
+      const bool present = uni(L.hot[c].present) != 0;
+      const bool nullable = present && uni(L.hot[c].has_nulls) != 0;
+      const uint32_t nr = present ? uni(L.hot[c].nruns) : 0u;
+      if (nr) {
+        // values of this sub-tile: [vs, vs + nvals)
+        const uint32_t vs = uni(L.hot[c].vbase) + (nullable ? uni(L.vrun[c]) : sub);
+        const uint32_t nvals = nullable ? uni(L.npre[c][WORDS]) : nsub;
+        const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
+        const LRun* runs = L.pool + c * PSTRIDE;
+        const int bw = int(uni(L.hot[c].bw));
+        const bool lut = uni(L.hot[c].lut_on) != 0;
+        if (8 * uint32_t(tid) < nvals) {
+          uint32_t idx[8];
+          hybrid_get8(vrs, runs, int(nr), vs + 8 * tid, bw, idx);
+          if (lut) {
 #pragma unroll
-      for (int j = 0; j < SLOTS; j++) isnull[j] = true, packed[j] = 0;
-      if (uni(L.hot[c].present)) {
-        const uint32_t vbase = uni(L.hot[c].vbase);
-        uint32_t vidx[SLOTS];
-        if (uni(L.hot[c].has_nulls)) {
-          const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
-          const LRun* druns = L.pool + c * 2 * RUN_CAP + RUN_CAP;
-          const int nd = int(uni(L.hot[c].ndruns));
-          const uint32_t rip = uni(L.hot[c].rip);
-          bool valid[SLOTS];
-#pragma unroll
-          for (int j = 0; j < SLOTS; j++) {
-            const uint32_t r = rip + min(sub + j * BLOCK + tid, tile_nrows - 1);
-            valid[j] = inrow[j] && hybrid_get_buf(drs, druns[find_run64(druns, nd, r)], r, 1) != 0;
-          }
-#pragma unroll
-          for (int j = 0; j < SLOTS; j++) {
-            vidx[j] = vbase + block_prefix(L, c, valid[j]);
-            isnull[j] = !valid[j];
-          }
-        } else {
-#pragma unroll
-          for (int j = 0; j < SLOTS; j++) {
-            vidx[j] = vbase + sub + j * BLOCK + tid;
-            isnull[j] = !inrow[j];
-          }
-        }
-        const uint32_t nr = uni(L.hot[c].nruns);
-        if (nr) {
-          const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
-          const LRun* runs = L.pool + c * 2 * RUN_CAP;
-          const int bw = int(uni(L.hot[c].bw));
-          uint32_t idx[SLOTS];
-#pragma unroll
-          for (int j = 0; j < SLOTS; j++) {
-            const uint32_t v = isnull[j] ? vbase : vidx[j];      // branch-free: NULL rows decode a valid value
-            idx[j] = hybrid_get_buf(vrs, runs[find_run64(runs, int(nr), v)], v, bw);
-          }
-          if (uni(L.hot[c].lut_on)) {
-#pragma unroll
-            for (int j = 0; j < SLOTS; j++) packed[j] = isnull[j] ? 0u : L.lut[s][idx[j]];
+            for (int e = 0; e < 8; e++) L.pk[8 * tid + e] = L.lut[s][idx[e] < LUT_CAP ? idx[e] : 0];
           } else {
             const uint32_t* remap = uptr(L.hot[c].remap);
             const uint32_t* tab = uptr(L.sp[s].strtab);
+            const uint32_t left = nvals - 8 * tid;
 #pragma unroll
-            for (int j = 0; j < SLOTS; j++) {
-              const uint32_t g = remap[idx[j]];
-              packed[j] = isnull[j] ? 0u : (tab ? tab[g] : g);
+            for (int e = 0; e < 8; e++) {
+              const uint32_t g = remap[e < int(left) ? idx[e] : idx[0]];
+              L.pk[8 * tid + e] = tab ? tab[g] : g;
             }
           }
         }
+        __syncthreads();
       }
-      // fold: group dimension + leaves of this column
       const uint32_t dstride = uni(L.sp[s].dim_stride), dnull = uni(L.sp[s].dim_null);
       const uint32_t lbase = uni(L.sp[s].lbase), lmask = uni(L.sp[s].lmask), hmask = uni(L.sp[s].hmask);
 #pragma unroll
       for (int j = 0; j < SLOTS; j++) {
-        const uint32_t bits = (packed[j] >> 24) << lbase;
-        const uint32_t dim = isnull[j] ? dnull : (packed[j] & DIM_MASK);
+        const uint32_t r = j * BLOCK + tid;   // row within the sub-tile
+        const int w = r >> 6;
+        bool valid = false;
+        uint32_t vi = 0;
+        if (nr && nullable) {
+          const unsigned long long m = L.nv[c][w];
+          valid = (m >> lane) & 1ull;
+          vi = L.npre[c][w] + __popcll(m & lane_lt);
+        } else if (nr) {
+          valid = r < nsub;
+          vi = r;
+        }
+        const uint32_t packed = valid ? L.pk[vi] : 0u;
+        const uint32_t bits = (packed >> 24) << lbase;
+        const uint32_t dim = valid ? (packed & DIM_MASK) : dnull;
         gid[j] += dim * dstride;
-        leafT[j] |= isnull[j] ? 0u : (bits & lmask);
-        leafF[j] |= isnull[j] ? hmask : (~bits & lmask);   // IS NOT NULL on NULL: FALSE; others NULL
+        leafT[j] |= valid ? (bits & lmask) : 0u;
+        leafF[j] |= valid ? (~bits & lmask) : hmask;   // IS NOT NULL on NULL: FALSE; others NULL
       }
+      if (nr) __syncthreads();   // the next column reuses pk
     }
-    // filter: truth table over the leaves' (T, F) bits (Kleene logic precomputed on the host)
+
+    // ============ 3. filter (truth table) -> pass bitmap, group ids; compaction ============
     {
       const uint32_t leaf_false = uni(L.leaf_false);
       const uint32_t nleaves = P.nleaves;
       const bool use_truth = P.truth != nullptr;
+      const bool ts_null = uni(L.hot[0].has_nulls) != 0 && uni(L.hot[0].present) != 0;
+      const bool ts_present = uni(L.hot[0].present) != 0;
 #pragma unroll
       for (int j = 0; j < SLOTS; j++) {
+        const uint32_t r = j * BLOCK + tid;
         const uint32_t T = leafT[j] & ~leaf_false, F = leafF[j] | leaf_false;
         bool ok;
         if (use_truth) {
@@ -329,104 +380,95 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
         } else {
           ok = interpret(P, T, F);
         }
-        const bool pass = (P.ablate & 2) ? (inrow[j] && (tid & 15) == 0) : (inrow[j] && ok);
+        if (P.ablate & 2) ok = (tid & 15) == 0;
+        bool pass = ok && r < nsub && ts_present;
+        if (ts_null) pass = pass && ((L.nv[0][r >> 6] >> lane) & 1ull);   // NULL timestamp fails the window
         const unsigned long long pm = __ballot(pass);
-        if (lane == 0) L.passw[j * (BLOCK / 64) + wave] = pm;
-        L.gidl[j * BLOCK + tid] = gid[j];
-      }
-    }
-    // timestamp / value validity (nullable pages): one bit per row
-    const bool nn0 = uni(L.hot[0].has_nulls) != 0, nn1 = uni(L.hot[1].has_nulls) != 0;
-#pragma unroll
-    for (int c = 0; c < 2; c++) {
-      if (!(c == 0 ? nn0 : nn1)) continue;
-      const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
-      const LRun* druns = L.pool + c * 2 * RUN_CAP + RUN_CAP;
-      const int nd = int(uni(L.hot[c].ndruns));
-      const uint32_t rip = uni(L.hot[c].rip);
-#pragma unroll
-      for (int j = 0; j < SLOTS; j++) {
-        const uint32_t r = rip + min(sub + j * BLOCK + tid, tile_nrows - 1);
-        const bool v = inrow[j] && hybrid_get_buf(drs, druns[find_run64(druns, nd, r)], r, 1) != 0;
-        const unsigned long long vm = __ballot(v);
-        if (lane == 0) L.nvw[c][j * (BLOCK / 64) + wave] = vm;
+        if (lane == 0) L.passw[r >> 6] = pm;
+        L.pk[r] = gid[j];   // pk is free: every fold that read it ended with a barrier
       }
     }
     __syncthreads();
-    // exclusive prefix of valid rows per 64-row group (nullable timestamp / value pages)
-    if (nn0 || nn1) {
-      if ((wave == 0 && nn0) || (wave == 1 && nn1)) {
-        const int c = wave;
-        uint32_t cnt = lane < SUBT / 64 ? __popcll(L.nvw[c][lane]) : 0;
-        uint32_t x = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-          uint32_t y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        const uint32_t rb = L.vrun[c];
-        if (lane < SUBT / 64) L.npre[c][lane] = rb + x - cnt;
-        const uint32_t tot = __shfl(x, 63, 64);
-        if (lane == 0) L.vrun[c] = rb + tot;
+    if (wave == 0) {
+      const uint32_t cnt = lane < WORDS ? __popcll(L.passw[lane]) : 0u;
+      uint32_t x = cnt;
+      for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
       }
-      __syncthreads();
+      if (lane < WORDS) L.ppre[lane] = x - cnt;
+      if (lane == WORDS - 1) L.ppre[WORDS] = x;
     }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < SLOTS; j++) {
+      const uint32_t r = j * BLOCK + tid;
+      const unsigned long long m = L.passw[r >> 6];
+      if ((m >> lane) & 1ull) L.list[L.ppre[r >> 6] + __popcll(m & lane_lt)] = uint16_t(r);
+    }
+    __syncthreads();
     if (stamp) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
       st_p1 += now - st_mark;
       st_mark = now;
     }
-    if (P.ablate & 1) {
-      __syncthreads();
-      continue;
-    }
 
-    // ============ phase 2: stream timestamp + value of passing rows, bucket, aggregate ============
-    {
-      const bool pres0 = uni(L.hot[0].present) != 0, pres1 = uni(L.hot[1].present) != 0;
-      const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(L.hot[0].vals, pres0 ? L.hot[0].vals_len : 0u);
+    // ============ 4. stream timestamp + value of listed rows, bucket, aggregate ============
+    const uint32_t nlist = uni(L.ppre[WORDS]);
+    if (!(P.ablate & 1) && nlist) {
+      const bool pres1 = uni(L.hot[1].present) != 0;
+      const bool nn0 = uni(L.hot[0].has_nulls) != 0, nn1 = pres1 && uni(L.hot[1].has_nulls) != 0;
+      const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(L.hot[0].vals, L.hot[0].vals_len);
       const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(L.hot[1].vals, pres1 ? L.hot[1].vals_len : 0u);
-      const uint32_t vb0 = uni(L.hot[0].vbase), vb1 = uni(L.hot[1].vbase);
-      v2u tsr[SLOTS], vr[SLOTS];
-      bool pass[SLOTS], vok[SLOTS];
-#pragma unroll
-      for (int j = 0; j < SLOTS; j++) {
-        const int w = j * (BLOCK / 64) + wave;
-        bool p = ((L.passw[w] >> lane) & 1ull) && pres0;
-        uint32_t tv = vb0 + sub + j * BLOCK + tid;
-        if (nn0) {
-          const unsigned long long m = L.nvw[0][w];
-          p = p && ((m >> lane) & 1ull);
-          tv = vb0 + L.npre[0][w] + __popcll(m & lane_lt);
-        }
-        pass[j] = p;
-        tsr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, p ? tv * 8u : OOB, 0, 0);
-        bool vv = pres1;
-        uint32_t vi = vb1 + sub + j * BLOCK + tid;
-        if (nn1) {
-          const unsigned long long m = L.nvw[1][w];
-          vv = vv && ((m >> lane) & 1ull);
-          vi = vb1 + L.npre[1][w] + __popcll(m & lane_lt);
-        }
-        vok[j] = vv;
-        if (AGG != AGG_COUNT) vr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, (p && vv) ? vi * 8u : OOB, 0, 0);
-        else vr[j] = v2u{0u, 0u};
-      }
+      const uint32_t vb0 = uni(L.hot[0].vbase) + (nn0 ? uni(L.vrun[0]) : sub);
+      const uint32_t vb1 = uni(L.hot[1].vbase) + (nn1 ? uni(L.vrun[1]) : sub);
       const int64_t win_lo = L.win_lo, win_hi = L.win_hi;
       const unsigned long long glob_base = (unsigned long long)uni(L.glob_slot) * P.nbuckets;
       const uint32_t step32 = uint32_t(P.step);
+      for (uint32_t cb = 0; cb < nlist; cb += PS * BLOCK) {
+      v2u tsr[PS], vr[PS];
+      uint32_t rows[PS];
+      bool vok[PS];
 #pragma unroll
-      for (int j = 0; j < SLOTS; j++) {
+      for (int j = 0; j < PS; j++) {
+        tsr[j] = v2u{0u, 0u};
+        vr[j] = v2u{0u, 0u};
+        rows[j] = 0;
+        vok[j] = false;
+        if (cb + j * BLOCK >= nlist) continue;                                // uniform
+        const uint32_t e = cb + j * BLOCK + tid;
+        const bool live = e < nlist;
+        const uint32_t r = live ? L.list[e] : 0u;
+        rows[j] = r;
+        const int w = r >> 6, ln = r & 63;
+        const unsigned long long below = (1ull << ln) - 1ull;
+        const uint32_t tv = nn0 ? L.npre[0][w] + __popcll(L.nv[0][w] & below) : r;
+        tsr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+        bool vv = pres1;
+        uint32_t vi = r;
+        if (nn1) {
+          const unsigned long long m = L.nv[1][w];
+          vv = (m >> ln) & 1ull;
+          vi = L.npre[1][w] + __popcll(m & below);
+        }
+        vok[j] = vv && live;
+        if (AGG != AGG_COUNT) vr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, (live && vv) ? (vb1 + vi) * 8u : OOB, 0, 0);
+        else vr[j] = v2u{0u, 0u};
+      }
+#pragma unroll
+      for (int j = 0; j < PS; j++) {
+        if (cb + j * BLOCK >= nlist) break;                                   // uniform
         const int64_t ts = (int64_t)(((uint64_t)tsr[j].y << 32) | tsr[j].x);
-        bool ok = pass[j] && ts >= win_lo && ts < win_hi;            // BaseExpr.scala:159-161
+        bool ok = (cb + j * BLOCK + tid < nlist) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
         int64_t b = 0;
         if (P.fast_div) {
           // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
           const uint32_t d = uint32_t(ts - P.bucket_base);
           uint32_t q = uint32_t(double(d) * P.inv_step);
-          int64_t r = int64_t(d) - int64_t(q) * step32;
-          q = r < 0 ? q - 1 : (r >= int64_t(step32) ? q + 1 : q);
-          r = int64_t(d) - int64_t(q) * step32;
-          if (P.metrics && r != 0 && ok) {
+          int64_t rm = int64_t(d) - int64_t(q) * step32;
+          q = rm < 0 ? q - 1 : (rm >= int64_t(step32) ? q + 1 : q);
+          rm = int64_t(d) - int64_t(q) * step32;
+          if (P.metrics && rm != 0 && ok) {
             atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
             ok = false;
           }
@@ -448,7 +490,7 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
           atomicOr(P.flags, FLAG_CELL_RANGE);
           continue;
         }
-        const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + L.gidl[j * BLOCK + tid];
+        const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + L.pk[rows[j]];
         if (cell != acc.key) {
           lds_merge<AGG>(L, P, acc);
           acc_reset<AGG>(acc, cell);
@@ -456,8 +498,11 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
         const double v = __longlong_as_double((long long)(((uint64_t)vr[j].y << 32) | vr[j].x));
         acc_add<AGG>(acc, vok[j], v);
       }
+      }
     }
-    __syncthreads();   // phase 1 of the next sub-tile overwrites passw / gidl
+    __syncthreads();   // the next sub-tile overwrites the bitmaps, pk, list
+    // advance the per-column non-null counters (read next after the next sub-tile's validity barriers)
+    if (any_nulls && tid < NC && L.hot[tid].present && L.hot[tid].has_nulls) L.vrun[tid] += L.npre[tid][WORDS];
     if (stamp) {
       const unsigned long long now = __builtin_amdgcn_s_memtime();
       st_p2 += now - st_mark;
