@@ -563,7 +563,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, nc * 8, st));
   if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, nc * 8, st));
   HIP_TRY(hipEventRecord(E.ev_scan0, st));
-  const size_t nstamp = size_t(P.max_tiles) * P.nsegs * 4;
+  const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
   if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
     P.stamps = static_cast<unsigned long long*>(E.workspace("stamps", nstamp * 8));
     HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
@@ -573,16 +573,24 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     std::vector<unsigned long long> h(nstamp);
     HIP_TRY(hipMemcpyAsync(h.data(), P.stamps, nstamp * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    double s[4] = {0, 0, 0, 0};
+    static const char* names[LK_NSTAMP] = {"prologue", "defs", "decode", "fold", "filter", "compact", "prefetch", "stream"};
+    double s[LK_NSTAMP] = {};
     size_t n = 0;
-    for (size_t i = 0; i < nstamp; i += 4) {
-      if (!h[i + 3]) continue;
-      for (int k = 0; k < 4; k++) s[k] += double(h[i + k]);
+    for (size_t i = 0; i < nstamp; i += LK_NSTAMP) {
+      if (!(h[i] >> 63)) continue;   // block exited early (zone map / past the segment's tiles)
+      h[i] &= ~(1ull << 63);
+      for (int k = 0; k < LK_NSTAMP; k++) s[k] += double(h[i + k]);
       n++;
     }
-    if (n)
-      fprintf(stderr, "[lk stamps] blocks=%zu mean cycles: prologue=%.0f phase1=%.0f phase2=%.0f total=%.0f\n", n,
-              s[0] / n, s[1] / n, s[2] / n, s[3] / n);
+    if (n) {
+      double tot = 0;
+      std::string line;
+      for (int k = 0; k < LK_NSTAMP; k++) {
+        tot += s[k] / n;
+        line += std::string(" ") + names[k] + "=" + std::to_string(long(s[k] / n));
+      }
+      fprintf(stderr, "[lk stamps] blocks=%zu mean cycles:%s total=%.0f\n", n, line.c_str(), tot);
+    }
   }
   HIP_TRY(hipEventRecord(E.ev_scan1, st));
 

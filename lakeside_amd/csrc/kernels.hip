@@ -238,13 +238,17 @@ hipError_t launch_merge_dd(double* hi, double* lo, const double* parts, int worl
 template <int AGG>
 static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
   const dim3 block(BLOCK);
+  if (!P.truth) {   // > TT_MAX_LEAVES leaves: one generic instantiation interprets the Kleene program per row
+    hipLaunchKernelGGL((scan_tiles<AGG, MAXSTR, false>), grid, block, 0, st, P);
+    return;
+  }
   switch (P.nstr) {
-    case 1: hipLaunchKernelGGL((scan_tiles<AGG, 1>), grid, block, 0, st, P); break;
-    case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2>), grid, block, 0, st, P); break;
-    case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3>), grid, block, 0, st, P); break;
-    case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4>), grid, block, 0, st, P); break;
-    case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5>), grid, block, 0, st, P); break;
-    default: hipLaunchKernelGGL((scan_tiles<AGG, 6>), grid, block, 0, st, P); break;
+    case 1: hipLaunchKernelGGL((scan_tiles<AGG, 1, true>), grid, block, 0, st, P); break;
+    case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2, true>), grid, block, 0, st, P); break;
+    case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true>), grid, block, 0, st, P); break;
+    case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true>), grid, block, 0, st, P); break;
+    case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true>), grid, block, 0, st, P); break;
+    default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true>), grid, block, 0, st, P); break;
   }
 }
 

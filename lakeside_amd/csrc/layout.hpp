@@ -106,6 +106,7 @@ enum Agg : int { AGG_SUM = 0, AGG_MIN = 1, AGG_MAX = 2, AGG_COUNT = 3 };
 enum Op : uint8_t { OP_AND = 0x80, OP_OR = 0x81, OP_NOT = 0x82, OP_TRUE = 0x83 };   // < 0x80: push leaf
 
 constexpr int TT_MAX_LEAVES = 6;   // filters with <= 6 leaves run as a truth table (4^6 bits)
+constexpr int LK_NSTAMP = 8;       // diagnostics: per-block s_memtime section totals (scan_kernel.hpp)
 
 struct StrParam {           // per string column of a query (device array; read inside the column loop)
   const uint32_t* strtab;   // global id -> (leaf bits << 24) | dim id; null: identity dim, no leaves

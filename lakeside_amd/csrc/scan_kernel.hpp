@@ -1,31 +1,32 @@
-// scan_tiles<AGG, NSTR>: the fused decode -> filter -> bucket -> aggregate kernel (included by kernels.hip).
+// scan_tiles<AGG, NSTR, TT>: the fused decode -> filter -> bucket -> aggregate kernel (included by kernels.hip).
 //
 // grid (tile, segment); one 256-thread workgroup per tile (a row range inside one page of every column).
 //   prologue: every fact about the tile's columns (stream pointers, run windows, value bases, flags) is read
 //     once and staged in LDS together with the run windows, small dictionaries' lookup values (dictionary index
 //     -> leaf bits | group-dim id) and the filter truth table.
-//   Per 2048-row sub-tile:
-//   1. definition levels of every nullable column, run-major: thread i unpacks the byte of rows 8i..8i+7
-//      (one bit-packed byte, or the RLE value) into an LDS validity bitmap; one wave per column turns the
-//      bitmap into per-64-row prefix counts (value index of every row);
-//   2. string columns, one at a time, value-major: thread i unpacks the 8 dictionary indices 8i..8i+7 of the
-//      sub-tile's values from one bit-packed group (one or two dword loads, shifts) and writes their lookup
-//      values to LDS; then every row (k-major: row j*256 + tid) folds its value into leaf T/F bits and its
-//      group id, in registers;
-//   3. the filter's truth table (Kleene logic precomputed on the host) gives the pass bit of every row
-//      (one ballot per 64 rows); passing rows are compacted, in row order, into an LDS list;
-//   4. streaming: timestamps and values are loaded only for listed rows, all loads of a thread issued before
-//      the first use; bucket by exact 32-bit reciprocal division; accumulate in a per-thread register cell
-//      (time-sorted rows hit it), spilling to an LDS hash table (LDS atomics; sums as compensated hi/lo with a
-//      returning-atomic TwoSum).
+//   Per 2048-row sub-tile, thread t owns rows 8t..8t+7 (wave w: rows 512w..512w+511):
+//   A. definition levels of nullable columns: one packed byte per thread (bit e = row 8t+e is non-NULL); value
+//      indices from a bit-sliced ballot prefix (4 ballots + mbcnt) and the per-wave totals (one barrier);
+//   B. string columns: a non-NULL column's values 8t..8t+7 are the thread's rows: unpacked from one bit-packed
+//      group (one 96-bit load issued a sub-tile ahead) straight into registers; a nullable column's values are
+//      unpacked value-major into LDS and gathered by value index (two barriers). Every row folds its value into
+//      leaf T/F bits and its group id;
+//   C. the filter's truth table (Kleene logic precomputed on the host; TT=false interprets the program) -> a
+//      pass byte per thread;
+//   D. passing rows are compacted, in row order, into the wave's own LDS list (ballot prefix; no barrier);
+//   E. the wave streams timestamp + value of its listed rows only (late materialization), buckets by exact
+//      32-bit reciprocal division and accumulates in a per-thread register cell (time-sorted rows hit it),
+//      spilling to an LDS hash table (LDS atomics; sums as compensated hi/lo with a returning-atomic TwoSum).
 //   tile end: LDS cells -> global table with device atomics (count/min/max exact, sums within 1 ulp).
+// Without nullable columns the sub-tile loop has no workgroup barrier: the four waves run independently.
 #pragma once
 #include "device_common.hpp"
 
 namespace lk {
 
-constexpr int WORDS = SUBT / 64;         // 64-row groups per sub-tile (32)
-constexpr int PS = 4;                    // listed rows per thread loaded together in phase 4
+constexpr int WAVES = BLOCK / 64;        // 4
+constexpr int WROWS = SUBT / WAVES;      // rows per wave per sub-tile (512)
+constexpr int PS = 4;                    // listed rows per lane loaded together in phase E
 
 struct ColHot {                          // one column over one tile, staged once per tile
   const uint8_t* vals;                   // value stream (absolute)
@@ -46,18 +47,16 @@ struct Lds {
   uint32_t hcnt[HCAP];
   double hhi[HCAP];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
   double hlo[HCAP];
-  uint32_t pk[SUBT];                     // decoded lookup values of one string column (value-major); after the
-                                         //   last column's fold: the group id of every row (phases 3-4)
-  uint16_t list[SUBT];                   // passing rows, in row order
-  unsigned long long passw[WORDS];       // pass bitmap
-  uint32_t ppre[WORDS + 1];              // its exclusive prefix (+ total)
-  unsigned long long nv[2 + NSTR][WORDS];  // validity bitmaps (nullable columns)
-  uint32_t npre[2 + NSTR][WORDS + 1];    // their exclusive prefix within the sub-tile (+ total)
-  uint32_t vrun[2 + NSTR];               // non-null values of the column before this sub-tile (tile-relative)
+  uint32_t pk[SUBT];                     // nullable string column: lookup values, value-major; otherwise each
+                                         //   thread's own 8 slots (scratch of the straddling-group decode)
+  uint2 list[WAVES][WROWS];              // per wave: passing rows {group id, ts index | value index << 11 |
+                                         //   value valid << 22} (indices relative to the sub-tile's values)
+  uint32_t wsum[2 + NSTR][WAVES];        // per nullable column: non-NULL rows of each wave in the sub-tile
   ColHot hot[2 + NSTR];                  // per-tile column state
   StrParam sp[NSTR];                     // per-query string column parameters
   int64_t win_lo, win_hi;
   uint32_t glob_slot, leaf_false;
+  unsigned long long stamp[LK_NSTAMP];   // diagnostics only
 };
 
 template <int AGG, int NSTR>
@@ -123,50 +122,108 @@ __device__ __forceinline__ const T* uptr(const T* p) {
   return reinterpret_cast<const T*>(uni_ptr(reinterpret_cast<const uint8_t*>(p)));
 }
 
-// 8 consecutive values [v, v+8) of a hybrid stream (runs staged in LDS, `n` runs + sentinel), bit width
-// bw <= 8: one bit-packed group (bw bytes) or the RLE value; other cases fall back to per-value reads.
-__device__ __forceinline__ void hybrid_get8(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
-                                            uint32_t out[8]) {
-  const int ri = find_run64(runs, n, v);
-  const LRun r = runs[ri];
-  const uint32_t end = runs[ri + 1].start;   // sentinel past the last run
-  const bool lit = (r.off_lit & 0x80000000u) != 0;
-  const bool whole = v + 8 <= end;
-  if (whole && !lit) {
+// Exclusive prefix over the wave's lanes of a count in 0..15, and the wave total (uniform): one ballot per bit.
+__device__ __forceinline__ uint32_t wave_prefix16(uint32_t cnt, uint32_t& total) {
+  uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int e = 0; e < 8; e++) out[e] = r.value;
-    return;
+  for (int k = 0; k < 4; k++) {
+    const unsigned long long b = __ballot((cnt >> k) & 1u);
+    pre += __builtin_amdgcn_mbcnt_hi(uint32_t(b >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(b), 0u)) << k;
+    tot += uint32_t(__popcll(b)) << k;
   }
-  if (whole && bw <= 8) {
-    // 8 values = 8*bw <= 64 bits starting at bit `bit`; the 96 bits from the enclosing dword cover them
-    const uint32_t bit = (v - r.start) * uint32_t(bw);
-    const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
-    const uint32_t al = byte & ~3u;
-    const v2u w01 = __builtin_amdgcn_raw_buffer_load_b64(rs, al, 0, 0);
-    const uint32_t w2 = __builtin_amdgcn_raw_buffer_load_b32(rs, al + 8, 0, 0);
-    const uint32_t sh = (byte & 3u) * 8u + (bit & 7u);                       // <= 31
-    const uint64_t lo = ((uint64_t)w01.y << 32) | w01.x;
-    const uint64_t x = sh ? ((lo >> sh) | ((uint64_t)w2 << (64 - sh))) : lo;
+  total = tot;
+  return pre;
+}
+
+// 8 consecutive values [v, v+8) of a hybrid RLE/bit-packed stream (runs staged in LDS: `n` runs + a sentinel
+// holding the end of the last one), in two steps so the load latency overlaps other work:
+//   g8_issue: run lookup; when [v, v+8) lies inside one bit-packed run with bw <= 8, load the 96 bits from the
+//             dword enclosing its first bit (8*bw <= 64 bits + <= 31 bits of misalignment);
+//   g8_unpack / g8_bits: unpack (an RLE run: its value; a group straddling runs or bw > 8: per-value reads).
+struct G8 {
+  v2u w01;
+  uint32_t w2;
+  uint32_t ri;   // run index
+};
+
+__device__ __forceinline__ G8 g8_issue(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
+                                       bool wide) {
+  G8 g;
+  g.ri = find_run64(runs, n, v);
+  const LRun r = runs[g.ri];
+  const bool fast = (r.off_lit & 0x80000000u) != 0 && v + 8 <= runs[g.ri + 1].start && bw <= 8;
+  const uint32_t byte = (r.off_lit & 0x7fffffffu) + (((v - r.start) * uint32_t(bw)) >> 3);
+  g.w01 = __builtin_amdgcn_raw_buffer_load_b64(rs, fast ? (byte & ~3u) : OOB, 0, 0);
+  g.w2 = wide ? __builtin_amdgcn_raw_buffer_load_b32(rs, fast ? (byte & ~3u) + 8u : OOB, 0, 0) : 0u;
+  return g;
+}
+
+// the 64 bits starting at value v's first bit (fast case)
+__device__ __forceinline__ uint64_t g8_window(const G8& g, const LRun& r, uint32_t v, int bw) {
+  const uint32_t bit = (v - r.start) * uint32_t(bw);
+  const uint32_t sh = (((r.off_lit & 0x7fffffffu) + (bit >> 3)) & 3u) * 8u + (bit & 7u);   // <= 31
+  const uint64_t lo = ((uint64_t)g.w01.y << 32) | g.w01.x;
+  return sh ? ((lo >> sh) | ((uint64_t)g.w2 << (64 - sh))) : lo;
+}
+
+// Unpack the group through `look` (dictionary index -> lookup value) into out[0..8); values at or past `left`
+// are looked up as index 0. An RLE run looks its value up once. The straddling / wide case is a rolled loop
+// through the thread's own 8 LDS slots `own` (no other thread reads them).
+template <class Look>
+__device__ __forceinline__ void g8_unpack(const G8& g, __amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v,
+                                          int bw, uint32_t left, uint32_t* own, Look look, uint32_t out[8]) {
+  const LRun r = runs[g.ri];
+  const bool lit = (r.off_lit & 0x80000000u) != 0;
+  const bool whole = v + 8 <= runs[g.ri + 1].start;
+  if (whole && !lit) {
+    const uint32_t x = look(r.value);
+#pragma unroll
+    for (int e = 0; e < 8; e++) out[e] = x;
+  } else if (whole && bw <= 8) {
+    const uint64_t x = g8_window(g, r, v, bw);
     const uint32_t mask = (1u << bw) - 1u;
 #pragma unroll
-    for (int e = 0; e < 8; e++) out[e] = uint32_t(x >> (e * bw)) & mask;
-    return;
-  }
+    for (int e = 0; e < 8; e++) out[e] = look(uint32_t(e) < left ? uint32_t(x >> (e * bw)) & mask : 0u);
+  } else {
+#pragma unroll 1
+    for (int e = 0; e < 8; e++) {
+      const uint32_t ve = v + e;
+      own[e] = look(uint32_t(e) < left ? hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, bw) : 0u);
+    }
 #pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const uint32_t ve = v + e;
-    out[e] = hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, bw);
+    for (int e = 0; e < 8; e++) out[e] = own[e];
   }
 }
 
-template <int AGG, int NSTR>
+// definition levels (bw 1): the 8 levels as bits, row v + e at bit e
+__device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t rs, const LRun* runs, int n,
+                                            uint32_t v) {
+  const LRun r = runs[g.ri];
+  const bool lit = (r.off_lit & 0x80000000u) != 0;
+  const bool whole = v + 8 <= runs[g.ri + 1].start;
+  if (whole && !lit) return r.value ? 0xffu : 0u;
+  if (whole) {
+    const uint32_t bit = v - r.start;
+    const uint32_t sh = (((r.off_lit & 0x7fffffffu) + (bit >> 3)) & 3u) * 8u + (bit & 7u);
+    const uint64_t lo = ((uint64_t)g.w01.y << 32) | g.w01.x;
+    return uint32_t(lo >> sh) & 0xffu;
+  }
+  uint32_t bits = 0;
+#pragma unroll 1
+  for (int e = 0; e < 8; e++) {
+    const uint32_t ve = v + e;
+    bits |= (hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, 1) & 1u) << e;
+  }
+  return bits;
+}
+
+template <int AGG, int NSTR, bool TT>
 __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
   constexpr int PSTRIDE = 2 * (RUN_CAP + 1);
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const unsigned long long lane_lt = (1ull << lane) - 1ull;
   const unsigned long long st0 = P.stamps ? __builtin_amdgcn_s_memtime() : 0;   // diagnostics only
 
   // ---- segment (grid.y) and tile (grid.x): uniform addresses -> scalar loads, once ----
@@ -198,8 +255,7 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
       h.lut_on = c >= 2 && tc.dict_n <= LUT_CAP;
     }
     L.hot[c] = h;
-    L.vrun[c] = 0;
-    if (c >= 2) L.sp[c - 2] = P.strp[c - 2];
+    if (c >= 2) L.sp[c - 2] = uint32_t(c - 2) < P.nstr ? P.strp[c - 2] : StrParam{};   // generic: unused columns
   }
   if (tid == 0) {
     L.win_lo = Sp->win_lo;
@@ -239,7 +295,7 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
       L.lut[s][i] = tab ? tab[g] : g;
     }
   }
-  if (P.truth) {
+  if (TT) {
     const uint32_t words = ((1u << (2 * P.nleaves)) + 31) / 32;
     for (uint32_t i = tid; i < words; i += BLOCK) L.truth[i] = P.truth[i];
   }
@@ -251,270 +307,306 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
     if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
     else L.hhi[i] = 0.0;
   }
+  const bool stamp = P.stamps != nullptr;   // diagnostics only
+  if (stamp && tid == 0)
+    for (int k = 0; k < LK_NSTAMP; k++) L.stamp[k] = 0;
   __syncthreads();
 
-  Acc acc;
-  acc_reset<AGG>(acc, EMPTY);
-  const bool stamp = P.stamps != nullptr;   // diagnostics only
-  unsigned long long st_pro = stamp ? __builtin_amdgcn_s_memtime() : 0, st_p1 = 0, st_p2 = 0, st_mark = st_pro;
+  // s_memtime section totals (wave 0): 0 prologue, 1 def levels, 2 decode, 3 fold, 4 filter, 5 compaction,
+  // 6 prefetch, 7 streaming
+  unsigned long long st_mark = stamp ? __builtin_amdgcn_s_memtime() : 0;
+  if (stamp && tid == 0) L.stamp[0] = st_mark - st0;
+#define LK_STAMP(k)                                                \
+  if (stamp && tid == 0) {                                         \
+    const unsigned long long now_ = __builtin_amdgcn_s_memtime();   \
+    L.stamp[k] += now_ - st_mark;                                  \
+    st_mark = now_;                                                \
+  }
 
-  for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
-    const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
+  // Per column: index (tile-relative) of the sub-tile's first value: its first row for a column without
+  // NULLs, the running non-NULL count for a nullable one.
+  uint32_t vrun[NC];
+#pragma unroll
+  for (int c = 0; c < NC; c++) vrun[c] = 0;
 
-    // ============ 1. validity bitmaps of nullable columns (run-major, 8 rows per thread) ============
-    bool any_nulls = false;
+  // Packed groups of the next sub-tile (first row s0): def levels of rows s0+8t.., dictionary indices of its
+  // values 8t.. (nullable: value-major). Issued one sub-tile ahead so the latency hides behind streaming.
+  G8 gd[NC], gv[NSTR];
+  auto prefetch = [&](uint32_t s0) {
 #pragma unroll
     for (int c = 0; c < NC; c++) {
+      gd[c] = G8{};
       if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
-      any_nulls = true;
       const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
-      const LRun* druns = L.pool + c * PSTRIDE + RUN_CAP + 1;
-      const int nd = int(uni(L.hot[c].ndruns));
-      const uint32_t r0 = uni(L.hot[c].rip) + sub + 8 * tid;    // rows 8*tid .. 8*tid+7 of the sub-tile
-      uint32_t bits = 0;
-      if (8 * uint32_t(tid) < nsub) {
-        uint32_t d[8];
-        hybrid_get8(drs, druns, nd, r0, 1, d);
-#pragma unroll
-        for (int e = 0; e < 8; e++) bits |= (d[e] & 1u) << e;
-        const uint32_t left = nsub - 8 * tid;
-        if (left < 8) bits &= (1u << left) - 1u;
-      }
-      reinterpret_cast<uint8_t*>(L.nv[c])[tid] = uint8_t(bits);
+      gd[c] = g8_issue(drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
+                       uni(L.hot[c].rip) + s0 + 8 * tid, 1, false);
     }
-    if (any_nulls) {
-      __syncthreads();
-      // per-64-row prefix counts (one wave per column; WORDS = 32 <= 64 lanes)
-      for (int c = wave; c < NC; c += BLOCK / 64) {
-        if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
-        const uint32_t cnt = lane < WORDS ? __popcll(L.nv[c][lane]) : 0u;
-        uint32_t x = cnt;
-        for (int o = 1; o < 64; o <<= 1) {
-          const uint32_t y = __shfl_up(x, o, 64);
-          if (lane >= o) x += y;
-        }
-        if (lane < WORDS) L.npre[c][lane] = x - cnt;
-        if (lane == WORDS - 1) L.npre[c][WORDS] = x;
-      }
-      __syncthreads();
-    }
-
-    // ============ 2. string columns: value-major decode to LDS, then fold per row ============
-    uint32_t leafT[SLOTS], leafF[SLOTS], gid[SLOTS];
-#pragma unroll
-    for (int j = 0; j < SLOTS; j++) leafT[j] = 0, leafF[j] = 0, gid[j] = 0;
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
+      gv[s] = G8{};
+      const uint32_t nr = uni(L.hot[c].present) ? uni(L.hot[c].nruns) : 0u;
+      if (!nr) continue;
+      const uint32_t vs = uni(L.hot[c].vbase) + (uni(L.hot[c].has_nulls) ? vrun[c] : s0);
+      const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
+      gv[s] = g8_issue(vrs, L.pool + c * PSTRIDE, int(nr), vs + 8 * tid, int(uni(L.hot[c].bw)), true);
+    }
+  };
+  prefetch(0);
+
+  Acc acc;
+  acc_reset<AGG>(acc, EMPTY);
+  uint32_t* own = L.pk + 8 * tid;
+  uint2* wlist = L.list[wave];
+
+  for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
+    const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
+    const uint32_t r0 = 8u * tid;   // the thread's first row in the sub-tile
+    const uint32_t inb = r0 < nsub ? (nsub - r0 >= 8 ? 0xffu : (1u << (nsub - r0)) - 1u) : 0u;
+
+    // ============ A. validity bytes and value indices ============
+    uint32_t vb[NC], vfirst[NC], ctot[NC];   // non-NULL rows (bit e = row r0+e), first value index, count
+    bool any_nulls = false;
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
       const bool present = uni(L.hot[c].present) != 0;
-      const bool nullable = present && uni(L.hot[c].has_nulls) != 0;
-      const uint32_t nr = present ? uni(L.hot[c].nruns) : 0u;
+      vb[c] = present ? inb : 0u;
+      vfirst[c] = r0;
+      ctot[c] = nsub;
+      if (present && uni(L.hot[c].has_nulls)) {
+        any_nulls = true;
+        const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
+        vb[c] = g8_bits(gd[c], drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
+                        uni(L.hot[c].rip) + sub + r0) & inb;
+        uint32_t wt;
+        vfirst[c] = wave_prefix16(__popc(vb[c]), wt);
+        if (lane == 0) L.wsum[c][wave] = wt;
+      }
+    }
+    if (any_nulls) {
+      __syncthreads();
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; w++) {
+          const uint32_t x = L.wsum[c][w];
+          before += w < wave ? x : 0u;
+          all += x;
+        }
+        vfirst[c] += before;
+        ctot[c] = uni(all);
+      }
+      __syncthreads();   // wsum is rewritten by the next sub-tile
+    }
+    LK_STAMP(1)
+
+    // ============ B. string columns -> leaf T/F bits and group id per row ============
+    uint32_t leafT[8], leafF[8], gid[8];
+#pragma unroll
+    for (int e = 0; e < 8; e++) leafT[e] = 0, leafF[e] = 0, gid[e] = 0;
+#pragma unroll
+    for (int s = 0; s < NSTR; s++) {
+      const int c = 2 + s;
+      const uint32_t nr = uni(L.hot[c].present) ? uni(L.hot[c].nruns) : 0u;
+      uint32_t packed[8];
+#pragma unroll
+      for (int e = 0; e < 8; e++) packed[e] = 0;
       if (nr) {
-        // values of this sub-tile: [vs, vs + nvals)
-        const uint32_t vs = uni(L.hot[c].vbase) + (nullable ? uni(L.vrun[c]) : sub);
-        const uint32_t nvals = nullable ? uni(L.npre[c][WORDS]) : nsub;
+        const bool nullable = uni(L.hot[c].has_nulls) != 0;
         const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
         const LRun* runs = L.pool + c * PSTRIDE;
         const int bw = int(uni(L.hot[c].bw));
-        const bool lut = uni(L.hot[c].lut_on) != 0;
-        if (8 * uint32_t(tid) < nvals) {
-          uint32_t idx[8];
-          hybrid_get8(vrs, runs, int(nr), vs + 8 * tid, bw, idx);
-          if (lut) {
-#pragma unroll
-            for (int e = 0; e < 8; e++) L.pk[8 * tid + e] = L.lut[s][idx[e] < LUT_CAP ? idx[e] : 0];
-          } else {
-            const uint32_t* remap = uptr(L.hot[c].remap);
-            const uint32_t* tab = uptr(L.sp[s].strtab);
-            const uint32_t left = nvals - 8 * tid;
-#pragma unroll
-            for (int e = 0; e < 8; e++) {
-              const uint32_t g = remap[e < int(left) ? idx[e] : idx[0]];
-              L.pk[8 * tid + e] = tab ? tab[g] : g;
-            }
-          }
+        const uint32_t v0 = uni(L.hot[c].vbase) + vrun[c] + r0;   // this thread's group: values r0.. of the sub-tile
+        const uint32_t left = ctot[c] > r0 ? ctot[c] - r0 : 0u;
+        uint32_t dec[8];
+        if (uni(L.hot[c].lut_on)) {
+          const uint32_t* lt = L.lut[s];
+          g8_unpack(gv[s], vrs, runs, int(nr), v0, bw, left, own, [&](uint32_t i) { return lt[i < LUT_CAP ? i : 0u]; },
+                    dec);
+        } else {
+          const uint32_t* remap = uptr(L.hot[c].remap);
+          const uint32_t* tab = uptr(L.sp[s].strtab);
+          g8_unpack(gv[s], vrs, runs, int(nr), v0, bw, left, own, [&](uint32_t i) {
+            const uint32_t g = remap[i];
+            return tab ? tab[g] : g;
+          }, dec);
         }
-        __syncthreads();
+        if (!nullable) {
+#pragma unroll
+          for (int e = 0; e < 8; e++) packed[e] = dec[e];
+        } else {
+          // values are value-major: publish them, then gather each row's value by its value index
+#pragma unroll
+          for (int e = 0; e < 8; e++) own[e] = dec[e];
+          __syncthreads();
+          uint32_t vi = vfirst[c];
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            const bool valid = (vb[c] >> e) & 1u;
+            packed[e] = valid ? L.pk[vi] : 0u;
+            vi += valid;
+          }
+          __syncthreads();   // pk is rewritten by the next column / sub-tile
+        }
       }
+      LK_STAMP(2)
       const uint32_t dstride = uni(L.sp[s].dim_stride), dnull = uni(L.sp[s].dim_null);
       const uint32_t lbase = uni(L.sp[s].lbase), lmask = uni(L.sp[s].lmask), hmask = uni(L.sp[s].hmask);
+      const uint32_t valid = nr ? vb[c] : 0u;
 #pragma unroll
-      for (int j = 0; j < SLOTS; j++) {
-        const uint32_t r = j * BLOCK + tid;   // row within the sub-tile
-        const int w = r >> 6;
-        bool valid = false;
-        uint32_t vi = 0;
-        if (nr && nullable) {
-          const unsigned long long m = L.nv[c][w];
-          valid = (m >> lane) & 1ull;
-          vi = L.npre[c][w] + __popcll(m & lane_lt);
-        } else if (nr) {
-          valid = r < nsub;
-          vi = r;
-        }
-        const uint32_t packed = valid ? L.pk[vi] : 0u;
-        const uint32_t bits = (packed >> 24) << lbase;
-        const uint32_t dim = valid ? (packed & DIM_MASK) : dnull;
-        gid[j] += dim * dstride;
-        leafT[j] |= valid ? (bits & lmask) : 0u;
-        leafF[j] |= valid ? (~bits & lmask) : hmask;   // IS NOT NULL on NULL: FALSE; others NULL
+      for (int e = 0; e < 8; e++) {
+        const bool ok = (valid >> e) & 1u;
+        const uint32_t bits = (packed[e] >> 24) << lbase;
+        gid[e] += (ok ? (packed[e] & DIM_MASK) : dnull) * dstride;
+        leafT[e] |= ok ? (bits & lmask) : 0u;
+        leafF[e] |= ok ? (~bits & lmask) : hmask;   // IS NOT NULL on NULL: FALSE; others NULL
       }
-      if (nr) __syncthreads();   // the next column reuses pk
+      LK_STAMP(3)
     }
 
-    // ============ 3. filter (truth table) -> pass bitmap, group ids; compaction ============
+    // ============ C. filter -> pass byte (NULL / absent timestamps fail the window) ============
+    uint32_t passb = 0;
     {
       const uint32_t leaf_false = uni(L.leaf_false);
       const uint32_t nleaves = P.nleaves;
-      const bool use_truth = P.truth != nullptr;
-      const bool ts_null = uni(L.hot[0].has_nulls) != 0 && uni(L.hot[0].present) != 0;
-      const bool ts_present = uni(L.hot[0].present) != 0;
 #pragma unroll
-      for (int j = 0; j < SLOTS; j++) {
-        const uint32_t r = j * BLOCK + tid;
-        const uint32_t T = leafT[j] & ~leaf_false, F = leafF[j] | leaf_false;
+      for (int e = 0; e < 8; e++) {
+        const uint32_t T = leafT[e] & ~leaf_false, F = leafF[e] | leaf_false;
         bool ok;
-        if (use_truth) {
+        if (TT) {
           const uint32_t ix = T | (F << nleaves);
           ok = (L.truth[ix >> 5] >> (ix & 31)) & 1u;
         } else {
           ok = interpret(P, T, F);
         }
-        if (P.ablate & 2) ok = (tid & 15) == 0;
-        bool pass = ok && r < nsub && ts_present;
-        if (ts_null) pass = pass && ((L.nv[0][r >> 6] >> lane) & 1ull);   // NULL timestamp fails the window
-        const unsigned long long pm = __ballot(pass);
-        if (lane == 0) L.passw[r >> 6] = pm;
-        L.pk[r] = gid[j];   // pk is free: every fold that read it ended with a barrier
+        passb |= uint32_t(ok) << e;
       }
+      passb &= vb[0];
     }
-    __syncthreads();
-    if (wave == 0) {
-      const uint32_t cnt = lane < WORDS ? __popcll(L.passw[lane]) : 0u;
-      uint32_t x = cnt;
-      for (int o = 1; o < 64; o <<= 1) {
-        const uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-      }
-      if (lane < WORDS) L.ppre[lane] = x - cnt;
-      if (lane == WORDS - 1) L.ppre[WORDS] = x;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < SLOTS; j++) {
-      const uint32_t r = j * BLOCK + tid;
-      const unsigned long long m = L.passw[r >> 6];
-      if ((m >> lane) & 1ull) L.list[L.ppre[r >> 6] + __popcll(m & lane_lt)] = uint16_t(r);
-    }
-    __syncthreads();
-    if (stamp) {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      st_p1 += now - st_mark;
-      st_mark = now;
-    }
+    LK_STAMP(4)
 
-    // ============ 4. stream timestamp + value of listed rows, bucket, aggregate ============
-    const uint32_t nlist = uni(L.ppre[WORDS]);
+    // ============ D. compact the wave's passing rows into its list, in row order ============
+    uint32_t nlist;
+    {
+      uint32_t k = wave_prefix16(__popc(passb), nlist);
+      uint32_t tv = vfirst[0], vv = vfirst[1];
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const uint32_t vok = (vb[1] >> e) & 1u;
+        if ((passb >> e) & 1u) {
+          wlist[k] = make_uint2(gid[e], tv | (vv << 11) | (vok << 22));
+          k++;
+        }
+        tv += (vb[0] >> e) & 1u;
+        vv += vok;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    LK_STAMP(5)
+
+    // next sub-tile's packed groups: in flight during the streaming phase
+    uint32_t vnext[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++) vnext[c] = vrun[c] + ctot[c];
+    if (sub + SUBT < tile_nrows) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) vrun[c] = vnext[c];
+      prefetch(sub + SUBT);
+#pragma unroll
+      for (int c = 0; c < NC; c++) vrun[c] = vnext[c] - ctot[c];
+    }
+    LK_STAMP(6)
+
+    // ============ E. stream timestamp + value of the wave's listed rows, bucket, aggregate ============
     if (!(P.ablate & 1) && nlist) {
       const bool pres1 = uni(L.hot[1].present) != 0;
-      const bool nn0 = uni(L.hot[0].has_nulls) != 0, nn1 = pres1 && uni(L.hot[1].has_nulls) != 0;
       const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(L.hot[0].vals, L.hot[0].vals_len);
       const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(L.hot[1].vals, pres1 ? L.hot[1].vals_len : 0u);
-      const uint32_t vb0 = uni(L.hot[0].vbase) + (nn0 ? uni(L.vrun[0]) : sub);
-      const uint32_t vb1 = uni(L.hot[1].vbase) + (nn1 ? uni(L.vrun[1]) : sub);
+      const uint32_t vb0 = uni(L.hot[0].vbase) + vrun[0];
+      const uint32_t vb1 = uni(L.hot[1].vbase) + vrun[1];
       const int64_t win_lo = L.win_lo, win_hi = L.win_hi;
       const unsigned long long glob_base = (unsigned long long)uni(L.glob_slot) * P.nbuckets;
       const uint32_t step32 = uint32_t(P.step);
-      for (uint32_t cb = 0; cb < nlist; cb += PS * BLOCK) {
-      v2u tsr[PS], vr[PS];
-      uint32_t rows[PS];
-      bool vok[PS];
+      for (uint32_t cb = 0; cb < nlist; cb += PS * 64) {
+        v2u tsr[PS], vr[PS];
+        uint32_t gids[PS];
+        bool vok[PS];
 #pragma unroll
-      for (int j = 0; j < PS; j++) {
-        tsr[j] = v2u{0u, 0u};
-        vr[j] = v2u{0u, 0u};
-        rows[j] = 0;
-        vok[j] = false;
-        if (cb + j * BLOCK >= nlist) continue;                                // uniform
-        const uint32_t e = cb + j * BLOCK + tid;
-        const bool live = e < nlist;
-        const uint32_t r = live ? L.list[e] : 0u;
-        rows[j] = r;
-        const int w = r >> 6, ln = r & 63;
-        const unsigned long long below = (1ull << ln) - 1ull;
-        const uint32_t tv = nn0 ? L.npre[0][w] + __popcll(L.nv[0][w] & below) : r;
-        tsr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-        bool vv = pres1;
-        uint32_t vi = r;
-        if (nn1) {
-          const unsigned long long m = L.nv[1][w];
-          vv = (m >> ln) & 1ull;
-          vi = L.npre[1][w] + __popcll(m & below);
+        for (int j = 0; j < PS; j++) {
+          tsr[j] = v2u{0u, 0u};
+          vr[j] = v2u{0u, 0u};
+          gids[j] = 0;
+          vok[j] = false;
+          if (cb + j * 64 >= nlist) continue;                                  // uniform
+          const uint32_t i = cb + j * 64 + lane;
+          const bool live = i < nlist;
+          const uint2 en = live ? wlist[i] : make_uint2(0u, 0u);
+          gids[j] = en.x;
+          const uint32_t tv = en.y & 0x7ffu, vv = (en.y >> 11) & 0x7ffu;
+          vok[j] = live && ((en.y >> 22) & 1u);
+          tsr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+          if (AGG != AGG_COUNT) vr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok[j] ? (vb1 + vv) * 8u : OOB, 0, 0);
         }
-        vok[j] = vv && live;
-        if (AGG != AGG_COUNT) vr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, (live && vv) ? (vb1 + vi) * 8u : OOB, 0, 0);
-        else vr[j] = v2u{0u, 0u};
-      }
 #pragma unroll
-      for (int j = 0; j < PS; j++) {
-        if (cb + j * BLOCK >= nlist) break;                                   // uniform
-        const int64_t ts = (int64_t)(((uint64_t)tsr[j].y << 32) | tsr[j].x);
-        bool ok = (cb + j * BLOCK + tid < nlist) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
-        int64_t b = 0;
-        if (P.fast_div) {
-          // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
-          const uint32_t d = uint32_t(ts - P.bucket_base);
-          uint32_t q = uint32_t(double(d) * P.inv_step);
-          int64_t rm = int64_t(d) - int64_t(q) * step32;
-          q = rm < 0 ? q - 1 : (rm >= int64_t(step32) ? q + 1 : q);
-          rm = int64_t(d) - int64_t(q) * step32;
-          if (P.metrics && rm != 0 && ok) {
-            atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
-            ok = false;
-          }
-          b = q;
-        } else if (ok) {
-          if (P.metrics) {
-            const int64_t d = ts - P.bucket_base;
-            b = d / P.step;
-            if (d - b * P.step != 0) {
+        for (int j = 0; j < PS; j++) {
+          if (cb + j * 64 >= nlist) break;                                     // uniform
+          const int64_t ts = (int64_t)(((uint64_t)tsr[j].y << 32) | tsr[j].x);
+          bool ok = (cb + j * 64 + lane < nlist) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
+          int64_t b = 0;
+          if (P.fast_div) {
+            // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
+            const uint32_t d = uint32_t(ts - P.bucket_base);
+            uint32_t q = uint32_t(double(d) * P.inv_step);
+            int64_t rm = int64_t(d) - int64_t(q) * step32;
+            q = rm < 0 ? q - 1 : (rm >= int64_t(step32) ? q + 1 : q);
+            rm = int64_t(d) - int64_t(q) * step32;
+            if (P.metrics && rm != 0 && ok) {
               atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
               ok = false;
             }
-          } else {
-            b = ((ts - ts % P.step) - P.bucket_base) / P.step;        // ts - ts % step (fmod, truncation)
+            b = q;
+          } else if (ok) {
+            if (P.metrics) {
+              const int64_t d = ts - P.bucket_base;
+              b = d / P.step;
+              if (d - b * P.step != 0) {
+                atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
+                ok = false;
+              }
+            } else {
+              b = ((ts - ts % P.step) - P.bucket_base) / P.step;        // ts - ts % step (fmod, truncation)
+            }
           }
+          if (!ok) continue;
+          if (b < 0 || (uint64_t)b >= P.nbuckets) {
+            atomicOr(P.flags, FLAG_CELL_RANGE);
+            continue;
+          }
+          const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + gids[j];
+          if (cell != acc.key) {
+            lds_merge<AGG>(L, P, acc);
+            acc_reset<AGG>(acc, cell);
+          }
+          const double v = __longlong_as_double((long long)(((uint64_t)vr[j].y << 32) | vr[j].x));
+          acc_add<AGG>(acc, vok[j], v);
         }
-        if (!ok) continue;
-        if (b < 0 || (uint64_t)b >= P.nbuckets) {
-          atomicOr(P.flags, FLAG_CELL_RANGE);
-          continue;
-        }
-        const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + L.pk[rows[j]];
-        if (cell != acc.key) {
-          lds_merge<AGG>(L, P, acc);
-          acc_reset<AGG>(acc, cell);
-        }
-        const double v = __longlong_as_double((long long)(((uint64_t)vr[j].y << 32) | vr[j].x));
-        acc_add<AGG>(acc, vok[j], v);
-      }
       }
     }
-    __syncthreads();   // the next sub-tile overwrites the bitmaps, pk, list
-    // advance the per-column non-null counters (read next after the next sub-tile's validity barriers)
-    if (any_nulls && tid < NC && L.hot[tid].present && L.hot[tid].has_nulls) L.vrun[tid] += L.npre[tid][WORDS];
-    if (stamp) {
-      const unsigned long long now = __builtin_amdgcn_s_memtime();
-      st_p2 += now - st_mark;
-      st_mark = now;
-    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) vrun[c] = vnext[c];
+    // the wave's list is rewritten only by this wave (next sub-tile's step D, after its own reads)
+    __builtin_amdgcn_wave_barrier();
+    LK_STAMP(7)
   }
+#undef LK_STAMP
   if (stamp && tid == 0) {
-    unsigned long long* o = P.stamps + 4 * (size_t(blockIdx.y) * P.max_tiles + blockIdx.x);
-    o[0] = st_pro - st0;
-    o[1] = st_p1;
-    o[2] = st_p2;
-    o[3] = __builtin_amdgcn_s_memtime() - st0;
+    unsigned long long* o = P.stamps + LK_NSTAMP * (size_t(blockIdx.y) * P.max_tiles + blockIdx.x);
+#pragma unroll
+    for (int k = 0; k < LK_NSTAMP; k++) o[k] = L.stamp[k] | (k == 0 ? 1ull << 63 : 0ull);   // bit 63: block ran
   }
   lds_merge<AGG>(L, P, acc);
   __syncthreads();
