@@ -47,10 +47,11 @@ struct Lds {
   uint32_t hcnt[HCAP];
   double hhi[HCAP];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
   double hlo[HCAP];
-  uint32_t pk[SUBT];                     // nullable string column: lookup values, value-major; otherwise each
-                                         //   thread's own 8 slots (scratch of the straddling-group decode)
   uint2 list[WAVES][WROWS];              // per wave: passing rows {group id, ts index | value index << 11 |
-                                         //   value valid << 22} (indices relative to the sub-tile's values)
+                                         //   value valid << 22} (indices relative to the sub-tile's values).
+                                         // Its first 2 KB per wave double as the wave's pk slots (thread t:
+                                         //   8 u32 at 8*lane): a nullable string column's lookup values,
+                                         //   value-major, and the straddling-group decode's scratch.
   uint32_t wsum[2 + NSTR][WAVES];        // per nullable column: non-NULL rows of each wave in the sub-tile
   ColHot hot[2 + NSTR];                  // per-tile column state
   StrParam sp[NSTR];                     // per-query string column parameters
@@ -218,7 +219,7 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
 }
 
 template <int AGG, int NSTR, bool TT>
-__global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : 2))) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
   constexpr int PSTRIDE = 2 * (RUN_CAP + 1);
@@ -323,20 +324,30 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
     st_mark = now_;                                                \
   }
 
+  // per-tile column flags as scalar bit masks (bit c): present, has NULLs, small-dictionary lookup in LDS
+  uint32_t presm = 0, nullm = 0, lutm = 0;
+#pragma unroll
+  for (int c = 0; c < NC; c++) {
+    presm |= (uni(L.hot[c].present) ? 1u : 0u) << c;
+    nullm |= (uni(L.hot[c].present) && uni(L.hot[c].has_nulls) ? 1u : 0u) << c;
+    lutm |= (uni(L.hot[c].lut_on) ? 1u : 0u) << c;
+  }
+  presm = uni(presm), nullm = uni(nullm), lutm = uni(lutm);
+
   // Per column: index (tile-relative) of the sub-tile's first value: its first row for a column without
   // NULLs, the running non-NULL count for a nullable one.
   uint32_t vrun[NC];
 #pragma unroll
   for (int c = 0; c < NC; c++) vrun[c] = 0;
 
-  // Packed groups of the next sub-tile (first row s0): def levels of rows s0+8t.., dictionary indices of its
-  // values 8t.. (nullable: value-major). Issued one sub-tile ahead so the latency hides behind streaming.
+  // Packed groups of a sub-tile (first row s0, first values vfirst_next[c]): def levels of rows s0+8t..,
+  // dictionary indices of its values 8t.. (nullable: value-major). Issued one sub-tile ahead.
   G8 gd[NC], gv[NSTR];
-  auto prefetch = [&](uint32_t s0) {
+  auto prefetch = [&](uint32_t s0, const uint32_t* vnext) {
 #pragma unroll
     for (int c = 0; c < NC; c++) {
       gd[c] = G8{};
-      if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
+      if (!((nullm >> c) & 1u)) continue;
       const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
       gd[c] = g8_issue(drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
                        uni(L.hot[c].rip) + s0 + 8 * tid, 1, false);
@@ -345,19 +356,104 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
       gv[s] = G8{};
-      const uint32_t nr = uni(L.hot[c].present) ? uni(L.hot[c].nruns) : 0u;
+      const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       if (!nr) continue;
-      const uint32_t vs = uni(L.hot[c].vbase) + (uni(L.hot[c].has_nulls) ? vrun[c] : s0);
       const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
-      gv[s] = g8_issue(vrs, L.pool + c * PSTRIDE, int(nr), vs + 8 * tid, int(uni(L.hot[c].bw)), true);
+      gv[s] = g8_issue(vrs, L.pool + c * PSTRIDE, int(nr), uni(L.hot[c].vbase) + vnext[c] + 8 * tid,
+                       int(uni(L.hot[c].bw)), true);
     }
   };
-  prefetch(0);
+  prefetch(0, vrun);
+
+  // streaming state: timestamp/value buffers of the tile's pages, window, glob cell base
+  const bool pres1 = (presm >> 1) & 1u;
+  const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(L.hot[0].vals, L.hot[0].vals_len);
+  const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(L.hot[1].vals, pres1 ? L.hot[1].vals_len : 0u);
+  const uint32_t vbase0 = uni(L.hot[0].vbase), vbase1 = uni(L.hot[1].vbase);
+  const int64_t win_lo = L.win_lo, win_hi = L.win_hi;
+  const unsigned long long glob_base = (unsigned long long)uni(L.glob_slot) * P.nbuckets;
+  const uint32_t step32 = uint32_t(P.step);
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
-  uint32_t* own = L.pk + 8 * tid;
   uint2* wlist = L.list[wave];
+  uint32_t* own = reinterpret_cast<uint32_t*>(wlist) + 8 * lane;   // the thread's 8 pk slots
+
+  // One chunk: up to PS*64 listed rows of a wave, loads in flight.
+  struct Chunk {
+    v2u ts[PS], v[PS];
+    uint32_t gid[PS];
+    uint32_t vok;   // bit j: value j is non-NULL
+    uint32_t n;     // rows in the chunk (uniform)
+  };
+  auto issue = [&](Chunk& ch, uint32_t cb, uint32_t nlist, uint32_t vb0, uint32_t vb1) {
+    ch.n = min(nlist - cb, uint32_t(PS * 64));
+    ch.vok = 0;
+#pragma unroll
+    for (int j = 0; j < PS; j++) {
+      ch.ts[j] = v2u{0u, 0u};
+      ch.v[j] = v2u{0u, 0u};
+      ch.gid[j] = 0;
+      if (uint32_t(j * 64) >= ch.n) continue;                                  // uniform
+      const uint32_t i = j * 64 + lane;
+      const bool live = i < ch.n;
+      const uint2 en = live ? wlist[cb + i] : make_uint2(0u, 0u);
+      ch.gid[j] = en.x;
+      const uint32_t tv = en.y & 0x7ffu, vv = (en.y >> 11) & 0x7ffu;
+      const bool vok = live && ((en.y >> 22) & 1u);
+      ch.vok |= uint32_t(vok) << j;
+      ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+      if (AGG != AGG_COUNT) ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
+    }
+  };
+  auto consume = [&](const Chunk& ch) {
+#pragma unroll
+    for (int j = 0; j < PS; j++) {
+      if (uint32_t(j * 64) >= ch.n) break;                                     // uniform
+      const int64_t ts = (int64_t)(((uint64_t)ch.ts[j].y << 32) | ch.ts[j].x);
+      bool ok = (uint32_t(j * 64 + lane) < ch.n) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
+      int64_t b = 0;
+      if (P.fast_div) {
+        // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
+        const uint32_t d = uint32_t(ts - P.bucket_base);
+        uint32_t q = uint32_t(double(d) * P.inv_step);
+        int64_t rm = int64_t(d) - int64_t(q) * step32;
+        q = rm < 0 ? q - 1 : (rm >= int64_t(step32) ? q + 1 : q);
+        rm = int64_t(d) - int64_t(q) * step32;
+        if (P.metrics && rm != 0 && ok) {
+          atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
+          ok = false;
+        }
+        b = q;
+      } else if (ok) {
+        if (P.metrics) {
+          const int64_t d = ts - P.bucket_base;
+          b = d / P.step;
+          if (d - b * P.step != 0) {
+            atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
+            ok = false;
+          }
+        } else {
+          b = ((ts - ts % P.step) - P.bucket_base) / P.step;        // ts - ts % step (fmod, truncation)
+        }
+      }
+      if (!ok) continue;
+      if (b < 0 || (uint64_t)b >= P.nbuckets) {
+        atomicOr(P.flags, FLAG_CELL_RANGE);
+        continue;
+      }
+      const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
+      if (cell != acc.key) {
+        lds_merge<AGG>(L, P, acc);
+        acc_reset<AGG>(acc, cell);
+      }
+      const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
+      acc_add<AGG>(acc, (ch.vok >> j) & 1u, v);
+    }
+  };
+  Chunk pend;   // the previous sub-tile's first chunk: consumed after this sub-tile's decode
+  pend.n = 0;
+  const bool stream_on = !(P.ablate & 1);
 
   for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
     const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
@@ -366,15 +462,12 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
 
     // ============ A. validity bytes and value indices ============
     uint32_t vb[NC], vfirst[NC], ctot[NC];   // non-NULL rows (bit e = row r0+e), first value index, count
-    bool any_nulls = false;
 #pragma unroll
     for (int c = 0; c < NC; c++) {
-      const bool present = uni(L.hot[c].present) != 0;
-      vb[c] = present ? inb : 0u;
+      vb[c] = ((presm >> c) & 1u) ? inb : 0u;
       vfirst[c] = r0;
       ctot[c] = nsub;
-      if (present && uni(L.hot[c].has_nulls)) {
-        any_nulls = true;
+      if ((nullm >> c) & 1u) {
         const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
         vb[c] = g8_bits(gd[c], drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
                         uni(L.hot[c].rip) + sub + r0) & inb;
@@ -383,11 +476,11 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
         if (lane == 0) L.wsum[c][wave] = wt;
       }
     }
-    if (any_nulls) {
+    if (nullm) {
       __syncthreads();
 #pragma unroll
       for (int c = 0; c < NC; c++) {
-        if (!(uni(L.hot[c].present) && uni(L.hot[c].has_nulls))) continue;
+        if (!((nullm >> c) & 1u)) continue;
         uint32_t before = 0, all = 0;
 #pragma unroll
         for (int w = 0; w < WAVES; w++) {
@@ -409,19 +502,18 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
-      const uint32_t nr = uni(L.hot[c].present) ? uni(L.hot[c].nruns) : 0u;
+      const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       uint32_t packed[8];
 #pragma unroll
       for (int e = 0; e < 8; e++) packed[e] = 0;
       if (nr) {
-        const bool nullable = uni(L.hot[c].has_nulls) != 0;
         const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
         const LRun* runs = L.pool + c * PSTRIDE;
         const int bw = int(uni(L.hot[c].bw));
         const uint32_t v0 = uni(L.hot[c].vbase) + vrun[c] + r0;   // this thread's group: values r0.. of the sub-tile
         const uint32_t left = ctot[c] > r0 ? ctot[c] - r0 : 0u;
         uint32_t dec[8];
-        if (uni(L.hot[c].lut_on)) {
+        if ((lutm >> c) & 1u) {
           const uint32_t* lt = L.lut[s];
           g8_unpack(gv[s], vrs, runs, int(nr), v0, bw, left, own, [&](uint32_t i) { return lt[i < LUT_CAP ? i : 0u]; },
                     dec);
@@ -433,22 +525,24 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
             return tab ? tab[g] : g;
           }, dec);
         }
-        if (!nullable) {
+        if (!((nullm >> c) & 1u)) {
 #pragma unroll
           for (int e = 0; e < 8; e++) packed[e] = dec[e];
         } else {
-          // values are value-major: publish them, then gather each row's value by its value index
+          // values are value-major: publish them (value i lives in wave i/512's list area), then gather each
+          // row's value by its value index
 #pragma unroll
           for (int e = 0; e < 8; e++) own[e] = dec[e];
           __syncthreads();
+          const uint32_t* pkw = reinterpret_cast<const uint32_t*>(L.list);
           uint32_t vi = vfirst[c];
 #pragma unroll
           for (int e = 0; e < 8; e++) {
             const bool valid = (vb[c] >> e) & 1u;
-            packed[e] = valid ? L.pk[vi] : 0u;
+            packed[e] = valid ? pkw[((vi >> 9) << 10) | (vi & 511u)] : 0u;
             vi += valid;
           }
-          __syncthreads();   // pk is rewritten by the next column / sub-tile
+          __syncthreads();   // the area is rewritten by the next column / the wave's list
         }
       }
       LK_STAMP(2)
@@ -508,100 +602,35 @@ __global__ __launch_bounds__(BLOCK) void scan_tiles(QParams P) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     LK_STAMP(5)
 
-    // next sub-tile's packed groups: in flight during the streaming phase
+    // next sub-tile's packed groups: in flight while this sub-tile streams
     uint32_t vnext[NC];
 #pragma unroll
     for (int c = 0; c < NC; c++) vnext[c] = vrun[c] + ctot[c];
-    if (sub + SUBT < tile_nrows) {
-#pragma unroll
-      for (int c = 0; c < NC; c++) vrun[c] = vnext[c];
-      prefetch(sub + SUBT);
-#pragma unroll
-      for (int c = 0; c < NC; c++) vrun[c] = vnext[c] - ctot[c];
-    }
+    if (sub + SUBT < tile_nrows) prefetch(sub + SUBT, vnext);
     LK_STAMP(6)
 
     // ============ E. stream timestamp + value of the wave's listed rows, bucket, aggregate ============
-    if (!(P.ablate & 1) && nlist) {
-      const bool pres1 = uni(L.hot[1].present) != 0;
-      const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(L.hot[0].vals, L.hot[0].vals_len);
-      const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(L.hot[1].vals, pres1 ? L.hot[1].vals_len : 0u);
-      const uint32_t vb0 = uni(L.hot[0].vbase) + vrun[0];
-      const uint32_t vb1 = uni(L.hot[1].vbase) + vrun[1];
-      const int64_t win_lo = L.win_lo, win_hi = L.win_hi;
-      const unsigned long long glob_base = (unsigned long long)uni(L.glob_slot) * P.nbuckets;
-      const uint32_t step32 = uint32_t(P.step);
-      for (uint32_t cb = 0; cb < nlist; cb += PS * 64) {
-        v2u tsr[PS], vr[PS];
-        uint32_t gids[PS];
-        bool vok[PS];
-#pragma unroll
-        for (int j = 0; j < PS; j++) {
-          tsr[j] = v2u{0u, 0u};
-          vr[j] = v2u{0u, 0u};
-          gids[j] = 0;
-          vok[j] = false;
-          if (cb + j * 64 >= nlist) continue;                                  // uniform
-          const uint32_t i = cb + j * 64 + lane;
-          const bool live = i < nlist;
-          const uint2 en = live ? wlist[i] : make_uint2(0u, 0u);
-          gids[j] = en.x;
-          const uint32_t tv = en.y & 0x7ffu, vv = (en.y >> 11) & 0x7ffu;
-          vok[j] = live && ((en.y >> 22) & 1u);
-          tsr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-          if (AGG != AGG_COUNT) vr[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok[j] ? (vb1 + vv) * 8u : OOB, 0, 0);
-        }
-#pragma unroll
-        for (int j = 0; j < PS; j++) {
-          if (cb + j * 64 >= nlist) break;                                     // uniform
-          const int64_t ts = (int64_t)(((uint64_t)tsr[j].y << 32) | tsr[j].x);
-          bool ok = (cb + j * 64 + lane < nlist) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
-          int64_t b = 0;
-          if (P.fast_div) {
-            // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
-            const uint32_t d = uint32_t(ts - P.bucket_base);
-            uint32_t q = uint32_t(double(d) * P.inv_step);
-            int64_t rm = int64_t(d) - int64_t(q) * step32;
-            q = rm < 0 ? q - 1 : (rm >= int64_t(step32) ? q + 1 : q);
-            rm = int64_t(d) - int64_t(q) * step32;
-            if (P.metrics && rm != 0 && ok) {
-              atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
-              ok = false;
-            }
-            b = q;
-          } else if (ok) {
-            if (P.metrics) {
-              const int64_t d = ts - P.bucket_base;
-              b = d / P.step;
-              if (d - b * P.step != 0) {
-                atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
-                ok = false;
-              }
-            } else {
-              b = ((ts - ts % P.step) - P.bucket_base) / P.step;        // ts - ts % step (fmod, truncation)
-            }
-          }
-          if (!ok) continue;
-          if (b < 0 || (uint64_t)b >= P.nbuckets) {
-            atomicOr(P.flags, FLAG_CELL_RANGE);
-            continue;
-          }
-          const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + gids[j];
-          if (cell != acc.key) {
-            lds_merge<AGG>(L, P, acc);
-            acc_reset<AGG>(acc, cell);
-          }
-          const double v = __longlong_as_double((long long)(((uint64_t)vr[j].y << 32) | vr[j].x));
-          acc_add<AGG>(acc, vok[j], v);
-        }
+    // The previous sub-tile's first chunk has had this sub-tile's decode to land; this sub-tile's first chunk
+    // is issued now and consumed after the next decode. Further chunks (dense filters) stream at once.
+    if (stream_on) {
+      consume(pend);
+      pend.n = 0;
+      const uint32_t vb0 = vbase0 + vrun[0], vb1 = vbase1 + vrun[1];
+      if (nlist) issue(pend, 0, nlist, vb0, vb1);
+      for (uint32_t cb = PS * 64; cb < nlist; cb += PS * 64) {
+        Chunk ch;
+        issue(ch, cb, nlist, vb0, vb1);
+        consume(ch);
       }
     }
 #pragma unroll
     for (int c = 0; c < NC; c++) vrun[c] = vnext[c];
-    // the wave's list is rewritten only by this wave (next sub-tile's step D, after its own reads)
+    // the list entries were copied to registers; the wave rewrites its list only after this point
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     LK_STAMP(7)
   }
+  consume(pend);
 #undef LK_STAMP
   if (stamp && tid == 0) {
     unsigned long long* o = P.stamps + LK_NSTAMP * (size_t(blockIdx.y) * P.max_tiles + blockIdx.x);
