@@ -33,6 +33,10 @@ QUERIES = {
                        "q2": {"k": "resource.service.name", "v": ["^svc-0[0-4]"], "op": "regex"}},
                agg="max", group_bys=["resource.service.name", "resource.k8s.namespace.name"],
                desc=":and(:eq name, :re service ^svc-0[0-4]) :by service,namespace :max, step 1m"),
+    # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
+    "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
+                          "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
+                  desc=":in _cardinalhq.name=<all 16> :sum, step 1m"),
 }
 
 
@@ -48,7 +52,7 @@ def main():
     ap.add_argument("--segments", type=int, default=64, help="segments per GPU")
     ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
-    ap.add_argument("--cpu-sample", type=int, default=2, help="segments timed on the CPU oracle (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=12, help="segments timed on the CPU oracle (0: skip)")
     ap.add_argument("--gen-workers", type=int, default=4)
     args = ap.parse_args()
 

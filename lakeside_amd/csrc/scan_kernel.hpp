@@ -373,6 +373,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   const int64_t win_lo = L.win_lo, win_hi = L.win_hi;
   const unsigned long long glob_base = (unsigned long long)uni(L.glob_slot) * P.nbuckets;
   const uint32_t step32 = uint32_t(P.step);
+  // Zone-map bucket: when the tile's timestamps (exact min/max of its non-NULL values) all lie in the window
+  // and in one step bucket, every listed row's bucket is known without reading its timestamp.
+  int64_t tile_b = -1;
+  {
+    const int64_t tmin = tdp->ts_min, tmax = tdp->ts_max;
+    if (tmin >= win_lo && tmax < win_hi) {
+      if (P.metrics) {
+        if (tmin == tmax && (tmin - P.bucket_base) % P.step == 0) tile_b = (tmin - P.bucket_base) / P.step;
+      } else {
+        const int64_t b0 = ((tmin - tmin % P.step) - P.bucket_base) / P.step;
+        const int64_t b1 = ((tmax - tmax % P.step) - P.bucket_base) / P.step;
+        if (b0 == b1) tile_b = b0;
+      }
+      if (tile_b >= int64_t(P.nbuckets)) tile_b = -1;   // out of the cell space: the per-row path flags it
+    }
+  }
+  const bool one_bucket = tile_b >= 0;
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
@@ -402,7 +419,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const uint32_t tv = en.y & 0x7ffu, vv = (en.y >> 11) & 0x7ffu;
       const bool vok = live && ((en.y >> 22) & 1u);
       ch.vok |= uint32_t(vok) << j;
-      ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+      if (!one_bucket) ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
       if (AGG != AGG_COUNT) ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
     }
   };
@@ -411,9 +428,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     for (int j = 0; j < PS; j++) {
       if (uint32_t(j * 64) >= ch.n) break;                                     // uniform
       const int64_t ts = (int64_t)(((uint64_t)ch.ts[j].y << 32) | ch.ts[j].x);
-      bool ok = (uint32_t(j * 64 + lane) < ch.n) && ts >= win_lo && ts < win_hi;   // BaseExpr.scala:159-161
+      bool ok = (uint32_t(j * 64 + lane) < ch.n) && (one_bucket || (ts >= win_lo && ts < win_hi));   // BaseExpr.scala:159-161
       int64_t b = 0;
-      if (P.fast_div) {
+      if (one_bucket) {
+        b = tile_b;
+      } else if (P.fast_div) {
         // d < 2^32: q from the double reciprocal is off by at most one; fix with the remainder
         const uint32_t d = uint32_t(ts - P.bucket_base);
         uint32_t q = uint32_t(double(d) * P.inv_step);

@@ -69,8 +69,10 @@ def test_no_segments_sentinel(engine):
     assert rows == [[(-1, -1.0, {})]]
 
 
-def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys, step=60000, glob_size=10):
-    """Synthetic segments written by tools/synth.cpp, evaluated by the GPU and by the oracle on the same bytes."""
+def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys, step=60000, glob_size=10,
+                window=None):
+    """Synthetic segments written by tools/synth.cpp, evaluated by the GPU and by the oracle on the same bytes.
+    window=(lo, hi): the segment requests' [startTs, endTs) narrowed by lo ms at the start and hi ms at the end."""
     import pyarrow as pa  # noqa: F401
     from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
     from lakeside_amd import synth
@@ -85,6 +87,9 @@ def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys,
         s.free()
         keys.append(key)
         segs.append(synth.segment_request(i, step=step))
+        if window:
+            segs[-1]["startTs"] += window[0]
+            segs[-1]["endTs"] -= window[1]
     req = json.dumps(synth.pushdown(filt, segs, agg, group_bys))
     pr = dx.parse_pushdown(req)
     cells = dx.evaluate_glob_cells(pr, glob_size, keys, sources=blobs)
@@ -124,6 +129,26 @@ def test_groupby_count_min_with_nulls(engine):
             "q2": synth.leaf(synth.NAMESPACE, "in", "ns-01")}
     _synth_case(engine, 2, 1 << 18, 1, 0.05, filt, "count", [synth.NAMESPACE], step=300000)
     _synth_case(engine, 2, 1 << 18, 1, 0.05, filt, "min", [synth.NAMESPACE], step=10000)
+
+
+def test_zone_map_bucket_paths(engine):
+    """Tiles whose timestamps fall in one step bucket skip the timestamp read (zone-map bucket); the others read
+    it. 2^22 rows/hour at a 1m step: most 32K-row tiles sit inside one minute, some straddle a boundary; a 1h
+    step puts every tile in one bucket; a 7s step none."""
+    from lakeside_amd import synth
+    filt = synth.leaf(synth.NAME, "in", "metric_03", "metric_11")
+    _synth_case(engine, 2, 1 << 22, 1, 0.05, filt, "sum", [synth.NAME])
+    _synth_case(engine, 1, 1 << 22, 0, 0.0, filt, "count", [], step=3600000)
+    _synth_case(engine, 1, 1 << 21, 1, 0.0, filt, "max", [], step=7000)
+
+
+def test_window_cuts_tiles(engine):
+    """A glob window narrower than the data: tiles crossing either edge filter rows by timestamp, tiles outside
+    are skipped by their zone map."""
+    from lakeside_amd import synth
+    filt = synth.leaf(synth.NAME, "eq", "metric_05")
+    _synth_case(engine, 2, 1 << 21, 1, 0.02, filt, "sum", [], window=(7 * 60000 + 123, 11 * 60000 - 17))
+    _synth_case(engine, 1, 1 << 21, 0, 0.0, filt, "count", [], step=3600000, window=(60000, 0))
 
 
 def test_full_size_properties(engine):
