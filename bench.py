@@ -141,9 +141,11 @@ def main():
         f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows")
 
     traffic = None
-    prof = os.path.join(ROOT, "profiles", f"pmc_{args.query}.json")
-    if os.path.exists(prof):
-        with open(prof) as f:
+    # PMC-measured HBM bytes per launch of the scan kernel, newest round's summary (scripts/gpu_bench_prof.sh)
+    import glob as _glob
+    profs = sorted(_glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{args.query}.json")))
+    if profs:
+        with open(profs[-1]) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
     cpu = None
