@@ -33,6 +33,11 @@ QUERIES = {
                        "q2": {"k": "resource.service.name", "v": ["^svc-0[0-4]"], "op": "regex"}},
                agg="max", group_bys=["resource.service.name", "resource.k8s.namespace.name"],
                desc=":and(:eq name, :re service ^svc-0[0-4]) :by service,namespace :max, step 1m"),
+    # C4 (configs[3], per GPU): :eq name :sum :by service (an unrestricted group dim: at N > 1 the ranks agree on
+    # the sorted union of their dictionaries before the scan)
+    "c4": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                       "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.service.name"],
+               desc=":eq _cardinalhq.name=metric_07 :sum :by resource.service.name, step 1m"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],

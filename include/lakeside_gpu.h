@@ -75,11 +75,20 @@ void lk_result_free(lk_result* r);
 
 const char* lk_last_error(void);
 
-/* ---- multi-GPU (one process per GPU; segments sharded across ranks, partial tables merged over RCCL) ---- */
+/* ---- multi-GPU (one process per GPU; segments sharded across ranks, partial tables merged over RCCL) ----
+ * Replaces the pod fan-out + query-api merge: SegmentSequencer.allSources (query-api/.../engine/
+ * SegmentSequencer.scala:53-160), QueryEngineV2.mergeSortedSource (QueryEngineV2.scala:76-97) and
+ * TimeGroupedSketchAggregator (core/.../eval/TimeGroupedSketchAggregator.scala:57-177). */
 #define LK_UNIQUE_ID_BYTES 128
 /* Fill `id` (LK_UNIQUE_ID_BYTES) on rank 0; broadcast it out of band (e.g. torch.distributed). */
 int lk_comm_unique_id(uint8_t* id);
 int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank);
+/* Host transport instead of RCCL (e.g. torch.distributed/gloo or MPI supplied by the caller; also lets several
+ * ranks share one GPU, which RCCL refuses).  fn(user, send, bytes, recv) must all-gather `bytes` from every rank
+ * into recv (world * bytes, rank order) and return 0; it is called from inside lk_eval_pushdown_dist, on the
+ * calling thread, the same number of times with the same sizes on every rank. */
+typedef int (*lk_allgather_fn)(void* user, const void* send, size_t bytes, void* recv);
+int lk_comm_init_host(lk_engine* e, int world, int rank, lk_allgather_fn fn, void* user);
 /* Like lk_eval_pushdown with LK_MERGED, but this rank evaluates only the segments whose index i has
  * shard[i] == rank; partial tables are reduced to rank 0 over RCCL, which alone receives rows
  * (other ranks get an empty result). shard == NULL: i % world. */

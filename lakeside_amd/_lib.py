@@ -48,6 +48,10 @@ SIGNATURES = [
                                          _c.POINTER(_c.c_int32), _c.c_int, _c.POINTER(_P)]),
 ]
 
+# int (*lk_allgather_fn)(void* user, const void* send, size_t bytes, void* recv)
+ALLGATHER_FN = _c.CFUNCTYPE(_c.c_int, _c.c_void_p, _c.c_void_p, _c.c_size_t, _c.c_void_p)
+SIGNATURES.append(("lk_comm_init_host", _c.c_int, [_P, _c.c_int, _c.c_int, ALLGATHER_FN, _c.c_void_p]))
+
 
 class LakesideError(RuntimeError):
     def __init__(self, code, msg):

@@ -1,16 +1,26 @@
-// RCCL over xGMI: the exchange step of the sharded evaluation.
+// The exchange step of the sharded evaluation: RCCL over xGMI (default), or a caller-supplied host all-gather.
 //
 // Reference: segments are spread over worker pods by Math.floorMod(segmentId.hashCode, pods)
 // (core/.../discovery/WorkerManager.scala:150-156) and the per-pod partial aggregates are merged by the
 // query-api (TimeGroupedSketchAggregator.scala:57-114).  Here each GPU scans its shard into a partial
-// table in a key space every rank derives identically from the request, then one reduce lands the
-// merged table on rank 0, which alone finalizes and emits.  Tables are small (KB-MB): the reduce is
-// latency-bound, a single collective per array.
+// table in a key space every rank derives identically from the request (bucket space from the window;
+// group dims from the filter, or from the sorted union of every rank's dictionary), then rank 0 gathers the
+// partial tables, folds them in rank order (merge_tables) and alone finalizes and emits.
+//
+// Two primitives carry everything:
+//   allgather_bytes: every rank's host blob (variable length) -> all ranks, in rank order
+//     (glob column unions, dictionaries);
+//   gather_table: every rank's device table block -> rank 0's device buffer, in rank order.
+// RCCL: all-gather of sizes + padded blobs; grouped ncclSend/ncclRecv into rank 0 (each peer on its own xGMI
+// link, the tables are KB-MB so this is latency-bound).  Host transport (lk_comm_init_host): the caller's
+// fixed-size all-gather callback (e.g. torch.distributed/gloo, MPI) over host copies of the same buffers;
+// it lets several ranks share one GPU (RCCL refuses two ranks on one device), and feeds the same merge.
 #include "comm.hpp"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cstring>
 #include <string>
 
@@ -19,12 +29,6 @@
 #include "plan.hpp"
 
 namespace lk {
-
-struct Comm {
-  ncclComm_t comm = nullptr;
-  int world = 1;
-  int rank = 0;
-};
 
 #define NCCL_TRY(x)                                                                            \
   do {                                                                                         \
@@ -40,48 +44,142 @@ struct Comm {
       throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
   } while (0)
 
+struct Comm {
+  int world = 1;
+  int rank = 0;
+  virtual ~Comm() = default;
+  // host blobs of every rank, rank order
+  virtual std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) = 0;
+  // `bytes` of device memory from every rank into rank 0's `recv` (world * bytes; slot 0 is left untouched),
+  // ordered on E.stream
+  virtual void gather_table(Engine& E, const void* send, void* recv, size_t bytes) = 0;
+};
+
+namespace {
+
+struct RcclComm final : Comm {
+  ncclComm_t comm = nullptr;
+  ~RcclComm() override {
+    if (comm) ncclCommDestroy(comm);
+  }
+
+  std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) override {
+    if (world == 1) return {mine};
+    HIP_TRY2(hipSetDevice(E.device));
+    hipStream_t st = E.stream;
+    uint64_t* dsz = static_cast<uint64_t*>(E.workspace("comm_sizes", size_t(world) * 8));
+    std::vector<uint64_t> sz(size_t(world), 0);
+    sz[size_t(rank)] = mine.size();
+    HIP_TRY2(hipMemcpyAsync(dsz + rank, &sz[size_t(rank)], 8, hipMemcpyHostToDevice, st));
+    NCCL_TRY(ncclAllGather(dsz + rank, dsz, 1, ncclUint64, comm, st));
+    HIP_TRY2(hipMemcpyAsync(sz.data(), dsz, size_t(world) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY2(hipStreamSynchronize(st));
+    uint64_t mx = 1;
+    for (uint64_t x : sz) mx = std::max(mx, x);
+    uint8_t* d = static_cast<uint8_t*>(E.workspace("comm_blobs", size_t(world) * mx));
+    if (!mine.empty())
+      HIP_TRY2(hipMemcpyAsync(d + size_t(rank) * mx, mine.data(), mine.size(), hipMemcpyHostToDevice, st));
+    NCCL_TRY(ncclAllGather(d + size_t(rank) * mx, d, mx, ncclUint8, comm, st));
+    std::string all(size_t(world) * mx, '\0');
+    HIP_TRY2(hipMemcpyAsync(&all[0], d, all.size(), hipMemcpyDeviceToHost, st));
+    HIP_TRY2(hipStreamSynchronize(st));
+    std::vector<std::string> out(static_cast<size_t>(world));
+    for (int r = 0; r < world; r++) out[size_t(r)] = all.substr(size_t(r) * mx, sz[size_t(r)]);
+    return out;
+  }
+
+  void gather_table(Engine& E, const void* send, void* recv, size_t bytes) override {
+    if (world == 1) return;
+    NCCL_TRY(ncclGroupStart());
+    if (rank == 0) {
+      for (int r = 1; r < world; r++)
+        NCCL_TRY(ncclRecv(static_cast<uint8_t*>(recv) + size_t(r) * bytes, bytes, ncclUint8, r, comm, E.stream));
+    } else {
+      NCCL_TRY(ncclSend(send, bytes, ncclUint8, 0, comm, E.stream));
+    }
+    NCCL_TRY(ncclGroupEnd());
+  }
+};
+
+struct HostComm final : Comm {
+  lk_allgather_fn fn = nullptr;
+  void* user = nullptr;
+
+  void allgather(const void* send, size_t bytes, void* recv) {
+    if (fn(user, send, bytes, recv) != 0) throw PlanError(LK_ERR_DEVICE, "host transport: all-gather callback failed");
+  }
+
+  std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) override {
+    if (world == 1) return {mine};
+    const uint64_t n = mine.size();
+    std::vector<uint64_t> sz(static_cast<size_t>(world));
+    allgather(&n, 8, sz.data());
+    uint64_t mx = 1;
+    for (uint64_t x : sz) mx = std::max(mx, x);
+    std::string pad(mine);
+    pad.resize(mx, '\0');
+    std::string all(size_t(world) * mx, '\0');
+    allgather(pad.data(), mx, &all[0]);
+    std::vector<std::string> out(static_cast<size_t>(world));
+    for (int r = 0; r < world; r++) out[size_t(r)] = all.substr(size_t(r) * mx, sz[size_t(r)]);
+    return out;
+  }
+
+  void gather_table(Engine& E, const void* send, void* recv, size_t bytes) override {
+    if (world == 1) return;
+    HIP_TRY2(hipSetDevice(E.device));
+    std::vector<uint8_t> mine(bytes), all(size_t(world) * bytes);
+    HIP_TRY2(hipMemcpyAsync(mine.data(), send, bytes, hipMemcpyDeviceToHost, E.stream));
+    HIP_TRY2(hipStreamSynchronize(E.stream));
+    allgather(mine.data(), bytes, all.data());
+    if (rank == 0) {
+      HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + bytes, all.data() + bytes, size_t(world - 1) * bytes,
+                              hipMemcpyHostToDevice, E.stream));
+      HIP_TRY2(hipStreamSynchronize(E.stream));   // `all` is freed on return
+    }
+  }
+};
+
+}  // namespace
+
 int comm_world(const Engine& E) { return E.comm ? E.comm->world : 1; }
 int comm_rank(const Engine& E) { return E.comm ? E.comm->rank : 0; }
 
 void Engine::comm_destroy() {
-  if (comm) {
-    if (comm->comm) ncclCommDestroy(comm->comm);
-    delete comm;
-    comm = nullptr;
-  }
+  delete comm;
+  comm = nullptr;
+}
+
+static Comm& need_comm(Engine& E) {
+  if (!E.comm) throw PlanError(LK_ERR_ARG, "lk_comm_init has not been called");
+  return *E.comm;
 }
 
 void comm_allreduce_max_u8(Engine& E, uint8_t* host, size_t n) {
-  if (!E.comm) throw PlanError(LK_ERR_ARG, "lk_comm_init has not been called");
-  uint8_t* d = static_cast<uint8_t*>(E.workspace("comm_u8", n));
-  HIP_TRY2(hipSetDevice(E.device));
-  HIP_TRY2(hipMemcpyAsync(d, host, n, hipMemcpyHostToDevice, E.stream));
-  NCCL_TRY(ncclAllReduce(d, d, n, ncclUint8, ncclMax, E.comm->comm, E.stream));
-  HIP_TRY2(hipMemcpyAsync(host, d, n, hipMemcpyDeviceToHost, E.stream));
-  HIP_TRY2(hipStreamSynchronize(E.stream));
+  Comm& C = need_comm(E);
+  if (C.world == 1) return;
+  std::vector<std::string> all = C.allgather_bytes(E, std::string(reinterpret_cast<const char*>(host), n));
+  for (auto& b : all) {
+    if (b.size() != n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
+    for (size_t i = 0; i < n; i++) host[i] = std::max(host[i], uint8_t(b[i]));
+  }
+}
+
+std::vector<std::string> comm_allgather_bytes(Engine& E, const std::string& mine) {
+  return need_comm(E).allgather_bytes(E, mine);
 }
 
 void comm_reduce_table(Engine& E, const QParams& P, int agg, size_t nc) {
-  if (!E.comm) throw PlanError(LK_ERR_ARG, "lk_comm_init has not been called");
-  Comm& C = *E.comm;
+  Comm& C = need_comm(E);
   if (C.world == 1) return;
-  ncclComm_t cm = C.comm;
-  hipStream_t st = E.stream;
-  NCCL_TRY(ncclReduce(P.rows, P.rows, nc, ncclUint64, ncclSum, 0, cm, st));
-  NCCL_TRY(ncclReduce(P.cnt, P.cnt, nc, ncclUint64, ncclSum, 0, cm, st));
-  if (agg == AGG_MIN) NCCL_TRY(ncclReduce(P.ext, P.ext, nc, ncclUint64, ncclMin, 0, cm, st));
-  if (agg == AGG_MAX) NCCL_TRY(ncclReduce(P.ext, P.ext, nc, ncclUint64, ncclMax, 0, cm, st));
-  if (agg == AGG_SUM) {
-    // hi and lo are adjacent in the table: one 2*nc-double message per rank, merged in rank order
-    double* parts = C.rank == 0 ? static_cast<double*>(E.workspace("comm_parts", size_t(C.world) * nc * 16)) : nullptr;
-    NCCL_TRY(ncclGroupStart());
-    if (C.rank == 0) {
-      for (int r = 1; r < C.world; r++) NCCL_TRY(ncclRecv(parts + size_t(r) * nc * 2, nc * 2, ncclFloat64, r, cm, st));
-    } else {
-      NCCL_TRY(ncclSend(P.hi, nc * 2, ncclFloat64, 0, cm, st));
-    }
-    NCCL_TRY(ncclGroupEnd());
-    if (C.rank == 0) HIP_TRY2(launch_merge_dd(P.hi, P.lo, parts, C.world, nc, st));
+  // the table is one contiguous block [rows | cnt | hi | lo | ext] (eval.cpp)
+  const size_t bytes = nc * 8 * 5;
+  unsigned long long* parts =
+      C.rank == 0 ? static_cast<unsigned long long*>(E.workspace("comm_parts", size_t(C.world) * bytes)) : nullptr;
+  C.gather_table(E, P.rows, parts, bytes);
+  if (C.rank == 0) {
+    TableRef T{P.rows, P.cnt, P.hi, P.lo, P.ext};
+    HIP_TRY2(launch_merge_tables(T, parts, C.world, nc, agg, E.stream));
   }
 }
 
@@ -112,7 +210,7 @@ int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
   if (hipSetDevice(E.device) != hipSuccess) return LK_ERR_DEVICE;
   ncclUniqueId u;
   memcpy(&u, id, sizeof(u));
-  auto* C = new lk::Comm();
+  auto* C = new lk::RcclComm();
   C->world = world;
   C->rank = rank;
   ncclResult_t r = ncclCommInitRank(&C->comm, world, u, rank);
@@ -121,6 +219,22 @@ int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
     delete C;
     return LK_ERR_DEVICE;
   }
+  E.comm = C;
+  return LK_OK;
+}
+
+int lk_comm_init_host(lk_engine* e, int world, int rank, lk_allgather_fn fn, void* user) {
+  if (!e || !fn || world < 1 || rank < 0 || rank >= world) return LK_ERR_ARG;
+  lk::Engine& E = *e->e;
+  if (E.comm) {
+    lk::set_error("communicator already initialised");
+    return LK_ERR_ARG;
+  }
+  auto* C = new lk::HostComm();
+  C->world = world;
+  C->rank = rank;
+  C->fn = fn;
+  C->user = user;
   E.comm = C;
   return LK_OK;
 }

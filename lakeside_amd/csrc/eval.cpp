@@ -55,7 +55,39 @@ struct StrCol {
   uint32_t lbase = 0, lmask = 0, hmask = 0;
   uint32_t dict_n = 0;                    // snapshot of the global dictionary size
   std::vector<int> dim_of_cand_null;      // restricted: candidate positions that collapse to absent
+  // distributed, unrestricted dim: the sorted union of every rank's dictionary (dim id = position), and
+  // this engine's global id -> position
+  bool exchanged = false;
+  std::vector<std::string> uvals;
+  std::vector<uint32_t> upos;
+  // the string of dim id d (d != dim_null); `gd` is this column's engine dictionary (caller holds its lock)
+  const std::string& dim_value(uint32_t d, const GlobalDict& gd) const {
+    return restricted ? cand[d] : exchanged ? uvals[d] : gd.vals[d];
+  }
 };
+
+// Length-prefixed encoding of a dictionary's values (the exchange blob) and its inverse.
+std::string pack_strings(const std::deque<std::string>& vals, size_t n) {
+  std::string out;
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t len = uint32_t(vals[i].size());
+    out.append(reinterpret_cast<const char*>(&len), 4);
+    out.append(vals[i]);
+  }
+  return out;
+}
+
+void unpack_strings(const std::string& blob, std::vector<std::string>& out) {
+  size_t o = 0;
+  while (o + 4 <= blob.size()) {
+    uint32_t len;
+    memcpy(&len, blob.data() + o, 4);
+    o += 4;
+    if (o + len > blob.size()) throw PlanError(LK_ERR_DEVICE, "internal: truncated dictionary exchange");
+    out.emplace_back(blob, o, len);
+    o += len;
+  }
+}
 
 struct GlobInfo {
   std::vector<int> segs;                  // request indices
@@ -285,8 +317,26 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       sc.restricted = true;
       sc.ndim = uint32_t(sc.cand.size()) + 1;     // + absent
       sc.dim_null = uint32_t(sc.cand.size());
+    } else if (dist) {
+      // Every rank holds its own engine dictionary: agree on one dim space, the sorted union of all ranks'
+      // values (RCCL all-gather of the dictionaries; identical on every rank, so the partial tables align).
+      std::string mine;
+      {
+        std::lock_guard<std::mutex> g(gd.mu);
+        mine = pack_strings(gd.vals, sc.dict_n);
+      }
+      for (const std::string& blob : comm_allgather_bytes(E, mine)) unpack_strings(blob, sc.uvals);
+      std::sort(sc.uvals.begin(), sc.uvals.end());
+      sc.uvals.erase(std::unique(sc.uvals.begin(), sc.uvals.end()), sc.uvals.end());
+      if (sc.uvals.size() + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
+      sc.exchanged = true;
+      sc.ndim = uint32_t(sc.uvals.size()) + 1;
+      sc.dim_null = uint32_t(sc.uvals.size());
+      std::lock_guard<std::mutex> g(gd.mu);
+      sc.upos.resize(sc.dict_n);
+      for (uint32_t i = 0; i < sc.dict_n; i++)
+        sc.upos[i] = uint32_t(std::lower_bound(sc.uvals.begin(), sc.uvals.end(), gd.vals[i]) - sc.uvals.begin());
     } else {
-      if (dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed group-by over an unrestricted column (round 1)");
       if (sc.dict_n + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
       sc.ndim = sc.dict_n + 1;
       sc.dim_null = sc.dict_n;
@@ -308,8 +358,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     GlobalDict& gd = E.dict(sc.name);
     std::lock_guard<std::mutex> g(gd.mu);
     bool null_like_present = gd.ids.count("null") || gd.ids.count("");
-    need_tab[s] = !sc.leaves.empty() || sc.restricted || (sc.is_dim && collapse_in_table && null_like_present) ||
-                  (!sc.is_dim && sc.leaves.empty());
+    need_tab[s] = !sc.leaves.empty() || sc.restricted || sc.exchanged ||
+                  (sc.is_dim && collapse_in_table && null_like_present) || (!sc.is_dim && sc.leaves.empty());
     if (!need_tab[s]) continue;
     std::vector<std::regex> res(sc.leaves.size());
     for (size_t j = 0; j < sc.leaves.size(); j++) {
@@ -337,7 +387,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
           dim = it == sc.cand.end() ? sc.dim_null : uint32_t(it - sc.cand.begin());
           if (collapse_in_table && null_like(v)) dim = sc.dim_null;
         } else {
-          dim = (collapse_in_table && null_like(v)) ? sc.dim_null : gid;
+          dim = (collapse_in_table && null_like(v)) ? sc.dim_null : (sc.exchanged ? sc.upos[gid] : gid);
         }
       }
       tab[gid] = (bits << 24) | dim;
@@ -375,8 +425,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       for (uint32_t d = 0; d < sc.ndim; d++) {
         m[d] = d;
         if (d == sc.dim_null) continue;
-        const std::string& v = sc.restricted ? sc.cand[d] : gd.vals[d];
-        if (null_like(v)) { m[d] = sc.dim_null; any = true; }
+        if (null_like(sc.dim_value(d, gd))) { m[d] = sc.dim_null; any = true; }
       }
       if (any) { fold_maps[s] = std::move(m); rekey = true; }
     }
@@ -520,7 +569,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     GlobalDict& gd = E.dict(kName);
     std::lock_guard<std::mutex> g(gd.mu);
     for (uint32_t d = 0; d < strs[0].ndim; d++) {
-      const std::string* v = d == strs[0].dim_null ? nullptr : (strs[0].restricted ? &strs[0].cand[d] : &gd.vals[d]);
+      const std::string* v = d == strs[0].dim_null ? nullptr : &strs[0].dim_value(d, gd);
       if (v && !null_like(*v)) order.emplace_back(TagList{{"name", *v}}, d);
       else order.emplace_back(qt, d);
     }
@@ -721,9 +770,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       const StrCol& sc = strs[col_str[c]];
       uint32_t d = uint32_t((gid[r] / sc.stride) % sc.ndim);
       const std::string* v = nullptr;
-      if (d != sc.dim_null) v = sc.restricted ? &sc.cand[d] : &gds[col_str[c]]->vals[d];
+      if (d != sc.dim_null) v = &sc.dim_value(d, *gds[col_str[c]]);
       if (v && !null_like(*v)) {
-        if (sc.restricted) {
+        if (sc.restricted || sc.exchanged) {   // strings local to this call: the result keeps a copy
           res->owned.push_back(*v);
           v = &res->owned.back();
         }

@@ -178,21 +178,36 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
   }
 }
 
-// Rank 0 of a sharded evaluation: add ranks 1..world-1's compensated sums (gathered as [hi | lo] blocks)
-// to its own, in rank order, so the merged sum is deterministic for a given shard assignment.
-__global__ __launch_bounds__(256) void merge_dd(double* hi, double* lo, const double* parts, int world, size_t nc) {
+// Rank 0 of a sharded evaluation: fold ranks 1..world-1's partial tables (gathered whole, one [rows | cnt | hi |
+// lo | ext] block of nc cells each, in rank order) into its own. rows/cnt add, min/max compare the
+// order-preserving bits (exact), compensated sums add hi by TwoSum in rank order, so the merged sum is
+// deterministic for a given shard assignment.
+__global__ __launch_bounds__(256) void merge_tables(TableRef T, const unsigned long long* parts, int world, size_t nc,
+                                                    int agg) {
   size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
   if (i >= nc) return;
-  double h = hi[i], l = lo[i];
+  unsigned long long rows = T.rows[i], cnt = T.cnt[i], ext = T.ext[i];
+  double h = T.hi[i], l = T.lo[i];
   for (int r = 1; r < world; r++) {
-    const double* p = parts + size_t(r) * nc * 2;
-    double s, e;
-    two_sum(h, p[i], s, e);
-    h = s;
-    l += e + p[nc + i];
+    const unsigned long long* p = parts + size_t(r) * nc * 5;
+    rows += p[i];
+    cnt += p[nc + i];
+    if (agg == AGG_SUM) {
+      double s, e;
+      two_sum(h, __longlong_as_double((long long)p[2 * nc + i]), s, e);
+      h = s;
+      l += e + __longlong_as_double((long long)p[3 * nc + i]);
+    } else if (agg == AGG_MIN) {
+      ext = min(ext, p[4 * nc + i]);
+    } else if (agg == AGG_MAX) {
+      ext = max(ext, p[4 * nc + i]);
+    }
   }
-  hi[i] = h;
-  lo[i] = l;
+  T.rows[i] = rows;
+  T.cnt[i] = cnt;
+  T.hi[i] = h;
+  T.lo[i] = l;
+  T.ext[i] = ext;
 }
 
 // Merged min/max when values can be NULL: per-glob cells keep NULL, "null" and "" group values apart (DuckDB
@@ -229,9 +244,10 @@ hipError_t launch_rekey_minmax(const RParams& R, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_merge_dd(double* hi, double* lo, const double* parts, int world, size_t nc, hipStream_t stream) {
-  if (nc == 0) return hipSuccess;
-  hipLaunchKernelGGL(merge_dd, dim3(uint32_t((nc + 255) / 256)), dim3(256), 0, stream, hi, lo, parts, world, nc);
+hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
+                              hipStream_t stream) {
+  if (nc == 0 || world <= 1) return hipSuccess;
+  hipLaunchKernelGGL(merge_tables, dim3(uint32_t((nc + 255) / 256)), dim3(256), 0, stream, T, parts, world, nc, agg);
   return hipGetLastError();
 }
 

@@ -48,7 +48,16 @@ struct RParams {                   // rekey_minmax: per-glob uncollapsed table -
 
 hipError_t launch_rekey_minmax(const RParams& R, hipStream_t stream);
 
-hipError_t launch_merge_dd(double* hi, double* lo, const double* parts, int world, size_t nc, hipStream_t stream);
+// The aggregation table: one contiguous block [rows | cnt | hi | lo | ext] of nc cells each.
+struct TableRef {
+  unsigned long long* rows;
+  unsigned long long* cnt;
+  double* hi;
+  double* lo;
+  unsigned long long* ext;
+};
+hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
+                               hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
 uint32_t finalize_blocks(unsigned long long nkeys);
 // d_counts must hold finalize_blocks(nkeys) + 1 entries; the row total lands in d_counts[nblocks].

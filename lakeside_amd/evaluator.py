@@ -22,35 +22,58 @@ Row = Tuple[int, float, Dict[str, str]]
 
 
 class Result:
-    """Rows of one evaluation (copied out of the library result)."""
+    """Rows of one evaluation.  Timestamps/values are copied out at once; tag strings are read from the library
+    result on first use (the result handle is owned here and freed on close / garbage collection)."""
 
     def __init__(self, handle):
         L = _lib.lib()
+        self._h = handle
         n = L.lk_result_num_rows(handle)
         self.ts = np.ctypeslib.as_array(L.lk_result_timestamps(handle), (n,)).copy() if n else np.zeros(0, np.int64)
         self.values = np.ctypeslib.as_array(L.lk_result_values(handle), (n,)).copy() if n else np.zeros(0)
         self.globs = np.ctypeslib.as_array(L.lk_result_globs(handle), (n,)).copy() if n else np.zeros(0, np.uint32)
         ncol = L.lk_result_num_tag_columns(handle)
         self.tag_names = [L.lk_result_tag_name(handle, c).decode() for c in range(ncol)]
-        self._tags = []
-        for r in range(n):
-            t = {}
-            for c in range(ncol):
-                v = L.lk_result_tag_value(handle, r, c)
-                if v is not None:
-                    t[self.tag_names[c]] = v.decode()
-            self._tags.append(t)
+        self._tags = None
         self.stats = json.loads(L.lk_result_stats(handle).decode())
+
+    @property
+    def tags(self) -> List[Dict[str, str]]:
+        if self._tags is None:
+            if self._h is None:
+                raise ValueError("result closed before its tags were read")
+            L = _lib.lib()
+            out = []
+            for r in range(len(self.ts)):
+                t = {}
+                for c, name in enumerate(self.tag_names):
+                    v = L.lk_result_tag_value(self._h, r, c)
+                    if v is not None:
+                        t[name] = v.decode()
+                out.append(t)
+            self._tags = out
+        return self._tags
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            _lib.lib().lk_result_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
     def __len__(self):
         return len(self.ts)
 
     def rows(self) -> List[Row]:
-        return [(int(t), float(v), g) for t, v, g in zip(self.ts, self.values, self._tags)]
+        return [(int(t), float(v), g) for t, v, g in zip(self.ts, self.values, self.tags)]
 
     def per_glob(self, nglobs: int) -> List[List[Row]]:
         out: List[List[Row]] = [[] for _ in range(nglobs)]
-        for t, v, g, tags in zip(self.ts, self.values, self.globs, self._tags):
+        for t, v, g, tags in zip(self.ts, self.values, self.globs, self.tags):
             out[int(g)].append((int(t), float(v), tags))
         return out
 
@@ -105,10 +128,7 @@ class Engine:
         arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
         h = ctypes.c_void_p()
         check(L.lk_eval_pushdown(self._h, request_json.encode(), arr, len(paths), glob_size, flags, ctypes.byref(h)))
-        try:
-            return Result(h)
-        finally:
-            L.lk_result_free(h)
+        return Result(h)
 
     # ---- multi-GPU ----
     @staticmethod
@@ -121,6 +141,13 @@ class Engine:
         buf = (ctypes.c_uint8 * _lib.LK_UNIQUE_ID_BYTES).from_buffer_copy(uid)
         check(_lib.lib().lk_comm_init(self._h, buf, world, rank))
 
+    def comm_init_host(self, world: int, rank: int, group=None, allgather=None) -> None:
+        """Host transport (lk_comm_init_host) over a torch.distributed group (default: the gloo world), or over
+        `allgather(bytes) -> [bytes per rank]`.  The callback object lives as long as the engine."""
+        from . import dist as _dist
+        self._allgather_cb = _dist.make_callback(allgather or _dist.gloo_allgather(group))
+        check(_lib.lib().lk_comm_init_host(self._h, world, rank, self._allgather_cb, None))
+
     def eval_pushdown_dist(self, request_json: str, paths: Sequence[str], shard: Optional[Sequence[int]] = None,
                            glob_size: int = 10) -> Result:
         L = _lib.lib()
@@ -129,10 +156,7 @@ class Engine:
         h = ctypes.c_void_p()
         check(L.lk_eval_pushdown_dist(self._h, request_json.encode(), arr, len(paths), sh, glob_size,
                                       ctypes.byref(h)))
-        try:
-            return Result(h)
-        finally:
-            L.lk_result_free(h)
+        return Result(h)
 
 
 def evaluate_push_down_request(engine: Engine, query_id: str, local_parquet: bool, push_down_request: str,

@@ -395,6 +395,7 @@ class Cell:
     values: Optional[np.ndarray] = None      # non-null values (for exact sum)
     vmin: float = math.inf
     vmax: float = -math.inf
+    gkey: Tuple = ()                          # the SQL group's raw key values (None = NULL), name first
 
     def agg_value(self, agg: str) -> float:
         """SQL aggregate of the cell, NULL -> 0.0 via JDBC getDouble (Commons.scala:427)."""
@@ -422,17 +423,26 @@ def exact_sum(v: np.ndarray) -> float:
     return math.fsum(v.tolist())
 
 
-def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str], sources=None):
+def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str], sources=None,
+                  only: Optional[Sequence[int]] = None, union: Optional[Sequence[str]] = None):
     """Rows of ONE glob = one DuckDB query (Commons.toGlobResultSet, Commons.scala:200-254, then
     resultSetToSource/toDataPoint 280-341, 399-462).  Returns list of (ts, value, tags) in ascending ts
-    order (ties ordered by tags for determinism; the reference's tie order is arbitrary, S17)."""
+    order (ties ordered by tags for determinism; the reference's tie order is arbitrary, S17).
+
+    Partial evaluation (the sharded protocol's decomposition, checked by tests/test_dist_cpu.py): `only`
+    = positions within the glob whose files are read here; `union` = the glob's column union agreed over
+    every shard.  Window and step still come from the whole glob."""
     be = pr.baseExpr
     chart = be.chart
     segs = [pr.segmentRequests[i] for i in seg_idx]
     vcol = value_column(be)
     fs = field_set(be)
     strings = sorted(set(_leaf_columns(be.filter)) | set(chart.groupBys) | {NAME})
-    union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
+    if only is not None:
+        paths = [paths[j] for j in only]
+        sources = None if sources is None else [sources[j] for j in only]
+    read_union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
+    union = list(union) if union is not None else read_union
     nonexistent = fs - set(union)                                   # Commons.scala:224
     # Columns the generated SQL references but that no file of the glob has: DuckDB raises a Binder
     # Error, which Commons.toGlobResultSet turns into an empty result (Commons.scala:249-253).  This
@@ -476,6 +486,8 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
         if len(v):
             cell.vmin = float(_sql_min(v))
             cell.vmax = float(_sql_max(v))
+        cell.gkey = tuple(c.dictionary[key[s, j + 1]] if key[s, j + 1] >= 0 else None
+                          for j, (_, c) in enumerate(keycols))
         tags = {}
         for j, (name, c) in enumerate(keycols):
             code = key[s, j + 1]
@@ -557,6 +569,28 @@ def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, 
         out.append((cs[0].ts, val, tags))
     out.sort(key=lambda r: (r[0], sorted(r[2].items()), r[1]))
     return out
+
+
+def merge_partial_cells(parts) -> list:
+    """Fold one glob's partial cells from several shards (lists of Cell) into the glob's cells: cells of the
+    same SQL group (bucket, raw key values) add rows/counts/values and take min/max, exactly as rank 0's
+    table merge does (lakeside_amd/csrc/kernels.hip merge_tables)."""
+    merged: Dict[Any, Cell] = {}
+    for cells in parts:
+        for c in cells:
+            k = (c.ts, c.gkey)
+            m = merged.get(k)
+            if m is None:
+                merged[k] = Cell(ts=c.ts, tags=dict(c.tags), rows=c.rows, count=c.count,
+                                 values=np.array(c.values, dtype=np.float64), vmin=c.vmin, vmax=c.vmax, gkey=c.gkey)
+                continue
+            m.rows += c.rows
+            m.count += c.count
+            m.values = np.concatenate([m.values, c.values])
+            if m.count:
+                m.vmin = float(_sql_min(m.values))
+                m.vmax = float(_sql_max(m.values))
+    return list(merged.values())
 
 
 def evaluate_merged(pr: PushDownRequest, paths: Sequence[str], glob_size: int = 10, sources=None):
