@@ -38,6 +38,12 @@ QUERIES = {
     "c4": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
                        "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.service.name"],
                desc=":eq _cardinalhq.name=metric_07 :sum :by resource.service.name, step 1m"),
+    # C5 (configs[4]): 10M-value group key, all segments in hour 0, one 1h bucket (<= 10M datapoints); 8 segments
+    # per GPU (64 over the node)
+    "c5": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                       "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.container.id"],
+               step=3600000, hour=0, highcard_n=10_000_000, segments=8,
+               desc=":eq _cardinalhq.name=metric_07 :sum :by resource.container.id (10M-value dictionary), step 1h"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
@@ -54,7 +60,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--segments", type=int, default=64, help="segments per GPU")
+    ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default: the query's config)")
     ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
     ap.add_argument("--cpu-sample", type=int, default=12, help="segments timed on the CPU oracle (0: skip)")
@@ -82,15 +88,17 @@ def main():
         eng.comm_init(obj[0], world, rank)
 
     # ---- segments of this rank (weak scaling: rank r owns global segments [r*S, (r+1)*S)) ----
-    S = args.segments
     q = QUERIES[args.query]
+    S = args.segments or q.get("segments", 64)
+    step, hour, highcard = q.get("step", 60000), q.get("hour"), q.get("highcard_n", 0)
     total = S * world
     mine = range(rank * S, (rank + 1) * S)
     keys = [f"seg/{i}" for i in range(total)]
     shard = [i // S for i in range(total)]
 
     def gen(i):
-        return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4))
+        return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour,
+                                                        highcard_n=highcard))
 
     t0 = time.time()
     bytes_loaded = 0
@@ -105,7 +113,7 @@ def main():
     log(f"rank {rank}: {S} segments ({bytes_loaded / 1e9:.1f} GB Parquet) resident, HBM cache "
         f"{eng.segment_bytes / 1e9:.1f} GB, load {time.time() - t0:.0f}s")
 
-    segs = [synth.segment_request(i) for i in range(total)]
+    segs = [synth.segment_request(i, step=step, hour=hour) for i in range(total)]
     req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"]))
 
     def step():
@@ -189,12 +197,13 @@ def cpu_baseline(args, q, synth):
     pa.set_io_thread_count(1)
     n = args.cpu_sample
     blobs = []
+    step, hour, highcard = q.get("step", 60000), q.get("hour"), q.get("highcard_n", 0)
     for i in range(n):
-        s = synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4))
+        s = synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour, highcard_n=highcard))
         blobs.append(s.bytes())
         s.free()
     keys = [f"cpu/{i}" for i in range(n)]
-    segs = [synth.segment_request(i) for i in range(n)]
+    segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
     pr = dx.parse_pushdown(json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"])))
     t = time.perf_counter()
     dx.evaluate_merged(pr, keys, 10, sources=blobs)

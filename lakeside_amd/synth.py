@@ -90,3 +90,4 @@ def leaf(k, op, *v):
 NAME = "_cardinalhq.name"
 SERVICE = "resource.service.name"
 NAMESPACE = "resource.k8s.namespace.name"
+CONTAINER = "resource.container.id"

@@ -70,7 +70,7 @@ def test_no_segments_sentinel(engine):
 
 
 def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys, step=60000, glob_size=10,
-                window=None):
+                window=None, highcard_n=0, hour=None):
     """Synthetic segments written by tools/synth.cpp, evaluated by the GPU and by the oracle on the same bytes.
     window=(lo, hi): the segment requests' [startTs, endTs) narrowed by lo ms at the start and hi ms at the end."""
     import pyarrow as pa  # noqa: F401
@@ -80,13 +80,14 @@ def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys,
     keys, blobs, segs = [], [], []
     for i in range(nseg):
         s = synth.make_segment(synth.segment_spec(i, rows=rows, value_mode=value_mode, null_frac=null_frac,
-                                                  rg_rows=1 << 18, page_rows=1 << 15))
-        key = f"synth/{rows}/{value_mode}/{null_frac}/{i}"
+                                                  rg_rows=1 << 18, page_rows=1 << 15, highcard_n=highcard_n,
+                                                  hour=hour))
+        key = f"synth/{rows}/{value_mode}/{null_frac}/{highcard_n}/{hour}/{i}"
         engine.put_segment_ptr(key, s.ptr, s.size)
         blobs.append(s.bytes())
         s.free()
         keys.append(key)
-        segs.append(synth.segment_request(i, step=step))
+        segs.append(synth.segment_request(i, step=step, hour=hour))
         if window:
             segs[-1]["startTs"] += window[0]
             segs[-1]["endTs"] -= window[1]
@@ -149,6 +150,18 @@ def test_window_cuts_tiles(engine):
     filt = synth.leaf(synth.NAME, "eq", "metric_05")
     _synth_case(engine, 2, 1 << 21, 1, 0.02, filt, "sum", [], window=(7 * 60000 + 123, 11 * 60000 - 17))
     _synth_case(engine, 1, 1 << 21, 0, 0.0, filt, "count", [], step=3600000, window=(60000, 0))
+
+
+def test_c5_shape_high_cardinality_group_by(engine):
+    """C5 shape: a high-cardinality group key (resource.container.id, 300k-value dictionary, ~2^18 distinct per
+    row group) over segments of one hour, 1h step: groups far beyond the LDS table spill to the global table."""
+    from lakeside_amd import synth
+    filt = synth.leaf(synth.NAME, "eq", "metric_07")
+    res = _synth_case(engine, 2, 1 << 20, 0, 0.0, filt, "sum", [synth.CONTAINER], step=3600000, highcard_n=300000,
+                      hour=0)
+    assert len(res) > 50000
+    _synth_case(engine, 2, 1 << 19, 1, 0.05, filt, "max", [synth.CONTAINER], step=600000, highcard_n=100000,
+                hour=0)
 
 
 def test_full_size_properties(engine):

@@ -193,7 +193,9 @@ void build_rg(const lk_synth_spec& sp, const std::vector<ColSpec>& cols, uint64_
   out.chunks.resize(cols.size());
   const uint32_t prow = sp.page_rows ? sp.page_rows : 131072;
   for (size_t c = 0; c < cols.size(); c++) {
-    Rng rng(sp.seed * 1000003ull + rg * 131ull + c * 7919ull + 1);
+    // independent stream per (segment, row group, column): the seed goes through a full 64-bit mix, so streams
+    // of neighbouring row groups / columns are not shifted copies of one another
+    Rng rng(Rng(Rng(sp.seed).next() ^ (rg * 0xA24BAED4963EE407ull)).next() ^ (c * 0x9FB21C651E98DF25ull + 1));
     const ColSpec& cs = cols[c];
     std::vector<uint8_t> valid;
     if (cs.kind != TS && sp.null_frac > 0) {
