@@ -126,12 +126,14 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
-    scan_ms, total_ms, alg_bytes, out_rows = [], [], 0, 0
+    scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
         scan_ms.append(res.stats["scan_ms"])
         total_ms.append(res.stats["total_ms"])
+        plan_ms.append(res.stats["plan_ms"])
+        device_ms.append(res.stats["device_ms"])
         alg_bytes = res.stats["algorithmic_bytes"]
         out_rows = len(res)
     torch.cuda.synchronize()
@@ -151,7 +153,8 @@ def main():
     scan_avg = sum(scan_ms) / len(scan_ms)
     achieved = alg_bytes / (scan_avg / 1e3) / 1e9
     log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
-        f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows")
+        f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows; in the call: plan {sum(plan_ms) / len(plan_ms):.2f} ms, "
+        f"device {sum(device_ms) / len(device_ms):.2f} ms, total {sum(total_ms) / len(total_ms):.2f} ms")
 
     traffic = None
     # PMC-measured HBM bytes per launch of the scan kernel, newest round's summary (scripts/gpu_bench_prof.sh)

@@ -135,7 +135,7 @@ const char* lk_result_tag_name(const lk_result* r, size_t col) {
 }
 const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col) {
   if (!r || row >= r->ts.size() || col >= r->tag_names.size()) return nullptr;
-  return r->tag_vals[row * r->tag_names.size() + col];
+  return r->tag(row, col);
 }
 const char* lk_result_stats(const lk_result* r) { return r ? r->stats.c_str() : nullptr; }
 void lk_result_free(lk_result* r) { delete r; }

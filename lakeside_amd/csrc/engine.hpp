@@ -7,6 +7,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <stdexcept>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -18,12 +19,34 @@ namespace lk {
 
 void set_error(const std::string& m);
 
-// Engine-global dictionary of one column name.  Values get dense ids in first-seen order; a deque keeps
-// every string at a stable address (result tag values point into it).
+// Append-only string array in fixed 64K-entry blocks behind a fixed block table: an element never moves, and
+// reading an element published before (under the owner's mutex) needs no lock, so results keep reading tag
+// strings while loads append to the dictionary.
+class StableStrs {
+ public:
+  static constexpr uint32_t kShift = 16, kBlock = 1u << kShift, kMaxBlocks = 1u << 14;   // 2^30 entries
+  size_t size() const { return n_; }
+  const std::string& operator[](size_t i) const { return blocks_[i >> kShift][i & (kBlock - 1)]; }
+  void push_back(const std::string& s) {
+    const size_t b = n_ >> kShift;
+    if (b >= kMaxBlocks) throw std::length_error("dictionary exceeds 2^30 values");
+    if (!blocks_[b]) blocks_[b].reset(new std::string[kBlock]);
+    blocks_[b][n_ & (kBlock - 1)] = s;
+    n_++;
+  }
+  const std::string& back() const { return (*this)[n_ - 1]; }
+
+ private:
+  std::unique_ptr<std::unique_ptr<std::string[]>[]> blocks_{new std::unique_ptr<std::string[]>[kMaxBlocks]};
+  size_t n_ = 0;
+};
+
+// Engine-global dictionary of one column name.  Values get dense ids in first-seen order, at stable
+// addresses (result tag values point into it).
 struct GlobalDict {
   std::mutex mu;
   std::unordered_map<std::string, uint32_t> ids;
-  std::deque<std::string> vals;
+  StableStrs vals;
   uint32_t intern(const std::string& s);   // caller holds mu
 };
 
@@ -102,12 +125,43 @@ struct lk_engine {
   std::unique_ptr<lk::Engine> e;
 };
 
+// Rows of one evaluation, columnar: timestamps, values, glob and group id per row.  Tag strings are decoded
+// from the group id on demand (lk_result_tag_value), so emitting millions of rows costs no per-row host work.
+// Tag values point into the engine's dictionaries: free results before destroying their engine.
 struct lk_result {
   std::vector<int64_t> ts;
   std::vector<double> val;
   std::vector<uint32_t> glob;
-  std::vector<std::string> tag_names;
-  std::vector<const char*> tag_vals;             // row-major: rows x tag columns
+  std::vector<unsigned long long> gid;           // group id: Σ dim id × stride over the group dims
+  std::vector<std::string> tag_names;            // "name", groupBys, then queryTags keys
+  struct TagCol {                                // a "name" / groupBy tag column
+    unsigned long long stride = 1, ndim = 1;
+    uint32_t dim_null = 0;                       // dim id of NULL: tag absent
+    std::vector<const char*> local;              // dim id -> string (nullptr: absent); empty: read `dict`
+    const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id)
+  };
+  std::vector<TagCol> tcols;
+  // Commons.scala:450-452: a row whose own tags are all absent takes its glob head's queryTags
+  std::vector<std::vector<std::pair<size_t, const char*>>> qt_of_glob;   // (tag column, value) per glob
+  bool per_glob = false;
   std::deque<std::string> owned;                 // strings not owned by a dictionary
   std::string stats;
+
+  const char* tag(size_t row, size_t col) const {
+    if (col < tcols.size()) return own_tag(row, col);
+    for (size_t c = 0; c < tcols.size(); c++)
+      if (own_tag(row, c)) return nullptr;
+    for (auto& kv : qt_of_glob[per_glob ? glob[row] : 0])
+      if (kv.first == col) return kv.second;
+    return nullptr;
+  }
+  // S15 (Commons.scala:433): NULL, "null" and "" drop the tag
+  const char* own_tag(size_t row, size_t c) const {
+    const TagCol& t = tcols[c];
+    const uint32_t d = uint32_t((gid[row] / t.stride) % t.ndim);
+    if (d == t.dim_null) return nullptr;
+    if (!t.local.empty()) return t.local[d];
+    const std::string& s = (*t.dict)[d];
+    return (s.empty() || s == "null") ? nullptr : s.c_str();
+  }
 };

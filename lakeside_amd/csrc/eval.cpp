@@ -67,7 +67,7 @@ struct StrCol {
 };
 
 // Length-prefixed encoding of a dictionary's values (the exchange blob) and its inverse.
-std::string pack_strings(const std::deque<std::string>& vals, size_t n) {
+std::string pack_strings(const StableStrs& vals, size_t n) {
   std::string out;
   for (size_t i = 0; i < n; i++) {
     const uint32_t len = uint32_t(vals[i].size());
@@ -138,6 +138,50 @@ void collect_leaves(const FilterNode* n, std::vector<const FilterNode*>& out) {
 
 bool null_like(const std::string& s) { return s.empty() || s == "null"; }
 
+// Conjuncts of the filter's top-level AND chain (a AND (b AND c) -> a, b, c).
+void conjuncts(const FilterNode* n, std::vector<const FilterNode*>& out) {
+  if (n->kind == FilterNode::AND) {
+    conjuncts(n->a.get(), out);
+    conjuncts(n->b.get(), out);
+  } else {
+    out.push_back(n);
+  }
+}
+
+// Truth table of a postfix Kleene program over L leaves: bit (T | F << L) = the program is TRUE.  An empty
+// program is TRUE.
+std::vector<uint32_t> truth_table(const std::vector<uint8_t>& prog, uint32_t L) {
+  std::vector<uint32_t> truth(((1u << (2 * L)) + 31) / 32, 0u);
+  for (uint32_t idx = 0; idx < (1u << (2 * L)); idx++) {
+    const uint32_t T = idx & ((1u << L) - 1), F = idx >> L;
+    uint64_t st = 0, sf = 0;
+    for (uint8_t op : prog) {
+      if (op < 0x80) {
+        st = (st << 1) | ((T >> op) & 1u);
+        sf = (sf << 1) | ((F >> op) & 1u);
+      } else if (op == OP_NOT) {
+        uint64_t t1 = st & 1, f1 = sf & 1;
+        st = (st & ~1ull) | f1;
+        sf = (sf & ~1ull) | t1;
+      } else if (op == OP_TRUE) {
+        st = (st << 1) | 1;
+        sf = sf << 1;
+      } else {
+        uint64_t t2 = st & 1, f2 = sf & 1;
+        st >>= 1;
+        sf >>= 1;
+        uint64_t t1 = st & 1, f1 = sf & 1;
+        uint64_t tt = op == OP_AND ? (t1 & t2) : (t1 | t2);
+        uint64_t ff = op == OP_AND ? (f1 | f2) : (f1 & f2);
+        st = (st & ~1ull) | tt;
+        sf = (sf & ~1ull) | ff;
+      }
+    }
+    if (prog.empty() || (st & 1)) truth[idx >> 5] |= 1u << (idx & 31);
+  }
+  return truth;
+}
+
 double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
@@ -166,8 +210,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   else if (R.aggregation == "count") agg = AGG_COUNT;
   else if (R.aggregation == "avg") agg = AGG_AVG;
   else throw PlanError(LK_ERR_UNSUPPORTED, "aggregation " + R.aggregation + " (sketch path) is not on the hot path");
-  if (agg == AGG_AVG && !per_glob_rows)
-    throw PlanError(LK_ERR_UNSUPPORTED, "avg is split into sum+count before the merge (QueryEngineV2.scala:280-283)");
+  // Merged avg: query-api runs AVG as separate SUM and COUNT pushdowns, merges them per (timestamp, tags) into
+  // a {sum, count} map and divides (QueryEngineV2.scala:280-283, TimeGroupedSketchAggregator.scala:74-78,
+  // BaseExpr.scala:88-91).  The table holds both, so one scan gives Σsum / Σcount (NaN when no value).
   if (dist && per_glob_rows) throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
   const bool metrics = R.dataset == "metrics";
   const std::string vcol = value_column(R);
@@ -484,38 +529,57 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   uint32_t max_tiles = 0;
   for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
   // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
-  std::vector<uint32_t> truth;
+  std::vector<uint32_t> truth, truth_early, truth_late;
+  uint32_t late_mask = 0;
   if (leaves.size() <= size_t(TT_MAX_LEAVES)) {
     const uint32_t L = uint32_t(leaves.size());
-    truth.assign(((1u << (2 * L)) + 31) / 32, 0u);
-    for (uint32_t idx = 0; idx < (1u << (2 * L)); idx++) {
-      const uint32_t T = idx & ((1u << L) - 1), F = idx >> L;
-      uint64_t st = 0, sf = 0;
-      for (uint8_t op : prog) {
-        if (op < 0x80) {
-          st = (st << 1) | ((T >> op) & 1u);
-          sf = (sf << 1) | ((F >> op) & 1u);
-        } else if (op == OP_NOT) {
-          uint64_t t1 = st & 1, f1 = sf & 1;
-          st = (st & ~1ull) | f1;
-          sf = (sf & ~1ull) | t1;
-        } else {
-          uint64_t t2 = st & 1, f2 = sf & 1;
-          st >>= 1;
-          sf >>= 1;
-          uint64_t t1 = st & 1, f1 = sf & 1;
-          uint64_t tt = op == OP_AND ? (t1 & t2) : (t1 | t2);
-          uint64_t ff = op == OP_AND ? (f1 | f2) : (f1 & f2);
-          st = (st & ~1ull) | tt;
-          sf = (sf & ~1ull) | ff;
-        }
+    truth = truth_table(prog, L);
+    // Predicate pushdown + late materialization.  filter = C_early AND C_late where C_early is the conjuncts
+    // over one "early" column (the name column when a conjunct constrains it alone).  The kernel decodes the
+    // early column for every row, lists the rows where C_early is TRUE, and decodes every other string column
+    // (late filter columns, group dims) only for listed rows, where it evaluates C_late.
+    std::vector<const FilterNode*> conj;
+    conjuncts(R.filter.get(), conj);
+    auto cols_of = [&](const FilterNode* n) {
+      std::vector<const FilterNode*> ls;
+      collect_leaves(n, ls);
+      uint32_t m = 0;
+      for (auto* l : ls) m |= 1u << str_index(l->k);
+      return m;
+    };
+    int early = -1;
+    for (auto* c : conj) {
+      const uint32_t m = cols_of(c);
+      if (__builtin_popcount(m) != 1) continue;
+      const int col = __builtin_ctz(m);
+      if (early < 0 || col == 0) early = col;
+      if (col == 0) break;
+    }
+    // The late pass sees only the late columns' leaves: a conjunct mixing the early column with others keeps
+    // every column early (no late pass).
+    bool mixed = false;
+    for (auto* c : conj) {
+      const uint32_t m = cols_of(c);
+      if (early >= 0 && m != (1u << early) && ((m >> early) & 1u)) mixed = true;
+    }
+    if (early >= 0 && strs.size() >= 2 && !mixed) {
+      std::vector<uint8_t> pe, pl;
+      for (auto* c : conj) {
+        std::vector<uint8_t>& dst = cols_of(c) == (1u << early) ? pe : pl;
+        const bool first = dst.empty();
+        postfix(c, leaves, dst);
+        if (!first) dst.push_back(OP_AND);
       }
-      if (st & 1) truth[idx >> 5] |= 1u << (idx & 31);
+      truth_early = truth_table(pe, L);
+      truth_late = truth_table(pl, L);
+      for (size_t sidx = 0; sidx < strs.size(); sidx++)
+        if (int(sidx) != early) late_mask |= 1u << sidx;
     }
   }
   if (total_tiles >= (1u << 31)) throw PlanError(LK_ERR_UNSUPPORTED, "too many tiles");
 
   // ---- device: upload, zero table, scan ----
+  const double plan_ms = ms_since(t_start);
   std::lock_guard<std::mutex> dev_guard(E.dev_mu);
   HIP_TRY(hipSetDevice(E.device));
   hipStream_t st = E.stream;
@@ -551,6 +615,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   auto reserve = [&](size_t n) { size_t o = (off + 255) / 256 * 256; off = o + n; return o; };
   const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
   const size_t o_truth = reserve(truth.size() * 4);
+  const size_t o_truth_e = reserve(truth_early.size() * 4);
+  const size_t o_truth_l = reserve(truth_late.size() * 4);
   std::vector<size_t> o_tab(strs.size());
   for (size_t s = 0; s < strs.size(); s++) o_tab[s] = need_tab[s] ? reserve(tabs[s].size() * 4) : 0;
   const size_t o_flags = reserve(sizeof(uint32_t) * 4);
@@ -584,6 +650,10 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   for (auto& q : qsegs) (void)q;
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
+  if (late_mask) {
+    memcpy(hbuf + o_truth_e, truth_early.data(), truth_early.size() * 4);
+    memcpy(hbuf + o_truth_l, truth_late.data(), truth_late.size() * 4);
+  }
   for (size_t s = 0; s < strs.size(); s++)
     if (need_tab[s]) {
       memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
@@ -596,6 +666,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
   P.flags = reinterpret_cast<uint32_t*>(dbuf + o_flags);
   P.truth = truth.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_truth);
+  P.late_mask = getenv("LK_NO_LATE") ? 0u : late_mask;   // env: diagnostics only (A/B of the late path)
+  P.truth_early = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_e) : nullptr;
+  P.truth_late = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_l) : nullptr;
   P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
 
   // aggregation table (SoA)
@@ -728,17 +801,18 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (hflags & FLAG_METRICS_UNALIGNED)
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
-  std::vector<unsigned long long> gid(nrows_out);
   res->ts.resize(nrows_out);
   res->val.resize(nrows_out);
   res->glob.resize(nrows_out);
+  res->gid.resize(nrows_out);
   if (nrows_out) {
     HIP_TRY(hipMemcpyAsync(res->ts.data(), d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(res->val.data(), d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(gid.data(), d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->gid.data(), d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipMemcpyAsync(res->glob.data(), d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
+  const double device_ms = ms_since(t_start) - plan_ms;
   float scan_ms = 0;
   HIP_TRY(hipEventElapsedTime(&scan_ms, E.ev_scan0, E.ev_scan1));
 
@@ -756,45 +830,50 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     for (auto& kv : g.query_tags)
       if (std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
   for (auto& k : qt_keys) res->tag_names.push_back(k);
-  const size_t ncol = res->tag_names.size();
-  res->tag_vals.assign(size_t(nrows_out) * ncol, nullptr);
-  std::vector<GlobalDict*> gds(strs.size());
-  std::vector<std::unique_lock<std::mutex>> locks;
-  for (size_t s = 0; s < strs.size(); s++) {
-    gds[s] = &E.dict(strs[s].name);
-    locks.emplace_back(gds[s]->mu);
-  }
-  for (uint32_t r = 0; r < nrows_out; r++) {
-    bool any = false;
-    for (size_t c = 0; c < nreg; c++) {
-      const StrCol& sc = strs[col_str[c]];
-      uint32_t d = uint32_t((gid[r] / sc.stride) % sc.ndim);
-      const std::string* v = nullptr;
-      if (d != sc.dim_null) v = &sc.dim_value(d, *gds[col_str[c]]);
-      if (v && !null_like(*v)) {
-        if (sc.restricted || sc.exchanged) {   // strings local to this call: the result keeps a copy
-          res->owned.push_back(*v);
-          v = &res->owned.back();
-        }
-        res->tag_vals[size_t(r) * ncol + c] = v->c_str();
-        any = true;
+  // Per tag column: how a row's group id decodes to the tag string (lk_result::tag; nullptr: tag dropped,
+  // Commons.scala:433).  Strings local to this call (filter candidates, the distributed union) move into the
+  // result once; engine-dictionary strings are read in place (stable addresses, StableStrs).
+  res->per_glob = per_glob_rows;
+  res->tcols.resize(nreg);
+  for (size_t c = 0; c < nreg; c++) {
+    StrCol& sc = strs[col_str[c]];
+    lk_result::TagCol& tc = res->tcols[c];
+    tc.stride = sc.stride ? sc.stride : 1;
+    tc.ndim = sc.ndim;
+    tc.dim_null = sc.dim_null;
+    tc.dict = &E.dict(sc.name).vals;
+    if (!sc.restricted && !sc.exchanged) continue;
+    auto& m = tc.local;
+    bool shared = false;
+    for (size_t c2 = 0; c2 < c && !shared; c2++)   // a groupBy listed twice shares the first column's strings
+      if (col_str[c2] == col_str[c] && !res->tcols[c2].local.empty()) {
+        m = res->tcols[c2].local;
+        shared = true;
       }
-    }
-    if (!any) {   // Commons.scala:450-452: empty tags -> the glob head's queryTags
-      const GlobInfo& g = globs[per_glob_rows ? res->glob[r] : 0];
-      for (auto& kv : g.query_tags) {
-        size_t c = nreg + size_t(std::find(qt_keys.begin(), qt_keys.end(), kv.first) - qt_keys.begin());
-        res->owned.push_back(kv.second);
-        res->tag_vals[size_t(r) * ncol + c] = res->owned.back().c_str();
-      }
+    if (shared) continue;
+    m.assign(sc.ndim, nullptr);
+    for (uint32_t d = 0; d < sc.ndim; d++) {
+      if (d == sc.dim_null) continue;
+      std::string& v = sc.restricted ? sc.cand[d] : sc.uvals[d];
+      if (null_like(v)) continue;
+      if (sc.restricted) res->owned.push_back(v);              // a few filter candidates: copied
+      else res->owned.push_back(std::move(v));                 // the distributed union (large): moved
+      m[d] = res->owned.back().c_str();
     }
   }
+  res->qt_of_glob.resize(globs.size());
+  for (size_t gi = 0; gi < globs.size(); gi++)
+    for (auto& kv : globs[gi].query_tags) {
+      size_t c = nreg + size_t(std::find(qt_keys.begin(), qt_keys.end(), kv.first) - qt_keys.begin());
+      res->owned.push_back(kv.second);
+      res->qt_of_glob[gi].emplace_back(c, res->owned.back().c_str());
+    }
   char buf[512];
   snprintf(buf, sizeof(buf),
-           "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"rows_scanned\":%llu,\"algorithmic_bytes\":%llu,\"tiles\":%u,"
-           "\"cells\":%llu,\"segments\":%zu}",
-           double(scan_ms), ms_since(t_start), (unsigned long long)rows_scanned, (unsigned long long)alg_bytes,
-           total_tiles, (unsigned long long)ncells, qsegs.size());
+           "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"rows_scanned\":%llu,"
+           "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu}",
+           double(scan_ms), ms_since(t_start), plan_ms, device_ms, (unsigned long long)rows_scanned,
+           (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size());
   res->stats = buf;
   return LK_OK;
 }

@@ -72,7 +72,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
       unsigned long long cell = ((unsigned long long)gs * F.nbuckets + b) * F.ngroups + g;
       if (F.rows[cell] == 0) continue;
       unsigned long long c = F.cnt[cell];
-      if (F.agg == AGG_SUM) {
+      if (F.agg == AGG_SUM || F.agg == AGG_AVG) {
         double s, e;
         two_sum(hi, F.hi[cell], s, e);
         hi = s;
@@ -93,6 +93,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   }
   if (!o.exists) return o;
   if (F.agg == AGG_SUM) o.value = hi + lo;
+  else if (F.agg == AGG_AVG) o.value = (hi + lo) / double(cnt);   // merged {sum, count} map: 0/0 = NaN
   else if (F.agg == AGG_COUNT) o.value = double(cnt);
   else o.value = ext;
   return o;

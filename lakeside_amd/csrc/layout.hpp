@@ -124,6 +124,11 @@ struct QParams {
   uint32_t total_tiles;
   uint32_t max_tiles;       // grid.x
   const uint32_t* truth;    // filter truth table: bit (T | F << nleaves) = row passes; null: interpret prog
+  // late materialization (truth tables only): filter = early AND late; string column s with bit s of late_mask
+  // is decoded only for rows where the early table passes (tiles where no late column / timestamp is NULL)
+  const uint32_t* truth_early;
+  const uint32_t* truth_late;
+  uint32_t late_mask;
   int32_t fast_div;         // 1: (ts - bucket_base) fits 32 bits for every window -> 32-bit bucket division
   double inv_step;          // 1.0 / step
   const StrParam* strp;     // [nstr]

@@ -42,6 +42,8 @@ struct Lds {
   LRun pool[(2 + NSTR) * 2 * (RUN_CAP + 1)];   // run windows: [column][value runs | def runs], + sentinel
   uint32_t lut[NSTR][LUT_CAP];
   uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
+  uint32_t truth_e[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   // late materialization: early / late
+  uint32_t truth_l[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   //   conjunct tables
   unsigned long long hkey[HCAP];
   uint32_t hrows[HCAP];
   uint32_t hcnt[HCAP];
@@ -299,6 +301,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   if (TT) {
     const uint32_t words = ((1u << (2 * P.nleaves)) + 31) / 32;
     for (uint32_t i = tid; i < words; i += BLOCK) L.truth[i] = P.truth[i];
+    if (NSTR > 1 && P.late_mask)
+      for (uint32_t i = tid; i < words; i += BLOCK) {
+        L.truth_e[i] = P.truth_early[i];
+        L.truth_l[i] = P.truth_late[i];
+      }
   }
   for (int i = tid; i < HCAP; i += BLOCK) {
     L.hkey[i] = EMPTY;
@@ -333,6 +340,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     lutm |= (uni(L.hot[c].lut_on) ? 1u : 0u) << c;
   }
   presm = uni(presm), nullm = uni(nullm), lutm = uni(lutm);
+  // Late materialization on this tile: late string columns are decoded per listed row (value index = row, so
+  // neither they nor the timestamps may hold NULLs here); otherwise every column is decoded up front.
+  const uint32_t latem = (TT && NSTR > 1) ? P.late_mask : 0u;
+  const bool late_ok = latem != 0 && (nullm & ((latem << 2) | 1u)) == 0;
+  const uint32_t skipm = late_ok ? latem : 0u;   // string columns not decoded in phase B
 
   // Per column: index (tile-relative) of the sub-tile's first value: its first row for a column without
   // NULLs, the running non-NULL count for a nullable one.
@@ -357,7 +369,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const int c = 2 + s;
       gv[s] = G8{};
       const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
-      if (!nr) continue;
+      if (!nr || ((skipm >> s) & 1u)) continue;
       const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
       gv[s] = g8_issue(vrs, L.pool + c * PSTRIDE, int(nr), uni(L.hot[c].vbase) + vnext[c] + 8 * tid,
                        int(uni(L.hot[c].bw)), true);
@@ -397,6 +409,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   uint32_t* own = reinterpret_cast<uint32_t*>(wlist) + 8 * lane;   // the thread's 8 pk slots
 
   // One chunk: up to PS*64 listed rows of a wave, loads in flight.
+  // Late columns: slot k = the k-th set bit of latem (at most NSTR - 1: the early column is never late).
+  constexpr int NLS = NSTR > 1 ? NSTR - 1 : 1;
+  uint32_t late_col[NLS];
+#pragma unroll
+  for (int k = 0; k < NLS; k++) {
+    uint32_t m = latem;
+    for (int q = 0; q < k && m; q++) m &= m - 1;
+    late_col[k] = m ? uint32_t(__builtin_ctz(m)) : 0xffu;   // string column index, 0xff: slot unused
+  }
   struct Chunk {
     v2u ts[PS], v[PS];
     uint32_t gid[PS];
@@ -521,6 +542,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
+      if ((skipm >> s) & 1u) continue;   // late column: decoded per listed row in phase E
       const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       uint32_t packed[8];
 #pragma unroll
@@ -590,7 +612,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         bool ok;
         if (TT) {
           const uint32_t ix = T | (F << nleaves);
-          ok = (L.truth[ix >> 5] >> (ix & 31)) & 1u;
+          ok = ((late_ok ? L.truth_e : L.truth)[ix >> 5] >> (ix & 31)) & 1u;
         } else {
           ok = interpret(P, T, F);
         }
@@ -619,6 +641,84 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+
+    // ============ D2. late columns of the listed rows: decode, late conjuncts, group dims; re-compact ============
+    if constexpr (NSTR > 1) {
+      if (late_ok) {
+        uint32_t n2 = 0;
+        for (uint32_t cb = 0; cb < nlist; cb += 64) {                         // uniform
+          const uint32_t i = cb + lane;
+          const bool live = i < nlist;
+          const uint2 en = live ? wlist[i] : make_uint2(0u, 0u);
+          const uint32_t row = en.y & 0x7ffu;   // = the timestamp value index (no NULL timestamps here)
+          v2u w[NLS];
+          uint32_t meta[NLS];
+#pragma unroll
+          for (int k = 0; k < NLS; k++) {                                      // issue every late load first
+            w[k] = v2u{0u, 0u};
+            meta[k] = 0;
+            const uint32_t sl = late_col[k];
+            if (sl == 0xffu) continue;                                         // uniform
+            const uint32_t c = 2 + sl;
+            const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
+            if (!nr) continue;                                                 // absent column
+            const LRun* runs = L.pool + c * PSTRIDE;
+            const uint32_t v = uni(L.hot[c].vbase) + sub + row;               // no NULLs: value index = row
+            const LRun r = runs[find_run64(runs, int(nr), v)];
+            const bool lit = (r.off_lit & 0x80000000u) != 0;
+            const uint32_t bit = (v - r.start) * uni(L.hot[c].bw);
+            const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
+            const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
+            w[k] = __builtin_amdgcn_raw_buffer_load_b64(vrs, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+            meta[k] = lit ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : r.value;
+          }
+          uint32_t gid = en.x, T = 0, F = 0;
+#pragma unroll
+          for (int k = 0; k < NLS; k++) {
+            const uint32_t sl = late_col[k];
+            if (sl == 0xffu) continue;                                         // uniform
+            const uint32_t c = 2 + sl;
+            const uint32_t dstride = uni(L.sp[sl].dim_stride), lbase = uni(L.sp[sl].lbase);
+            const uint32_t lmask = uni(L.sp[sl].lmask);
+            if (!((presm >> c) & 1u) || !uni(L.hot[c].nruns)) {               // absent: NULL in every row
+              gid += uni(L.sp[sl].dim_null) * dstride;
+              F |= uni(L.sp[sl].hmask);
+              continue;
+            }
+            const uint32_t bw = uni(L.hot[c].bw);
+            const uint64_t x = ((uint64_t)w[k].y << 32) | w[k].x;
+            const uint32_t idx = (meta[k] >> 31) ? uint32_t(x >> (meta[k] & 63u)) & (bw >= 32 ? ~0u : ((1u << bw) - 1u))
+                                                 : meta[k];
+            uint32_t packed;
+            if ((lutm >> c) & 1u) {
+              packed = L.lut[sl][idx < LUT_CAP ? idx : 0u];
+            } else {
+              const uint32_t g = uptr(L.hot[c].remap)[idx];
+              const uint32_t* tab = uptr(L.sp[sl].strtab);
+              packed = tab ? tab[g] : g;
+            }
+            const uint32_t bits = (packed >> 24) << lbase;
+            gid += (packed & DIM_MASK) * dstride;
+            T |= bits & lmask;
+            F |= ~bits & lmask;
+          }
+          const uint32_t leaf_false = uni(L.leaf_false);
+          T &= ~leaf_false;
+          F |= leaf_false;
+          const uint32_t ix = T | (F << P.nleaves);
+          const bool pass = live && ((L.truth_l[ix >> 5] >> (ix & 31)) & 1u);
+          const unsigned long long bal = __ballot(pass);
+          const uint32_t pos = n2 + __builtin_amdgcn_mbcnt_hi(uint32_t(bal >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bal), 0u));
+          __builtin_amdgcn_wave_barrier();   // every lane has read its entry before any is overwritten
+          if (pass) wlist[pos] = make_uint2(gid, en.y);
+          n2 += uint32_t(__popcll(bal));
+        }
+        nlist = n2;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
     LK_STAMP(5)
 
     // next sub-tile's packed groups: in flight while this sub-tile streams

@@ -21,17 +21,45 @@ log = logging.getLogger("lakeside_amd")
 Row = Tuple[int, float, Dict[str, str]]
 
 
+class _Handle:
+    """Owns an lk_result; freed when the last Result / array view referencing it goes away."""
+
+    def __init__(self, h):
+        self.h = h
+
+    def __del__(self):
+        try:
+            if self.h is not None:
+                _lib.lib().lk_result_free(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+class _View:
+    """numpy array interface over a result column (zero copy; keeps the owning handle alive)."""
+
+    def __init__(self, owner: _Handle, ptr, n: int, typestr: str):
+        self._owner = owner
+        self.__array_interface__ = {"shape": (n,), "typestr": typestr, "version": 3,
+                                    "data": (ctypes.cast(ptr, ctypes.c_void_p).value, True)}
+
+
 class Result:
-    """Rows of one evaluation.  Timestamps/values are copied out at once; tag strings are read from the library
-    result on first use (the result handle is owned here and freed on close / garbage collection)."""
+    """Rows of one evaluation.  Timestamps, values and glob indices are read-only numpy views of the library
+    result (no copy); tag strings are decoded from the library result on first use."""
 
     def __init__(self, handle):
         L = _lib.lib()
-        self._h = handle
+        self._owner = _Handle(handle)
         n = L.lk_result_num_rows(handle)
-        self.ts = np.ctypeslib.as_array(L.lk_result_timestamps(handle), (n,)).copy() if n else np.zeros(0, np.int64)
-        self.values = np.ctypeslib.as_array(L.lk_result_values(handle), (n,)).copy() if n else np.zeros(0)
-        self.globs = np.ctypeslib.as_array(L.lk_result_globs(handle), (n,)).copy() if n else np.zeros(0, np.uint32)
+
+        def col(ptr, typestr, dtype):
+            return np.asarray(_View(self._owner, ptr, n, typestr)) if n else np.zeros(0, dtype)
+
+        self.ts = col(L.lk_result_timestamps(handle), "<i8", np.int64)
+        self.values = col(L.lk_result_values(handle), "<f8", np.float64)
+        self.globs = col(L.lk_result_globs(handle), "<u4", np.uint32)
         ncol = L.lk_result_num_tag_columns(handle)
         self.tag_names = [L.lk_result_tag_name(handle, c).decode() for c in range(ncol)]
         self._tags = None
@@ -40,14 +68,15 @@ class Result:
     @property
     def tags(self) -> List[Dict[str, str]]:
         if self._tags is None:
-            if self._h is None:
+            if self._owner is None:
                 raise ValueError("result closed before its tags were read")
             L = _lib.lib()
+            h = self._owner.h
             out = []
             for r in range(len(self.ts)):
                 t = {}
                 for c, name in enumerate(self.tag_names):
-                    v = L.lk_result_tag_value(self._h, r, c)
+                    v = L.lk_result_tag_value(h, r, c)
                     if v is not None:
                         t[name] = v.decode()
                 out.append(t)
@@ -55,15 +84,8 @@ class Result:
         return self._tags
 
     def close(self):
-        if getattr(self, "_h", None) is not None:
-            _lib.lib().lk_result_free(self._h)
-            self._h = None
-
-    def __del__(self):
-        try:
-            self.close()
-        except Exception:
-            pass
+        """Drop this object's reference; the library result is freed once no array view remains."""
+        self._owner = None
 
     def __len__(self):
         return len(self.ts)

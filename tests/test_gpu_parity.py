@@ -124,6 +124,29 @@ def test_c3_shape_and_regex_by2_max_with_nulls(engine):
     _synth_case(engine, 4, 1 << 19, 1, 0.05, filt, "max", [synth.SERVICE, synth.NAMESPACE])
 
 
+def test_late_materialization_paths(engine):
+    """NULL-free tiles take the late path: the early column (a conjunct on one column alone, name first) is
+    decoded for every row, every other string column only for rows the early conjuncts pass."""
+    from lakeside_amd import synth
+    c3 = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"),
+          "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
+    _synth_case(engine, 3, 1 << 19, 1, 0.0, c3, "max", [synth.SERVICE, synth.NAMESPACE])          # C3 shape
+    _synth_case(engine, 3, 1 << 19, 0, 0.0, synth.leaf(synth.NAME, "eq", "metric_07"), "sum",
+                [synth.SERVICE])                                                                   # C4 shape
+    late_or = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_02"),
+               "q2": {"op": "or", "q1": synth.leaf(synth.SERVICE, "!=", "svc-003"),
+                      "q2": {"not": synth.leaf(synth.NAMESPACE, "eq", "ns-01")}}}
+    _synth_case(engine, 2, 1 << 19, 1, 0.0, late_or, "count", [synth.NAMESPACE])
+    # early column other than name: name becomes a late group dim
+    _synth_case(engine, 2, 1 << 19, 1, 0.0, synth.leaf(synth.SERVICE, "in", "svc-010", "svc-011"), "min",
+                [synth.NAME])
+    # a conjunct mixing the early column with another: no late pass
+    mixed = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_02"),
+             "q2": {"op": "or", "q1": synth.leaf(synth.NAME, "eq", "metric_01"),
+                    "q2": synth.leaf(synth.SERVICE, "eq", "svc-003")}}
+    _synth_case(engine, 2, 1 << 19, 1, 0.0, mixed, "sum", [synth.SERVICE])
+
+
 def test_groupby_count_min_with_nulls(engine):
     from lakeside_amd import synth
     filt = {"op": "or", "q1": {"not": synth.leaf(synth.SERVICE, "eq", "svc-001")},
