@@ -221,7 +221,7 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
 }
 
 template <int AGG, int NSTR, bool TT>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : 2))) void scan_tiles(QParams P) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : (NSTR <= 3 ? 3 : 2)))) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
   constexpr int PSTRIDE = 2 * (RUN_CAP + 1);
@@ -421,12 +421,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   struct Chunk {
     v2u ts[PS], v[PS];
     uint32_t gid[PS];
-    uint32_t vok;   // bit j: value j is non-NULL
-    uint32_t n;     // rows in the chunk (uniform)
+    uint32_t vok;    // bit j: value j is non-NULL
+    uint32_t live;   // bit j: slot j holds a row
+    uint32_t n;      // slots in use x 64 (uniform)
   };
   auto issue = [&](Chunk& ch, uint32_t cb, uint32_t nlist, uint32_t vb0, uint32_t vb1) {
     ch.n = min(nlist - cb, uint32_t(PS * 64));
     ch.vok = 0;
+    ch.live = 0;
 #pragma unroll
     for (int j = 0; j < PS; j++) {
       ch.ts[j] = v2u{0u, 0u};
@@ -440,16 +442,34 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const uint32_t tv = en.y & 0x7ffu, vv = (en.y >> 11) & 0x7ffu;
       const bool vok = live && ((en.y >> 22) & 1u);
       ch.vok |= uint32_t(vok) << j;
+      ch.live |= uint32_t(live) << j;
       if (!one_bucket) ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
       if (AGG != AGG_COUNT) ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
     }
+  };
+  // One row per lane (the late stage's survivors, in place: no compaction), slot 0.
+  auto issue_one = [&](Chunk& ch, bool live, uint32_t gid, uint32_t ey, uint32_t vb0, uint32_t vb1) {
+    ch.n = 64;
+#pragma unroll
+    for (int j = 0; j < PS; j++) {
+      ch.ts[j] = v2u{0u, 0u};
+      ch.v[j] = v2u{0u, 0u};
+      ch.gid[j] = 0;
+    }
+    ch.gid[0] = gid;
+    const uint32_t tv = ey & 0x7ffu, vv = (ey >> 11) & 0x7ffu;
+    const bool vok = live && ((ey >> 22) & 1u);
+    ch.vok = uint32_t(vok);
+    ch.live = uint32_t(live);
+    if (!one_bucket) ch.ts[0] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+    if (AGG != AGG_COUNT) ch.v[0] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
   };
   auto consume = [&](const Chunk& ch) {
 #pragma unroll
     for (int j = 0; j < PS; j++) {
       if (uint32_t(j * 64) >= ch.n) break;                                     // uniform
       const int64_t ts = (int64_t)(((uint64_t)ch.ts[j].y << 32) | ch.ts[j].x);
-      bool ok = (uint32_t(j * 64 + lane) < ch.n) && (one_bucket || (ts >= win_lo && ts < win_hi));   // BaseExpr.scala:159-161
+      bool ok = ((ch.live >> j) & 1u) && (one_bucket || (ts >= win_lo && ts < win_hi));   // BaseExpr.scala:159-161
       int64_t b = 0;
       if (one_bucket) {
         b = tile_b;
@@ -494,6 +514,85 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   Chunk pend;   // the previous sub-tile's first chunk: consumed after this sub-tile's decode
   pend.n = 0;
   const bool stream_on = !(P.ablate & 1);
+
+  // Late stage (late_ok tiles), one row per lane: the listed row's late columns' packed words in flight.
+  // Pipelined: the loads of a sub-tile's first 64 listed rows land during the next sub-tile's decode; the
+  // survivors' timestamp/value loads land during the one after (through `pend`).
+  struct LPend {
+    uint2 en;              // list entry
+    v2u w[NLS];            // packed words of the late columns
+    uint32_t meta[NLS];    // bit 31: bit-packed (bits 0..5: bit shift), else the RLE run's value
+    uint32_t n;            // listed rows in the chunk (uniform; 0: none)
+    uint32_t vb0, vb1;     // timestamp / value bases of the chunk's sub-tile (uniform)
+  };
+  auto late_issue = [&](LPend& lp, uint32_t cb, uint32_t nlist, uint32_t sub, uint32_t vb0, uint32_t vb1) {
+    lp.n = min(nlist - cb, 64u);
+    lp.vb0 = vb0;
+    lp.vb1 = vb1;
+    const bool live = uint32_t(lane) < lp.n;
+    lp.en = live ? wlist[cb + lane] : make_uint2(0u, 0u);
+    const uint32_t row = lp.en.y & 0x7ffu;   // = the timestamp value index (no NULL timestamps here)
+#pragma unroll
+    for (int k = 0; k < NLS; k++) {
+      lp.w[k] = v2u{0u, 0u};
+      lp.meta[k] = 0;
+      const uint32_t sl = late_col[k];
+      if (sl == 0xffu) continue;                                             // uniform
+      const uint32_t c = 2 + sl;
+      const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
+      if (!nr) continue;                                                     // absent column
+      const LRun* runs = L.pool + c * PSTRIDE;
+      const uint32_t v = uni(L.hot[c].vbase) + sub + row;                   // no NULLs: value index = row
+      const LRun r = runs[find_run64(runs, int(nr), v)];
+      const bool lit = (r.off_lit & 0x80000000u) != 0;
+      const uint32_t bit = (v - r.start) * uni(L.hot[c].bw);
+      const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
+      const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
+      lp.w[k] = __builtin_amdgcn_raw_buffer_load_b64(vrs, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      lp.meta[k] = lit ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : r.value;
+    }
+  };
+  // Late conjuncts + late group dims of the chunk's rows; returns whether the lane's row passes.
+  auto late_eval = [&](const LPend& lp, uint32_t& gid) -> bool {
+    gid = lp.en.x;
+    uint32_t T = 0, F = 0;
+#pragma unroll
+    for (int k = 0; k < NLS; k++) {
+      const uint32_t sl = late_col[k];
+      if (sl == 0xffu) continue;                                             // uniform
+      const uint32_t c = 2 + sl;
+      const uint32_t dstride = uni(L.sp[sl].dim_stride), lbase = uni(L.sp[sl].lbase);
+      const uint32_t lmask = uni(L.sp[sl].lmask);
+      if (!((presm >> c) & 1u) || !uni(L.hot[c].nruns)) {                   // absent: NULL in every row
+        gid += uni(L.sp[sl].dim_null) * dstride;
+        F |= uni(L.sp[sl].hmask);
+        continue;
+      }
+      const uint32_t bw = uni(L.hot[c].bw);
+      const uint64_t x = ((uint64_t)lp.w[k].y << 32) | lp.w[k].x;
+      const uint32_t idx = (lp.meta[k] >> 31) ? uint32_t(x >> (lp.meta[k] & 63u)) & (bw >= 32 ? ~0u : ((1u << bw) - 1u))
+                                              : lp.meta[k];
+      uint32_t packed;
+      if ((lutm >> c) & 1u) {
+        packed = L.lut[sl][idx < LUT_CAP ? idx : 0u];
+      } else {
+        const uint32_t g = uptr(L.hot[c].remap)[idx];
+        const uint32_t* tab = uptr(L.sp[sl].strtab);
+        packed = tab ? tab[g] : g;
+      }
+      const uint32_t bits = (packed >> 24) << lbase;
+      gid += (packed & DIM_MASK) * dstride;
+      T |= bits & lmask;
+      F |= ~bits & lmask;
+    }
+    const uint32_t leaf_false = uni(L.leaf_false);
+    T &= ~leaf_false;
+    F |= leaf_false;
+    const uint32_t ix = T | (F << P.nleaves);
+    return uint32_t(lane) < lp.n && ((L.truth_l[ix >> 5] >> (ix & 31)) & 1u);
+  };
+  LPend lpend;
+  lpend.n = 0;
 
   for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
     const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
@@ -643,82 +742,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 
     // ============ D2. late columns of the listed rows: decode, late conjuncts, group dims; re-compact ============
-    if constexpr (NSTR > 1) {
-      if (late_ok) {
-        uint32_t n2 = 0;
-        for (uint32_t cb = 0; cb < nlist; cb += 64) {                         // uniform
-          const uint32_t i = cb + lane;
-          const bool live = i < nlist;
-          const uint2 en = live ? wlist[i] : make_uint2(0u, 0u);
-          const uint32_t row = en.y & 0x7ffu;   // = the timestamp value index (no NULL timestamps here)
-          v2u w[NLS];
-          uint32_t meta[NLS];
-#pragma unroll
-          for (int k = 0; k < NLS; k++) {                                      // issue every late load first
-            w[k] = v2u{0u, 0u};
-            meta[k] = 0;
-            const uint32_t sl = late_col[k];
-            if (sl == 0xffu) continue;                                         // uniform
-            const uint32_t c = 2 + sl;
-            const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
-            if (!nr) continue;                                                 // absent column
-            const LRun* runs = L.pool + c * PSTRIDE;
-            const uint32_t v = uni(L.hot[c].vbase) + sub + row;               // no NULLs: value index = row
-            const LRun r = runs[find_run64(runs, int(nr), v)];
-            const bool lit = (r.off_lit & 0x80000000u) != 0;
-            const uint32_t bit = (v - r.start) * uni(L.hot[c].bw);
-            const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
-            const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
-            w[k] = __builtin_amdgcn_raw_buffer_load_b64(vrs, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
-            meta[k] = lit ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : r.value;
-          }
-          uint32_t gid = en.x, T = 0, F = 0;
-#pragma unroll
-          for (int k = 0; k < NLS; k++) {
-            const uint32_t sl = late_col[k];
-            if (sl == 0xffu) continue;                                         // uniform
-            const uint32_t c = 2 + sl;
-            const uint32_t dstride = uni(L.sp[sl].dim_stride), lbase = uni(L.sp[sl].lbase);
-            const uint32_t lmask = uni(L.sp[sl].lmask);
-            if (!((presm >> c) & 1u) || !uni(L.hot[c].nruns)) {               // absent: NULL in every row
-              gid += uni(L.sp[sl].dim_null) * dstride;
-              F |= uni(L.sp[sl].hmask);
-              continue;
-            }
-            const uint32_t bw = uni(L.hot[c].bw);
-            const uint64_t x = ((uint64_t)w[k].y << 32) | w[k].x;
-            const uint32_t idx = (meta[k] >> 31) ? uint32_t(x >> (meta[k] & 63u)) & (bw >= 32 ? ~0u : ((1u << bw) - 1u))
-                                                 : meta[k];
-            uint32_t packed;
-            if ((lutm >> c) & 1u) {
-              packed = L.lut[sl][idx < LUT_CAP ? idx : 0u];
-            } else {
-              const uint32_t g = uptr(L.hot[c].remap)[idx];
-              const uint32_t* tab = uptr(L.sp[sl].strtab);
-              packed = tab ? tab[g] : g;
-            }
-            const uint32_t bits = (packed >> 24) << lbase;
-            gid += (packed & DIM_MASK) * dstride;
-            T |= bits & lmask;
-            F |= ~bits & lmask;
-          }
-          const uint32_t leaf_false = uni(L.leaf_false);
-          T &= ~leaf_false;
-          F |= leaf_false;
-          const uint32_t ix = T | (F << P.nleaves);
-          const bool pass = live && ((L.truth_l[ix >> 5] >> (ix & 31)) & 1u);
-          const unsigned long long bal = __ballot(pass);
-          const uint32_t pos = n2 + __builtin_amdgcn_mbcnt_hi(uint32_t(bal >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(bal), 0u));
-          __builtin_amdgcn_wave_barrier();   // every lane has read its entry before any is overwritten
-          if (pass) wlist[pos] = make_uint2(gid, en.y);
-          n2 += uint32_t(__popcll(bal));
-        }
-        nlist = n2;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
     LK_STAMP(5)
 
     // next sub-tile's packed groups: in flight while this sub-tile streams
@@ -729,12 +752,43 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     LK_STAMP(6)
 
     // ============ E. stream timestamp + value of the wave's listed rows, bucket, aggregate ============
+    const uint32_t vb0 = vbase0 + vrun[0], vb1 = vbase1 + vrun[1];
+    bool late_done = false;
+    if constexpr (NSTR > 1) {
+      if (late_ok) {
+        // E'. late tiles, three stages in flight across sub-tiles:
+        //   stream rows of sub-tile k-2's survivors (loads issued one decode ago) -> aggregate;
+        //   late columns of sub-tile k-1's first 64 listed rows -> survivors' timestamp/value loads;
+        //   late-column loads of this sub-tile's first 64 listed rows.
+        // Further listed rows (dense early filters) run the late stage and stream at once.
+        late_done = true;
+        if (stream_on) consume(pend);
+        pend.n = 0;
+        if (lpend.n) {
+          uint32_t g;
+          const bool pass = late_eval(lpend, g);
+          if (stream_on) issue_one(pend, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
+          lpend.n = 0;
+        }
+        if (nlist) late_issue(lpend, 0, nlist, sub, vb0, vb1);
+        for (uint32_t cb = 64; cb < nlist; cb += 64) {                          // uniform
+          LPend lp;
+          late_issue(lp, cb, nlist, sub, vb0, vb1);
+          uint32_t g;
+          const bool pass = late_eval(lp, g);
+          if (stream_on) {
+            Chunk ch;
+            issue_one(ch, pass, g, lp.en.y, vb0, vb1);
+            consume(ch);
+          }
+        }
+      }
+    }
     // The previous sub-tile's first chunk has had this sub-tile's decode to land; this sub-tile's first chunk
     // is issued now and consumed after the next decode. Further chunks (dense filters) stream at once.
-    if (stream_on) {
+    if (stream_on && !late_done) {
       consume(pend);
       pend.n = 0;
-      const uint32_t vb0 = vbase0 + vrun[0], vb1 = vbase1 + vrun[1];
       if (nlist) issue(pend, 0, nlist, vb0, vb1);
       for (uint32_t cb = PS * 64; cb < nlist; cb += PS * 64) {
         Chunk ch;
@@ -749,7 +803,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     __builtin_amdgcn_wave_barrier();
     LK_STAMP(7)
   }
+  // drain: the last stream chunk, then the last late chunk's survivors
   consume(pend);
+  if constexpr (NSTR > 1) {
+    if (lpend.n) {
+      uint32_t g;
+      const bool pass = late_eval(lpend, g);
+      if (stream_on) {
+        issue_one(pend, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
+        consume(pend);
+      }
+    }
+  }
 #undef LK_STAMP
   if (stamp && tid == 0) {
     unsigned long long* o = P.stamps + LK_NSTAMP * (size_t(blockIdx.y) * P.max_tiles + blockIdx.x);

@@ -547,8 +547,9 @@ def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, 
       * without groupBys the merged row takes "the first input's" tags (TimeGroupedSketchAggregator.scala:
         57-60, arrival order); we take the smallest tag map."""
     agg = pr.baseExpr.chart.aggregation
-    if agg == AVG:
-        raise NotImplementedError("avg is split into sum+count before the merge (QueryEngineV2.scala:280-283)")
+    # AVG: query-api sends SUM and COUNT pushdowns (QueryEngineV2.scala:280-283); their rows merge per
+    # (timestamp, tags) into one {sum, count} map (TimeGroupedSketchAggregator.scala:74-78) and the value is
+    # sum / count (BaseExpr.scala:88-91; 0/0 = NaN).
     has_gb = bool(pr.baseExpr.chart.groupBys)
     merged: Dict[Any, list] = {}
     for cells in glob_cells:
@@ -562,6 +563,10 @@ def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, 
             val = exact_sum(np.concatenate([c.values for c in cs]))
         elif agg == COUNT:
             val = float(sum(c.count for c in cs))
+        elif agg == AVG:
+            n = sum(c.count for c in cs)
+            s = exact_sum(np.concatenate([c.values for c in cs]))
+            val = s / n if n else math.nan
         elif agg == MIN:
             val = min(c.agg_value(MIN) for c in cs)
         else:

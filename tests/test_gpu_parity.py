@@ -98,11 +98,9 @@ def _synth_case(engine, nseg, rows, value_mode, null_frac, filt, agg, group_bys,
     got = engine.eval_pushdown(req, keys, glob_size, LK_PER_GLOB_ROWS).per_glob(len(want_pg))
     for gi, (g, w) in enumerate(zip(got, want_pg)):
         assert_rows_equal(g, w, agg, f"glob {gi}")
-    if agg != "avg":
-        merged = engine.eval_pushdown(req, keys, glob_size, LK_MERGED)
-        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "merged")
-        return merged
-    return None
+    merged = engine.eval_pushdown(req, keys, glob_size, LK_MERGED)
+    assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "merged")
+    return merged
 
 
 def test_c1_shape_eq_sum(engine):
@@ -115,6 +113,15 @@ def test_c1_shape_eq_sum(engine):
 def test_real_values_sum_within_one_ulp(engine):
     from lakeside_amd import synth
     _synth_case(engine, 3, 1 << 19, 1, 0.0, synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "sum", [])
+
+
+def test_avg_merged_single_scan(engine):
+    """Merged avg = Σsum / Σcount of the SUM and COUNT pushdowns query-api would send (one scan here), with
+    NULL values (all-NULL cells: 0/0 = NaN), with and without groupBys."""
+    from lakeside_amd import synth
+    _synth_case(engine, 3, 1 << 19, 1, 0.05, synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "avg", [])
+    _synth_case(engine, 2, 1 << 18, 1, 0.3, synth.leaf(synth.NAME, "eq", "metric_04"), "avg",
+                [synth.SERVICE, synth.NAMESPACE], step=10000)
 
 
 def test_c3_shape_and_regex_by2_max_with_nulls(engine):
