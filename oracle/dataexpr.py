@@ -604,3 +604,80 @@ def evaluate_merged(pr: PushDownRequest, paths: Sequence[str], glob_size: int = 
 
 def rows_to_jsonable(rows):
     return [[int(ts), float(v).hex(), dict(sorted(tags.items()))] for ts, v, tags in rows]
+
+
+# ----------------------------------------------------------------------------------------------
+# query-api final evaluation of merged rows (§8(f) f1)
+# ----------------------------------------------------------------------------------------------
+def clause_label(q) -> str:
+    """QueryClause.toString (ASTUtils.scala:102-122)."""
+    if isinstance(q, Filter):
+        sym = {EQ: "=", GT: ">", GE: ">=", LT: "<", LE: "<="}
+        if q.op in sym:
+            return f"{q.k} {sym[q.op]} {q.v[0]}"
+        if q.op == REGEX:
+            return f"regexMatches({q.k}, {q.v[0]})"
+        if q.op == CONTAINS:
+            return f"{q.k} contains {q.v[0]}"
+        if q.op == IN:
+            return f"{q.k} in ({', '.join(q.v)})"
+        return ""
+    if isinstance(q, BinaryClause):
+        return f"({clause_label(q.q1)} {q.op} {clause_label(q.q2)})"
+    return f"not({clause_label(q.inner)})"
+
+
+def _jvm_div(a: float, b: float) -> float:
+    """Double division as on the JVM (IEEE: x/0 = +-Infinity, 0/0 = NaN)."""
+    if b != 0:
+        return a / b
+    if a != a or a == 0:
+        return math.nan
+    return math.copysign(math.inf, a) * math.copysign(1.0, b)
+
+
+def final_eval(base_expr: dict, merged_rows, step_ms: int, now_ms: int) -> List[dict]:
+    """Merged rows (S19) -> timeseries payloads:
+      * drop ts > now (TimeGroupedSketchAggregator.scala:204-207);
+      * value = transformer(map[agg]) (BaseExpr.scala:677-687; ASTUtils.getTransformerFunc 190-219, step in
+        whole seconds = stepInMillis / 1000 on Longs; MetricType "count"/"counter" -> COUNTER,
+        MetricType.scala:65-73, Commons.scala:49-52);
+      * results of one timestamp keyed by toGroupByKey (ASTUtils.scala:87-89) or "default"
+        (BaseExpr.scala:689-690), a later row overwriting an earlier one; the reference's order is a hash
+        map's, here the smallest sorted tag list wins;
+      * label: BaseExpr.label (BaseExpr.scala:697-716); payload: QueryEngineV2.toGenericSSEPayload (400-417)."""
+    be = to_base_expr(base_expr)
+    ctype = (be.chart.type if be.chart.type is not None else "count").lower().strip()
+    mtype = (base_expr.get("metricType") or "gauge").lower().strip()
+    secs = float(int(step_ms) // 1000)
+
+    def transform(v: float) -> float:
+        if be.dataset == METRICS:
+            if ctype == "count" and mtype == "rate":
+                return v * secs
+            if ctype == "rate" and mtype in ("count", "counter"):
+                return _jvm_div(v, secs)
+            return v
+        return _jvm_div(v, secs) if ctype == "rate" else v
+
+    keys = sorted(set(be.chart.groupBys))
+    by_ts: Dict[int, list] = {}
+    for ts, v, tags in merged_rows:
+        if ts > now_ms:
+            continue
+        by_ts.setdefault(int(ts), []).append((float(v), dict(tags)))
+    out = []
+    for ts in sorted(by_ts):
+        chosen = {}
+        for v, tags in sorted(by_ts[ts], key=lambda x: sorted(x[1].items()), reverse=True):
+            gk = ":".join(str(tags.get(k, "")) for k in keys) if keys else "default"
+            chosen[gk] = (v, tags)
+        for gk in sorted(chosen):
+            v, tags = chosen[gk]
+            if keys:
+                lab = "(" + ", ".join(f"{k} = {tags[k]}" for k in keys if k in tags) + ")"
+            else:
+                lab = "(" + clause_label(be.filter) + ")"
+            out.append({"id": base_expr.get("id", "_"), "type": "timeseries",
+                        "message": {"timestamp": ts, "tags": tags, "value": transform(v), "label": lab}})
+    return out

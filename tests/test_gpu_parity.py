@@ -215,3 +215,41 @@ def test_full_size_properties(engine):
         if tags["name"] == "metric_03":
             by_ts[t] = v
     assert {t: v for t, v, _ in part.rows()} == by_ts
+
+
+def test_queryapi_end_to_end(engine):
+    """query-api over the engine (lakeside_amd/queryapi.py: merged table -> drop future -> transformer ->
+    group-key collapse -> payload) vs the oracle's merge + final_eval: merged avg in one scan with a rate chart,
+    a :by whose rows collide on the group key (name differs), and :and/:re :max with a rate chart."""
+    from lakeside_amd import queryapi, synth
+    from oracle import dataexpr as dx
+    keys, blobs, segs = [], [], []
+    for i in range(3):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 19, value_mode=1, null_frac=0.05, rg_rows=1 << 18,
+                                                  page_rows=1 << 15))
+        key = f"queryapi/{i}"
+        engine.put_segment_ptr(key, s.ptr, s.size)
+        blobs.append(s.bytes())
+        s.free()
+        keys.append(key)
+        segs.append(synth.segment_request(i, step=60000))
+    names = synth.leaf(synth.NAME, "in", "metric_01", "metric_02")
+    c3 = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_03"),
+          "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
+    now = synth.T0 + 2 * synth.HOUR + 30 * 60000          # the last half hour is "in the future": dropped
+    for filt, agg, gbs, ctype in [(names, "avg", [], "rate"), (names, "sum", [synth.NAMESPACE], "count"),
+                                  (c3, "max", [synth.SERVICE], "rate")]:
+        req = synth.pushdown(filt, segs, agg, gbs)
+        be = req["baseExpr"]
+        be["chart"]["type"] = ctype
+        got = queryapi.evaluate_base_expr(engine, be, segs, keys, 60000, now_ms=now)
+        pr = dx.parse_pushdown(json.dumps(req))
+        merged = dx.merge_glob_cells(pr, dx.evaluate_glob_cells(pr, 10, keys, sources=blobs))
+        want = dx.final_eval(be, merged, 60000, now)
+        assert len(got) == len(want) > 0, (agg, len(got), len(want))
+        for g, w in zip(got, want):
+            gm, wm = g["message"], w["message"]
+            assert (gm["timestamp"], gm["tags"], gm["label"]) == (wm["timestamp"], wm["tags"], wm["label"])
+            gv, wv = gm["value"], wm["value"]
+            tol = 2 * math.ulp(wv) if agg in ("sum", "avg") else 0.0     # <= 1 ulp sum, then one division
+            assert gv == wv or (math.isnan(gv) and math.isnan(wv)) or abs(gv - wv) <= tol, (agg, gm, wm)
