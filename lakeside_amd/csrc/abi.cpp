@@ -125,16 +125,16 @@ int lk_eval_pushdown_dist(lk_engine* e, const char* push_down_json, const char* 
   return eval_common(e, push_down_json, paths, n_paths, shard, glob_size, LK_MERGED, true, out);
 }
 
-size_t lk_result_num_rows(const lk_result* r) { return r ? r->ts.size() : 0; }
-const int64_t* lk_result_timestamps(const lk_result* r) { return r ? r->ts.data() : nullptr; }
-const double* lk_result_values(const lk_result* r) { return r ? r->val.data() : nullptr; }
-const uint32_t* lk_result_globs(const lk_result* r) { return r ? r->glob.data() : nullptr; }
+size_t lk_result_num_rows(const lk_result* r) { return r ? r->nrows : 0; }
+const int64_t* lk_result_timestamps(const lk_result* r) { return r ? r->ts : nullptr; }
+const double* lk_result_values(const lk_result* r) { return r ? r->val : nullptr; }
+const uint32_t* lk_result_globs(const lk_result* r) { return r ? r->glob : nullptr; }
 size_t lk_result_num_tag_columns(const lk_result* r) { return r ? r->tag_names.size() : 0; }
 const char* lk_result_tag_name(const lk_result* r, size_t col) {
   return (r && col < r->tag_names.size()) ? r->tag_names[col].c_str() : nullptr;
 }
 const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col) {
-  if (!r || row >= r->ts.size() || col >= r->tag_names.size()) return nullptr;
+  if (!r || row >= r->nrows || col >= r->tag_names.size()) return nullptr;
   return r->tag(row, col);
 }
 const char* lk_result_stats(const lk_result* r) { return r ? r->stats.c_str() : nullptr; }

@@ -12,7 +12,9 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <new>
 #include <deque>
 #include <fstream>
 #include <map>
@@ -60,6 +62,52 @@ uint32_t GlobalDict::intern(const std::string& s) {
   vals.push_back(s);
   ids.emplace(vals.back(), id);
   return id;
+}
+
+// ------------------------------------------------------------------------------------------------
+// pinned host blocks for result columns: allocated on first need, recycled by freed results
+// ------------------------------------------------------------------------------------------------
+namespace {
+std::mutex g_pool_mu;
+std::vector<HostBlock> g_pool;            // free blocks
+constexpr size_t kPoolKeep = 8;
+}  // namespace
+
+HostBlock pinned_acquire(size_t bytes) {
+  {
+    std::lock_guard<std::mutex> g(g_pool_mu);
+    size_t best = SIZE_MAX;
+    for (size_t i = 0; i < g_pool.size(); i++)
+      if (g_pool[i].cap >= bytes && (best == SIZE_MAX || g_pool[i].cap < g_pool[best].cap)) best = i;
+    if (best != SIZE_MAX) {
+      HostBlock b = g_pool[best];
+      g_pool.erase(g_pool.begin() + long(best));
+      return b;
+    }
+  }
+  HostBlock b;
+  b.cap = std::max<size_t>(align_up(bytes, size_t(1) << 20), size_t(1) << 20);
+  if (hipHostMalloc(&b.p, b.cap, hipHostMallocDefault) == hipSuccess) {
+    b.pinned = true;
+  } else {
+    (void)hipGetLastError();
+    b.p = std::malloc(b.cap);
+    if (!b.p) throw std::bad_alloc();
+  }
+  return b;
+}
+
+void pinned_release(HostBlock b) {
+  if (!b.p) return;
+  std::lock_guard<std::mutex> g(g_pool_mu);
+  g_pool.push_back(b);
+  if (g_pool.size() > kPoolKeep) {   // drop the smallest
+    auto it = std::min_element(g_pool.begin(), g_pool.end(),
+                               [](const HostBlock& x, const HostBlock& y) { return x.cap < y.cap; });
+    if (it->pinned) (void)hipHostFree(it->p);
+    else std::free(it->p);
+    g_pool.erase(it);
+  }
 }
 
 GlobalDict& Engine::dict(const std::string& col) {

@@ -92,6 +92,15 @@ struct Workspace {
 
 struct Comm;   // comm.cpp
 
+// Process-wide pool of pinned host blocks for result columns (engine.cpp).
+struct HostBlock {
+  void* p = nullptr;
+  size_t cap = 0;
+  bool pinned = false;
+};
+HostBlock pinned_acquire(size_t bytes);
+void pinned_release(HostBlock b);
+
 struct Engine {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -129,10 +138,12 @@ struct lk_engine {
 // from the group id on demand (lk_result_tag_value), so emitting millions of rows costs no per-row host work.
 // Tag values point into the engine's dictionaries: free results before destroying their engine.
 struct lk_result {
-  std::vector<int64_t> ts;
-  std::vector<double> val;
-  std::vector<uint32_t> glob;
-  std::vector<unsigned long long> gid;           // group id: Σ dim id × stride over the group dims
+  size_t nrows = 0;
+  int64_t* ts = nullptr;                         // columns carved out of one pinned host block (pinned_acquire):
+  double* val = nullptr;                         //   device-to-host copies run at full link rate and a freed
+  uint32_t* glob = nullptr;                      //   result hands the block to the next one
+  unsigned long long* gid = nullptr;             // group id: Σ dim id × stride over the group dims
+  lk::HostBlock blk;
   std::vector<std::string> tag_names;            // "name", groupBys, then queryTags keys
   struct TagCol {                                // a "name" / groupBy tag column
     unsigned long long stride = 1, ndim = 1;
@@ -146,6 +157,20 @@ struct lk_result {
   bool per_glob = false;
   std::deque<std::string> owned;                 // strings not owned by a dictionary
   std::string stats;
+
+  lk_result() = default;
+  lk_result(const lk_result&) = delete;
+  lk_result& operator=(const lk_result&) = delete;
+  ~lk_result() { lk::pinned_release(blk); }
+  void alloc_rows(size_t n) {
+    blk = lk::pinned_acquire(n * 32 + 64);
+    nrows = n;
+    auto* b = static_cast<uint8_t*>(blk.p);
+    ts = reinterpret_cast<int64_t*>(b);
+    val = reinterpret_cast<double*>(b + n * 8);
+    gid = reinterpret_cast<unsigned long long*>(b + n * 16);
+    glob = reinterpret_cast<uint32_t*>(b + n * 24);
+  }
 
   const char* tag(size_t row, size_t col) const {
     if (col < tcols.size()) return own_tag(row, col);

@@ -232,9 +232,11 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   // no segments: the worker answers one sentinel row (Commons.scala:393-396)
   if (R.segments.empty()) {
     if (per_glob_rows) {
-      res->ts.push_back(-1);
-      res->val.push_back(-1.0);
-      res->glob.push_back(0);
+      res->alloc_rows(1);
+      res->ts[0] = -1;
+      res->val[0] = -1.0;
+      res->glob[0] = 0;
+      res->gid[0] = 0;
     }
     res->stats = "{\"scan_ms\":0,\"total_ms\":0,\"rows_scanned\":0,\"algorithmic_bytes\":0,\"tiles\":0,\"cells\":0}";
     return LK_OK;
@@ -801,15 +803,12 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (hflags & FLAG_METRICS_UNALIGNED)
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
-  res->ts.resize(nrows_out);
-  res->val.resize(nrows_out);
-  res->glob.resize(nrows_out);
-  res->gid.resize(nrows_out);
+  res->alloc_rows(nrows_out);
   if (nrows_out) {
-    HIP_TRY(hipMemcpyAsync(res->ts.data(), d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->val.data(), d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->gid.data(), d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->glob.data(), d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->ts, d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->val, d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->gid, d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
   }
   const double device_ms = ms_since(t_start) - plan_ms;
