@@ -35,6 +35,7 @@ struct ColHot {                          // one column over one tile, staged onc
   uint32_t vals_len, defs_len;
   uint32_t vbase, rip, nruns, ndruns;
   uint32_t bw, has_nulls, present, lut_on;
+  uint32_t dict_n, pad;
 };
 
 template <int NSTR>
@@ -256,6 +257,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       h.bw = tc.bw;
       h.has_nulls = tc.has_nulls;
       h.lut_on = c >= 2 && tc.dict_n <= LUT_CAP;
+      h.dict_n = tc.dict_n;
     }
     L.hot[c] = h;
     if (c >= 2) L.sp[c - 2] = uint32_t(c - 2) < P.nstr ? P.strp[c - 2] : StrParam{};   // generic: unused columns
@@ -346,6 +348,29 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   const bool late_ok = latem != 0 && (nullm & ((latem << 2) | 1u)) == 0;
   const uint32_t skipm = late_ok ? latem : 0u;   // string columns not decoded in phase B
 
+  // Fast early filter: when phase B decodes a single string column (the only one, or the early column of a
+  // late tile) that has no NULLs here and at most 64 dictionary entries, its filter outcome depends on the code
+  // alone: a 64-bit mask over the codes (this tile's chunk dictionary) replaces the lookup + fold + truth table
+  // per row, and listed rows carry the code until the compaction, where it becomes their group-dim term.
+  const int ecol = (NSTR > 1 && late_ok) ? __builtin_ctz(~latem & ((1u << NSTR) - 1u)) : 0;
+  // (NSTR <= 3: with more columns the extra live state pushes the kernel past its VGPR budget.)
+  const bool fast = TT && NSTR <= 3 && (NSTR == 1 || late_ok) && ((presm >> (2 + ecol)) & 1u) &&
+                    !((nullm >> (2 + ecol)) & 1u) && ((lutm >> (2 + ecol)) & 1u) &&
+                    uni(L.hot[2 + ecol].dict_n) <= 64u && uni(L.hot[2 + ecol].nruns) > 0u;
+  unsigned long long emask = 0;
+  if (fast) {
+    const uint32_t* tt = (NSTR > 1 && late_ok) ? L.truth_e : L.truth;
+    const uint32_t lbase = uni(L.sp[ecol].lbase), lmask = uni(L.sp[ecol].lmask), lf = uni(L.leaf_false);
+    bool pass = false;
+    if (uint32_t(lane) < uni(L.hot[2 + ecol].dict_n)) {
+      const uint32_t bits = (L.lut[ecol][lane] >> 24) << lbase;
+      const uint32_t T = bits & lmask & ~lf, F = (~bits & lmask) | lf;
+      const uint32_t ix = T | (F << P.nleaves);
+      pass = (tt[ix >> 5] >> (ix & 31)) & 1u;
+    }
+    emask = __ballot(pass);
+  }
+
   // Per column: index (tile-relative) of the sub-tile's first value: its first row for a column without
   // NULLs, the running non-NULL count for a nullable one.
   uint32_t vrun[NC];
@@ -408,7 +433,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   uint2* wlist = L.list[wave];
   uint32_t* own = reinterpret_cast<uint32_t*>(wlist) + 8 * lane;   // the thread's 8 pk slots
 
-  // One chunk: up to PS*64 listed rows of a wave, loads in flight.
+  // One chunk: up to PSN*64 listed rows of a wave, loads in flight (2 slots with 3+ string columns: VGPRs).
+  constexpr int PSN = NSTR >= 3 ? 2 : PS;
   // Late columns: slot k = the k-th set bit of latem (at most NSTR - 1: the early column is never late).
   constexpr int NLS = NSTR > 1 ? NSTR - 1 : 1;
   uint32_t late_col[NLS];
@@ -419,18 +445,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     late_col[k] = m ? uint32_t(__builtin_ctz(m)) : 0xffu;   // string column index, 0xff: slot unused
   }
   struct Chunk {
-    v2u ts[PS], v[PS];
-    uint32_t gid[PS];
+    v2u ts[PSN], v[PSN];
+    uint32_t gid[PSN];
     uint32_t vok;    // bit j: value j is non-NULL
     uint32_t live;   // bit j: slot j holds a row
     uint32_t n;      // slots in use x 64 (uniform)
   };
   auto issue = [&](Chunk& ch, uint32_t cb, uint32_t nlist, uint32_t vb0, uint32_t vb1) {
-    ch.n = min(nlist - cb, uint32_t(PS * 64));
+    ch.n = min(nlist - cb, uint32_t(PSN * 64));
     ch.vok = 0;
     ch.live = 0;
 #pragma unroll
-    for (int j = 0; j < PS; j++) {
+    for (int j = 0; j < PSN; j++) {
       ch.ts[j] = v2u{0u, 0u};
       ch.v[j] = v2u{0u, 0u};
       ch.gid[j] = 0;
@@ -451,7 +477,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   auto issue_one = [&](Chunk& ch, bool live, uint32_t gid, uint32_t ey, uint32_t vb0, uint32_t vb1) {
     ch.n = 64;
 #pragma unroll
-    for (int j = 0; j < PS; j++) {
+    for (int j = 0; j < PSN; j++) {
       ch.ts[j] = v2u{0u, 0u};
       ch.v[j] = v2u{0u, 0u};
       ch.gid[j] = 0;
@@ -466,7 +492,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   };
   auto consume = [&](const Chunk& ch) {
 #pragma unroll
-    for (int j = 0; j < PS; j++) {
+    for (int j = 0; j < PSN; j++) {
       if (uint32_t(j * 64) >= ch.n) break;                                     // uniform
       const int64_t ts = (int64_t)(((uint64_t)ch.ts[j].y << 32) | ch.ts[j].x);
       bool ok = ((ch.live >> j) & 1u) && (one_bucket || (ts >= win_lo && ts < win_hi));   // BaseExpr.scala:159-161
@@ -638,10 +664,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     uint32_t leafT[8], leafF[8], gid[8];
 #pragma unroll
     for (int e = 0; e < 8; e++) leafT[e] = 0, leafF[e] = 0, gid[e] = 0;
+    uint32_t passf = 0;   // fast early filter: pass bits straight from the codes
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
       const int c = 2 + s;
       if ((skipm >> s) & 1u) continue;   // late column: decoded per listed row in phase E
+      if (fast && s == ecol) {           // uniform: codes only (gid[] carries them to the compaction)
+        uint32_t dec[8];
+        g8_unpack(gv[s], make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8), L.pool + c * PSTRIDE,
+                  int(uni(L.hot[c].nruns)), uni(L.hot[c].vbase) + vrun[c] + r0, int(uni(L.hot[c].bw)),
+                  ctot[c] > r0 ? ctot[c] - r0 : 0u, own, [](uint32_t i) { return i; }, dec);
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          gid[e] = dec[e];
+          passf |= uint32_t((emask >> (dec[e] & 63u)) & 1ull) << e;
+        }
+        continue;
+      }
       const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       uint32_t packed[8];
 #pragma unroll
@@ -702,7 +741,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
 
     // ============ C. filter -> pass byte (NULL / absent timestamps fail the window) ============
     uint32_t passb = 0;
-    {
+    if (fast) {
+      passb = passf & vb[0];
+    } else {
       const uint32_t leaf_false = uni(L.leaf_false);
       const uint32_t nleaves = P.nleaves;
 #pragma unroll
@@ -740,8 +781,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-
-    // ============ D2. late columns of the listed rows: decode, late conjuncts, group dims; re-compact ============
+    if (fast) {   // listed rows only: the early column's code -> its group-dim term
+      const uint32_t dstride = uni(L.sp[ecol].dim_stride);
+      const uint32_t* lt = L.lut[ecol];
+      for (uint32_t cb = 0; cb < nlist; cb += 64) {                           // uniform
+        const uint32_t i = cb + lane;
+        if (i < nlist) wlist[i].x = (lt[wlist[i].x & (LUT_CAP - 1)] & DIM_MASK) * dstride;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
     LK_STAMP(5)
 
     // next sub-tile's packed groups: in flight while this sub-tile streams
@@ -790,7 +840,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       consume(pend);
       pend.n = 0;
       if (nlist) issue(pend, 0, nlist, vb0, vb1);
-      for (uint32_t cb = PS * 64; cb < nlist; cb += PS * 64) {
+      for (uint32_t cb = PSN * 64; cb < nlist; cb += PSN * 64) {
         Chunk ch;
         issue(ch, cb, nlist, vb0, vb1);
         consume(ch);
