@@ -11,7 +11,7 @@ OBJDIR  = build/obj
 LIB     = lakeside_amd/liblakeside_gpu.so
 SYNTH   = lakeside_amd/liblakeside_synth.so
 
-HOST_SRCS = $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_SRCS = $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o
 HDRS = $(wildcard $(SRC)/*.hpp) include/lakeside_gpu.h
@@ -27,7 +27,7 @@ $(OBJDIR)/kernels.o: $(SRC)/kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
 
 $(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
 	g++ -O3 -std=c++17 -fPIC -shared -pthread -Wall -o $@ tools/synth.cpp

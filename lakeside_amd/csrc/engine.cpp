@@ -29,6 +29,7 @@
 #include "engine.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
+#include "codec.hpp"
 #include "parquet.hpp"
 #include "plan.hpp"
 #include "thrift.hpp"
@@ -146,6 +147,7 @@ struct Builder {
   Segment& S;
   std::vector<uint8_t> stage;
   std::vector<std::vector<HostPage>> pages;   // per column
+  std::deque<std::vector<uint8_t>> plain;     // decompressed pages (host_vals point into them until tiling)
 
   size_t put(const uint8_t* p, size_t n) {
     size_t off = align_up(stage.size(), 16);
@@ -192,9 +194,9 @@ PageStreams split_page(const pq::PageHeader& h, const uint8_t* data, size_t n, b
 
 void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m) {
   HostCol& col = B.S.cols[ci];
-  if (m.codec != 0)
-    throw PlanError(LK_ERR_UNSUPPORTED, "parquet: compressed column chunks (codec " + std::to_string(m.codec) +
-                                            ") are not supported yet");
+  if (!pq::codec_supported(m.codec))
+    throw PlanError(LK_ERR_UNSUPPORTED, "parquet: compression codec " + std::to_string(m.codec) + " in column " +
+                                            col.name + " is not supported");
   int64_t start = m.data_page_offset;
   if (m.dictionary_page_offset > 0 && m.dictionary_page_offset < start) start = m.dictionary_page_offset;
   if (start < 4 || size_t(start) >= B.size) throw PlanError(LK_ERR_IO, "parquet: bad page offset");
@@ -212,6 +214,22 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
     size_t n = size_t(h.compressed);
     if (pos + h.header_len + n > B.size) throw PlanError(LK_ERR_IO, "parquet: page overruns the file");
     pos += h.header_len + n;
+    if (m.codec != pq::CODEC_UNCOMPRESSED &&
+        (h.type == pq::DICTIONARY_PAGE || h.type == pq::DATA_PAGE || h.type == pq::DATA_PAGE_V2)) {
+      // v1 and dictionary pages: the whole payload is compressed; v2: the levels stay plain, the values are
+      // compressed unless is_compressed = false (parquet.thrift DataPageHeaderV2)
+      const size_t lv = h.type == pq::DATA_PAGE_V2 ? size_t(h.rep_len) + size_t(h.def_len) : 0;
+      if (h.uncompressed < 0 || lv > n || lv > size_t(h.uncompressed))
+        throw PlanError(LK_ERR_IO, "parquet: bad page sizes");
+      if (h.type != pq::DATA_PAGE_V2 || h.v2_compressed) {
+        B.plain.emplace_back(size_t(h.uncompressed));
+        std::vector<uint8_t>& out = B.plain.back();
+        if (lv) memcpy(out.data(), data, lv);
+        pq::decompress(m.codec, data + lv, n - lv, out.data() + lv, out.size() - lv);
+        data = out.data();
+        n = out.size();
+      }
+    }
     if (h.type == pq::DICTIONARY_PAGE) {
       if (!col.is_string) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: dictionary-encoded non-string column " + col.name);
       GlobalDict& gd = B.E.dict(col.name);
@@ -454,7 +472,7 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     if (g.columns.size() != S->cols.size()) throw PlanError(LK_ERR_IO, "parquet: row group column count mismatch");
     S->rg_rows.push_back(g.num_rows);
   }
-  Builder B{*this, F, size, *S, {}, {}};
+  Builder B{*this, F, size, *S, {}, {}, {}};
   B.pages.resize(S->cols.size());
   B.stage.reserve(size);
   for (uint32_t rg = 0; rg < fm.row_groups.size(); rg++) {
