@@ -284,10 +284,57 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
     }
     d.nvals = nvals;
     if (col.is_string) {
-      if (st.encoding != pq::RLE_DICTIONARY && st.encoding != pq::PLAIN_DICTIONARY)
-        throw PlanError(LK_ERR_UNSUPPORTED, "parquet: non-dictionary string page in column " + col.name +
-                                                " (PLAIN fallback not supported yet)");
-      if (!have_dict) throw PlanError(LK_ERR_IO, "parquet: dictionary page missing for " + col.name);
+      uint32_t page_remap = remap_off, page_dict_n = dict_n;
+      if (st.encoding == pq::PLAIN) {
+        // PLAIN BYTE_ARRAY page (a writer's dictionary fallback, or no dictionary at all): the page gets its own
+        // dictionary — its distinct values in first-seen order, remapped to engine-global ids — and its values
+        // are re-encoded as one bit-packed literal run of indices, so the kernels see a dictionary page.
+        std::unordered_map<std::string, uint32_t> local;
+        std::vector<uint32_t> idx(nvals);
+        page_remap = uint32_t(col.remap.size());
+        {
+          GlobalDict& gd = B.E.dict(col.name);
+          std::lock_guard<std::mutex> g(gd.mu);
+          size_t p = 0;
+          for (uint32_t i = 0; i < nvals; i++) {
+            if (p + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY page in " + col.name);
+            uint32_t L;
+            memcpy(&L, st.vals + p, 4);
+            p += 4;
+            if (p + L > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY value in " + col.name);
+            auto ins = local.emplace(std::string(reinterpret_cast<const char*>(st.vals + p), L), uint32_t(local.size()));
+            if (ins.second) col.remap.push_back(gd.intern(ins.first->first));
+            idx[i] = ins.first->second;
+            p += L;
+          }
+        }
+        page_dict_n = uint32_t(local.size());
+        int pbw = 1;
+        while (pbw < 32 && (1ull << pbw) < page_dict_n) pbw++;
+        const size_t ngroups = (size_t(nvals) + 7) / 8;
+        B.plain.emplace_back();
+        std::vector<uint8_t>& enc = B.plain.back();
+        enc.push_back(uint8_t(pbw));
+        for (uint64_t hdr = (uint64_t(ngroups) << 1) | 1u;; hdr >>= 7) {   // literal-run header (ULEB128)
+          enc.push_back(uint8_t((hdr & 0x7f) | (hdr >= 0x80 ? 0x80 : 0)));
+          if (hdr < 0x80) break;
+        }
+        const size_t base = enc.size();
+        enc.resize(base + ngroups * size_t(pbw), 0);
+        for (size_t i = 0; i < size_t(nvals); i++) {
+          const uint64_t bit = uint64_t(i) * uint64_t(pbw);
+          for (int b = 0; b < pbw; b++)
+            if ((idx[i] >> b) & 1u) enc[base + ((bit + b) >> 3)] |= uint8_t(1u << ((bit + b) & 7));
+        }
+        st.vals = enc.data();
+        st.vals_len = enc.size();
+      } else if (st.encoding != pq::RLE_DICTIONARY && st.encoding != pq::PLAIN_DICTIONARY) {
+        throw PlanError(LK_ERR_UNSUPPORTED, "parquet: string page encoding " + std::to_string(st.encoding) + " in " +
+                                                col.name);
+      } else if (!have_dict) {
+        throw PlanError(LK_ERR_IO, "parquet: dictionary page missing for " + col.name);
+      }
+      const uint32_t dict_n = page_dict_n;
       if (st.vals_len < 1 && nvals) throw PlanError(LK_ERR_IO, "parquet: empty dictionary-index page");
       int bw = st.vals_len ? st.vals[0] : 0;
       if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
@@ -305,7 +352,7 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       hp.run_n = uint32_t(runs.size());
       d.kind = PAGE_DICT;
       d.bw = uint8_t(bw);
-      d.remap = remap_off;
+      d.remap = page_remap;
       d.dict_n = dict_n;
       d.vals = B.put(stream, slen);
       d.vals_len = uint32_t(slen);

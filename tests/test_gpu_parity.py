@@ -288,3 +288,46 @@ def test_compressed_segments(engine, tmp_path, codec):
         if case["expected_merged"] is not None:
             res = engine.eval_pushdown(req, paths, case["glob_size"], LK_MERGED)
             assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"{codec} {name} merged")
+
+
+def test_plain_string_pages(engine, tmp_path):
+    """PLAIN BYTE_ARRAY string pages: a writer's dictionary fallback mid-chunk (tiny
+    dictionary page limit on a high-cardinality column) and columns written without dictionaries, compressed
+    and not; each fallback page gets its own dictionary at load."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(11)
+    keys, blobs, segs = [], [], []
+    for i, (dicts, codec) in enumerate([([synth.NAME, synth.SERVICE, synth.CONTAINER], "NONE"),
+                                        ([synth.NAME], "zstd"), ([], "snappy")]):
+        n = 200_000
+        t0 = synth.T0 + i * synth.HOUR
+        t = pa.table({
+            dx.TIMESTAMP: pa.array(np.sort(rng.integers(t0, t0 + synth.HOUR, n)), pa.int64()),
+            dx.VALUE: pa.array(rng.integers(0, 1000, n).astype(np.float64), pa.float64(), mask=rng.random(n) < 0.05),
+            synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 16, n)], pa.string()),
+            synth.SERVICE: pa.array([f"svc-{k:03d}" for k in rng.integers(0, 100, n)], pa.string(),
+                                    mask=rng.random(n) < 0.05),
+            synth.CONTAINER: pa.array([f"c{k:07d}" for k in rng.integers(0, 60_000, n)], pa.string()),
+        })
+        path = str(tmp_path / f"plain{i}.parquet")
+        pq.write_table(t, path, compression=codec, use_dictionary=dicts, dictionary_pagesize_limit=16384,
+                       column_encoding={c: "PLAIN" for c in t.column_names if c not in dicts},
+                       row_group_size=100_000, data_page_size=32768)
+        engine.load_segment(path)
+        keys.append(path)
+        blobs.append(open(path, "rb").read())
+        segs.append(synth.segment_request(i))
+    for filt, agg, gbs in [(synth.leaf(synth.NAME, "eq", "metric_07"), "sum", [synth.CONTAINER]),
+                           (synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]"), "count", [synth.SERVICE]),
+                           (synth.leaf(synth.CONTAINER, "in", "c0000001", "c0000002", "c0059999"), "max", [])]:
+        req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 2, keys, sources=blobs)
+        got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS).per_glob(len(cells))
+        for gi, (g, cs) in enumerate(zip(got, cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"plain glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "plain merged")
