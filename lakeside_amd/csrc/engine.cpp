@@ -111,6 +111,40 @@ void pinned_release(HostBlock b) {
   }
 }
 
+std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size_t n) {
+  std::lock_guard<std::mutex> g(order_mu);
+  auto& slot = orders[col];
+  if (slot && slot->n == n) return slot;
+  GlobalDict& gd = dict(col);
+  std::vector<const std::string*> v(n);
+  {
+    std::lock_guard<std::mutex> dg(gd.mu);
+    for (size_t i = 0; i < n; i++) v[i] = &gd.vals[i];   // stable addresses (StableStrs)
+  }
+  auto o = std::make_shared<DictOrder>();
+  o->n = n;
+  o->perm.resize(n);
+  for (size_t i = 0; i < n; i++) o->perm[i] = uint32_t(i);
+  std::sort(o->perm.begin(), o->perm.end(), [&](uint32_t a, uint32_t b) { return *v[a] < *v[b]; });
+  o->rank.resize(n);
+  uint64_t h0 = 1469598103934665603ull, h1 = 0x84222325cbf29ce4ull;   // FNV-1a, two bases / primes
+  auto mix = [&](uint8_t b) {
+    h0 = (h0 ^ b) * 1099511628211ull;
+    h1 = (h1 ^ b) * 0x100000001b3ull * 0x9e3779b97f4a7c15ull;
+  };
+  for (size_t d = 0; d < n; d++) {
+    o->rank[o->perm[d]] = uint32_t(d);
+    const std::string& s = *v[o->perm[d]];
+    const uint32_t len = uint32_t(s.size());
+    for (int k = 0; k < 4; k++) mix(uint8_t(len >> (8 * k)));
+    for (unsigned char c : s) mix(c);
+  }
+  o->fp[0] = h0;
+  o->fp[1] = h1 ^ uint64_t(n);
+  slot = o;
+  return slot;
+}
+
 GlobalDict& Engine::dict(const std::string& col) {
   std::lock_guard<std::mutex> g(dict_mu);
   auto& p = dicts[col];

@@ -92,6 +92,16 @@ struct Workspace {
 
 struct Comm;   // comm.cpp
 
+// The sorted order of a column's engine dictionary (its first n values) and a 128-bit fingerprint of the sorted
+// values: ranks holding the same value set agree on a distributed group-dim space by comparing fingerprints
+// instead of exchanging dictionaries.
+struct DictOrder {
+  size_t n = 0;
+  std::vector<uint32_t> perm;   // dim id (sorted position) -> engine global id
+  std::vector<uint32_t> rank;   // engine global id -> dim id
+  uint64_t fp[2] = {0, 0};
+};
+
 // Process-wide pool of pinned host blocks for result columns (engine.cpp).
 struct HostBlock {
   void* p = nullptr;
@@ -116,6 +126,9 @@ struct Engine {
   void* pinned = nullptr;
   size_t pinned_cap = 0;
   Comm* comm = nullptr;
+  std::mutex order_mu;
+  std::unordered_map<std::string, std::shared_ptr<const DictOrder>> orders;   // per column, latest size
+  std::shared_ptr<const DictOrder> dict_order(const std::string& col, size_t n);
 
   explicit Engine(int dev);
   ~Engine();
@@ -149,7 +162,8 @@ struct lk_result {
     unsigned long long stride = 1, ndim = 1;
     uint32_t dim_null = 0;                       // dim id of NULL: tag absent
     std::vector<const char*> local;              // dim id -> string (nullptr: absent); empty: read `dict`
-    const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id)
+    const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id, or perm[dim id])
+    std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
   };
   std::vector<TagCol> tcols;
   // Commons.scala:450-452: a row whose own tags are all absent takes its glob head's queryTags
@@ -186,7 +200,7 @@ struct lk_result {
     const uint32_t d = uint32_t((gid[row] / t.stride) % t.ndim);
     if (d == t.dim_null) return nullptr;
     if (!t.local.empty()) return t.local[d];
-    const std::string& s = (*t.dict)[d];
+    const std::string& s = (*t.dict)[t.order ? t.order->perm[d] : d];
     return (s.empty() || s == "null") ? nullptr : s.c_str();
   }
 };

@@ -60,10 +60,13 @@ struct StrCol {
   bool exchanged = false;
   std::vector<std::string> uvals;
   std::vector<uint32_t> upos;
+  std::shared_ptr<const DictOrder> order;   // exchanged by fingerprint: dim id = sorted position (no uvals/upos)
   // the string of dim id d (d != dim_null); `gd` is this column's engine dictionary (caller holds its lock)
   const std::string& dim_value(uint32_t d, const GlobalDict& gd) const {
-    return restricted ? cand[d] : exchanged ? uvals[d] : gd.vals[d];
+    return restricted ? cand[d] : !exchanged ? gd.vals[d] : order ? gd.vals[order->perm[d]] : uvals[d];
   }
+  // engine global id -> dim id of an exchanged dim
+  uint32_t exchanged_dim(uint32_t gid) const { return order ? order->rank[gid] : upos[gid]; }
 };
 
 // Length-prefixed encoding of a dictionary's values (the exchange blob) and its inverse.
@@ -364,9 +367,26 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       sc.restricted = true;
       sc.ndim = uint32_t(sc.cand.size()) + 1;     // + absent
       sc.dim_null = uint32_t(sc.cand.size());
+    } else if (dist && [&] {
+                 // Every rank holds its own engine dictionary; the dim space is the sorted union of all ranks'
+                 // values.  When every rank holds the same value set (same count and 128-bit fingerprint of the
+                 // sorted values) the union is each rank's own sorted dictionary: no exchange, and the sort is
+                 // cached per dictionary size.
+                 sc.order = E.dict_order(sc.name, sc.dict_n);
+                 uint64_t key[3] = {uint64_t(sc.order->n), sc.order->fp[0], sc.order->fp[1]};
+                 const std::string mine(reinterpret_cast<const char*>(key), sizeof(key));
+                 for (const std::string& b : comm_allgather_bytes(E, mine))
+                   if (b != mine) return false;
+                 return true;
+               }()) {
+      if (sc.dict_n + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
+      sc.exchanged = true;
+      sc.ndim = sc.dict_n + 1;
+      sc.dim_null = sc.dict_n;
     } else if (dist) {
-      // Every rank holds its own engine dictionary: agree on one dim space, the sorted union of all ranks'
-      // values (RCCL all-gather of the dictionaries; identical on every rank, so the partial tables align).
+      // Value sets differ: all-gather the dictionaries and build the sorted union (identical on every rank, so
+      // the partial tables align).
+      sc.order.reset();
       std::string mine;
       {
         std::lock_guard<std::mutex> g(gd.mu);
@@ -434,7 +454,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
           dim = it == sc.cand.end() ? sc.dim_null : uint32_t(it - sc.cand.begin());
           if (collapse_in_table && null_like(v)) dim = sc.dim_null;
         } else {
-          dim = (collapse_in_table && null_like(v)) ? sc.dim_null : (sc.exchanged ? sc.upos[gid] : gid);
+          dim = (collapse_in_table && null_like(v)) ? sc.dim_null : (sc.exchanged ? sc.exchanged_dim(gid) : gid);
         }
       }
       tab[gid] = (bits << 24) | dim;
@@ -841,7 +861,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     tc.ndim = sc.ndim;
     tc.dim_null = sc.dim_null;
     tc.dict = &E.dict(sc.name).vals;
-    if (!sc.restricted && !sc.exchanged) continue;
+    tc.order = sc.order;   // fingerprint-agreed dim: strings read through the sorted order, none copied
+    if (!sc.restricted && (!sc.exchanged || sc.order)) continue;
     auto& m = tc.local;
     bool shared = false;
     for (size_t c2 = 0; c2 < c && !shared; c2++)   // a groupBy listed twice shares the first column's strings
