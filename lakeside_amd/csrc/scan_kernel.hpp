@@ -38,9 +38,15 @@ struct ColHot {                          // one column over one tile, staged onc
   uint32_t dict_n, pad;
 };
 
+constexpr int RS = RUN_CAP + 1;                  // staged runs per stream (+ sentinel)
+constexpr int RBLK = TILE_ROWS / 64 + 8;         // run-block table entries per string column
+
 template <int NSTR>
 struct Lds {
-  LRun pool[(2 + NSTR) * 2 * (RUN_CAP + 1)];   // run windows: [column][value runs | def runs], + sentinel
+  LRun pool[(2 + 2 * NSTR) * RS];        // run windows (+ sentinel): def runs of column c at c*RS, value runs of
+                                         //   string column s at (2 + NSTR + s)*RS
+  uint8_t rblk[NSTR][RBLK];              // per string column: run holding value index vbase + 64b (tile-relative
+                                         //   64-value blocks), so a run lookup is one table read + a short search
   uint32_t lut[NSTR][LUT_CAP];
   uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
   uint32_t truth_e[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   // late materialization: early / late
@@ -150,10 +156,25 @@ struct G8 {
   uint32_t ri;   // run index
 };
 
+// Run holding value v through the run-block table: runs blk[b] .. blk[b+1] bracket the 64-value block of v
+// (v >= vbase; values past the tile clamp to the last block — their lanes are masked by the caller).
+__device__ __forceinline__ int find_run_blk(const LRun* runs, const uint8_t* blk, uint32_t nb, uint32_t vbase,
+                                            uint32_t v) {
+  uint32_t b = (v - vbase) >> 6;
+  b = b < nb ? b : nb - 1u;
+  int lo = blk[b], hi = blk[b + 1];
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (runs[m].start <= v) lo = m;
+    else hi = m - 1;
+  }
+  return lo;
+}
+
 __device__ __forceinline__ G8 g8_issue(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
-                                       bool wide) {
+                                       bool wide, const uint8_t* blk = nullptr, uint32_t nb = 0, uint32_t vbase = 0) {
   G8 g;
-  g.ri = find_run64(runs, n, v);
+  g.ri = blk ? find_run_blk(runs, blk, nb, vbase, v) : find_run64(runs, n, v);
   const LRun r = runs[g.ri];
   const bool fast = (r.off_lit & 0x80000000u) != 0 && v + 8 <= runs[g.ri + 1].start && bw <= 8;
   const uint32_t byte = (r.off_lit & 0x7fffffffu) + (((v - r.start) * uint32_t(bw)) >> 3);
@@ -225,7 +246,8 @@ template <int AGG, int NSTR, bool TT>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : (NSTR <= 3 ? 3 : 2)))) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
-  constexpr int PSTRIDE = 2 * (RUN_CAP + 1);
+  auto druns = [&](int c) { return L.pool + c * RS; };                  // def-level runs of column c
+  auto vruns = [&](int c) { return L.pool + (NSTR + c) * RS; };         // value runs of string column c >= 2
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const unsigned long long st0 = P.stamps ? __builtin_amdgcn_s_memtime() : 0;   // diagnostics only
@@ -274,19 +296,33 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     if (!uni(L.hot[c].present)) continue;
     const TileCol* tc = Sp->cols[c].tcols + t;
     const RunDesc* runs = Sp->cols[c].runs;
-    LRun* vp = L.pool + c * PSTRIDE;
-    const uint32_t nr = uni(L.hot[c].nruns), nd = uni(L.hot[c].ndruns);
+    const uint32_t nr = c >= 2 ? uni(L.hot[c].nruns) : 0u, nd = uni(L.hot[c].ndruns);
     const uint32_t rlo = tc->run_lo, dlo = tc->drun_lo;
-    for (uint32_t i = tid; i < nr; i += BLOCK) {
-      const RunDesc r = runs[rlo + i];
-      vp[i] = LRun{r.start, r.off_lit, r.value};
-      if (i == nr - 1) vp[nr] = LRun{r.start + r.count, 0u, 0u};          // sentinel: end of the last run
+    if (c >= 2) {
+      LRun* vp = vruns(c);
+      for (uint32_t i = tid; i < nr; i += BLOCK) {
+        const RunDesc r = runs[rlo + i];
+        vp[i] = LRun{r.start, r.off_lit, r.value};
+        if (i == nr - 1) vp[nr] = LRun{r.start + r.count, 0u, 0u};        // sentinel: end of the last run
+      }
     }
+    LRun* dp = druns(c);
     for (uint32_t i = tid; i < nd; i += BLOCK) {
       const RunDesc r = runs[dlo + i];
-      vp[RUN_CAP + 1 + i] = LRun{r.start, r.off_lit, r.value};
-      if (i == nd - 1) vp[RUN_CAP + 1 + nd] = LRun{r.start + r.count, 0u, 0u};
+      dp[i] = LRun{r.start, r.off_lit, r.value};
+      if (i == nd - 1) dp[nd] = LRun{r.start + r.count, 0u, 0u};
     }
+  }
+  // run-block tables of the string columns' value runs (the runs just staged)
+  const uint32_t nblk = (tile_nrows + 63u) / 64u;
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NSTR; s++) {
+    const int c = 2 + s;
+    const uint32_t nr = ((uni(L.hot[c].present)) ? uni(L.hot[c].nruns) : 0u);
+    if (!nr) continue;
+    const uint32_t vb = uni(L.hot[c].vbase);
+    for (uint32_t b = tid; b <= nblk; b += BLOCK) L.rblk[s][b] = uint8_t(find_run64(vruns(c), int(nr), vb + 64u * b));
   }
 #pragma unroll
   for (int s = 0; s < NSTR; s++) {
@@ -386,8 +422,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       gd[c] = G8{};
       if (!((nullm >> c) & 1u)) continue;
       const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
-      gd[c] = g8_issue(drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
-                       uni(L.hot[c].rip) + s0 + 8 * tid, 1, false);
+      gd[c] = g8_issue(drs, druns(c), int(uni(L.hot[c].ndruns)), uni(L.hot[c].rip) + s0 + 8 * tid, 1, false);
     }
 #pragma unroll
     for (int s = 0; s < NSTR; s++) {
@@ -396,8 +431,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       if (!nr || ((skipm >> s) & 1u)) continue;
       const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
-      gv[s] = g8_issue(vrs, L.pool + c * PSTRIDE, int(nr), uni(L.hot[c].vbase) + vnext[c] + 8 * tid,
-                       int(uni(L.hot[c].bw)), true);
+      const uint32_t vb = uni(L.hot[c].vbase);
+      gv[s] = g8_issue(vrs, vruns(c), int(nr), vb + vnext[c] + 8 * tid, int(uni(L.hot[c].bw)), true, L.rblk[s],
+                       nblk, vb);
     }
   };
   prefetch(0, vrun);
@@ -567,9 +603,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const uint32_t c = 2 + sl;
       const uint32_t nr = ((presm >> c) & 1u) ? uni(L.hot[c].nruns) : 0u;
       if (!nr) continue;                                                     // absent column
-      const LRun* runs = L.pool + c * PSTRIDE;
-      const uint32_t v = uni(L.hot[c].vbase) + sub + row;                   // no NULLs: value index = row
-      const LRun r = runs[find_run64(runs, int(nr), v)];
+      const LRun* runs = vruns(int(c));
+      const uint32_t vb = uni(L.hot[c].vbase);
+      const uint32_t v = vb + sub + row;                                    // no NULLs: value index = row
+      const LRun r = runs[find_run_blk(runs, L.rblk[sl], nblk, vb, v)];
       const bool lit = (r.off_lit & 0x80000000u) != 0;
       const uint32_t bit = (v - r.start) * uni(L.hot[c].bw);
       const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
@@ -634,7 +671,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       ctot[c] = nsub;
       if ((nullm >> c) & 1u) {
         const __amdgpu_buffer_rsrc_t drs = make_rsrc(L.hot[c].defs, L.hot[c].defs_len + 8);
-        vb[c] = g8_bits(gd[c], drs, L.pool + c * PSTRIDE + RUN_CAP + 1, int(uni(L.hot[c].ndruns)),
+        vb[c] = g8_bits(gd[c], drs, druns(c), int(uni(L.hot[c].ndruns)),
                         uni(L.hot[c].rip) + sub + r0) & inb;
         uint32_t wt;
         vfirst[c] = wave_prefix16(__popc(vb[c]), wt);
@@ -671,7 +708,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       if ((skipm >> s) & 1u) continue;   // late column: decoded per listed row in phase E
       if (fast && s == ecol) {           // uniform: codes only (gid[] carries them to the compaction)
         uint32_t dec[8];
-        g8_unpack(gv[s], make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8), L.pool + c * PSTRIDE,
+        g8_unpack(gv[s], make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8), vruns(c),
                   int(uni(L.hot[c].nruns)), uni(L.hot[c].vbase) + vrun[c] + r0, int(uni(L.hot[c].bw)),
                   ctot[c] > r0 ? ctot[c] - r0 : 0u, own, [](uint32_t i) { return i; }, dec);
 #pragma unroll
@@ -687,7 +724,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       for (int e = 0; e < 8; e++) packed[e] = 0;
       if (nr) {
         const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
-        const LRun* runs = L.pool + c * PSTRIDE;
+        const LRun* runs = vruns(c);
         const int bw = int(uni(L.hot[c].bw));
         const uint32_t v0 = uni(L.hot[c].vbase) + vrun[c] + r0;   // this thread's group: values r0.. of the sub-tile
         const uint32_t left = ctot[c] > r0 ? ctot[c] - r0 : 0u;
