@@ -312,7 +312,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       for (size_t k = 0; k < np; k++)
         if (segs[si]->all_columns.count(probe_cols[k])) exists[gi * np + k] = 1;
       int vc = segs[si]->col_index(vcol);
-      if (vc < 0 || segs[si]->cols[vc].any_nulls || segs[si]->cols[vc].nullable) exists.back() = 1;
+      // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
+      if (vc < 0 || segs[si]->cols[vc].any_nulls) exists.back() = 1;
     }
   if (dist) comm_allreduce_max_u8(E, exists.data(), exists.size());   // every rank sees every glob's union
   const bool value_nulls = exists.back() != 0;

@@ -66,6 +66,7 @@ struct Lds {
   StrParam sp[NSTR];                     // per-query string column parameters
   int64_t win_lo, win_hi;
   uint32_t glob_slot, leaf_false;
+  uint32_t hfull;                        // the LDS table refused a key: later cells go straight to HBM
   unsigned long long stamp[LK_NSTAMP];   // diagnostics only
 };
 
@@ -75,6 +76,7 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const 
   uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (HCAP - 1);
   for (int probe = 0; probe < HPROBE; probe++) {
     unsigned long long prev = atomicCAS(&L.hkey[h], EMPTY, a.key);
+    if (probe == 0 && prev != EMPTY && prev != a.key && L.hfull) break;   // table known full: no more probes
     if (prev == EMPTY || prev == a.key) {
       atomicAdd(&L.hrows[h], a.rows);
       if (a.cnt) {
@@ -94,6 +96,7 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const 
     }
     h = (h + 1) & (HCAP - 1);
   }
+  L.hfull = 1u;                                                     // benign race: any writer stores 1
   global_merge<AGG>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
 }
 
@@ -289,6 +292,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     L.win_hi = Sp->win_hi;
     L.glob_slot = Sp->glob_slot;
     L.leaf_false = Sp->leaf_false;
+    L.hfull = 0u;
   }
   __syncthreads();
 #pragma unroll
