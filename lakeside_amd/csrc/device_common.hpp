@@ -51,11 +51,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const uint8_t* base,
   return __builtin_amdgcn_make_buffer_rsrc((void*)uni_ptr(base), (short)0, int(uni(bytes)), 0x00020000);
 }
 
-// Branch-free run lookup over at most RUN_CAP (64) staged runs: last run whose start <= v.
-__device__ __forceinline__ int find_run64(const LRun* runs, int n, uint32_t v) {
+// Branch-free run lookup over at most RUN_CAP staged runs: last run whose start <= v.
+__device__ __forceinline__ int find_run(const LRun* runs, int n, uint32_t v) {
+  static_assert((RUN_CAP & (RUN_CAP - 1)) == 0, "RUN_CAP: power of two");
   int lo = 0;
 #pragma unroll
-  for (int step = 32; step >= 1; step >>= 1) {
+  for (int step = int(RUN_CAP) / 2; step >= 1; step >>= 1) {
     const int m = lo + step;
     const uint32_t st = runs[m < n ? m : n - 1].start;
     lo = (m < n && st <= v) ? m : lo;

@@ -23,7 +23,7 @@ constexpr int MAXPROG = 48;     // postfix filter program length
 constexpr int LEAF_BITS = 8;    // leaf bits per string column in the packed lookup value
 constexpr uint32_t DIM_MASK = 0x00ffffffu;   // group-dim id bits of the packed lookup value
 constexpr uint32_t TILE_ROWS = 65536;        // max rows per tile
-constexpr uint32_t RUN_CAP = 64;             // max runs of one stream of one column inside a tile
+constexpr uint32_t RUN_CAP = 128;            // max runs of one stream of one column inside a tile
 
 enum PageKind : uint8_t { PAGE_PLAIN64 = 1, PAGE_DICT = 2 };
 

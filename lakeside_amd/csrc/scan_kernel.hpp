@@ -39,6 +39,10 @@ struct ColHot {                          // one column over one tile, staged onc
 };
 
 constexpr int RS = RUN_CAP + 1;                  // staged runs per stream (+ sentinel)
+// LDS hash entries: a single string column (name) has few cells per tile, so half a table buys the LDS the
+// 128-run windows need while keeping four workgroups per CU
+template <int NSTR>
+constexpr int hcap_v = NSTR == 1 ? HCAP / 2 : HCAP;
 constexpr int RBLK = TILE_ROWS / 64 + 8;         // run-block table entries per string column
 
 template <int NSTR>
@@ -51,11 +55,11 @@ struct Lds {
   uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
   uint32_t truth_e[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   // late materialization: early / late
   uint32_t truth_l[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   //   conjunct tables
-  unsigned long long hkey[HCAP];
-  uint32_t hrows[HCAP];
-  uint32_t hcnt[HCAP];
-  double hhi[HCAP];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
-  double hlo[HCAP];
+  unsigned long long hkey[hcap_v<NSTR>];
+  uint32_t hrows[hcap_v<NSTR>];
+  uint32_t hcnt[hcap_v<NSTR>];
+  double hhi[hcap_v<NSTR>];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
+  double hlo[hcap_v<NSTR>];
   uint2 list[WAVES][WROWS];              // per wave: passing rows {group id, ts index | value index << 11 |
                                          //   value valid << 22} (indices relative to the sub-tile's values).
                                          // Its first 2 KB per wave double as the wave's pk slots (thread t:
@@ -73,7 +77,7 @@ struct Lds {
 template <int AGG, int NSTR>
 __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const Acc& a) {
   if (a.rows == 0) return;
-  uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (HCAP - 1);
+  uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (hcap_v<NSTR> - 1);
   for (int probe = 0; probe < HPROBE; probe++) {
     unsigned long long prev = atomicCAS(&L.hkey[h], EMPTY, a.key);
     if (probe == 0 && prev != EMPTY && prev != a.key && L.hfull) break;   // table known full: no more probes
@@ -94,7 +98,7 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const 
       }
       return;
     }
-    h = (h + 1) & (HCAP - 1);
+    h = (h + 1) & (hcap_v<NSTR> - 1);
   }
   L.hfull = 1u;                                                     // benign race: any writer stores 1
   global_merge<AGG>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
@@ -177,7 +181,7 @@ __device__ __forceinline__ int find_run_blk(const LRun* runs, const uint8_t* blk
 __device__ __forceinline__ G8 g8_issue(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
                                        bool wide, const uint8_t* blk = nullptr, uint32_t nb = 0, uint32_t vbase = 0) {
   G8 g;
-  g.ri = blk ? find_run_blk(runs, blk, nb, vbase, v) : find_run64(runs, n, v);
+  g.ri = blk ? find_run_blk(runs, blk, nb, vbase, v) : find_run(runs, n, v);
   const LRun r = runs[g.ri];
   const bool fast = (r.off_lit & 0x80000000u) != 0 && v + 8 <= runs[g.ri + 1].start && bw <= 8;
   const uint32_t byte = (r.off_lit & 0x7fffffffu) + (((v - r.start) * uint32_t(bw)) >> 3);
@@ -216,7 +220,7 @@ __device__ __forceinline__ void g8_unpack(const G8& g, __amdgpu_buffer_rsrc_t rs
 #pragma unroll 1
     for (int e = 0; e < 8; e++) {
       const uint32_t ve = v + e;
-      own[e] = look(uint32_t(e) < left ? hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, bw) : 0u);
+      own[e] = look(uint32_t(e) < left ? hybrid_get_buf(rs, runs[find_run(runs, n, ve)], ve, bw) : 0u);
     }
 #pragma unroll
     for (int e = 0; e < 8; e++) out[e] = own[e];
@@ -240,7 +244,7 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
 #pragma unroll 1
   for (int e = 0; e < 8; e++) {
     const uint32_t ve = v + e;
-    bits |= (hybrid_get_buf(rs, runs[find_run64(runs, n, ve)], ve, 1) & 1u) << e;
+    bits |= (hybrid_get_buf(rs, runs[find_run(runs, n, ve)], ve, 1) & 1u) << e;
   }
   return bits;
 }
@@ -326,7 +330,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     const uint32_t nr = ((uni(L.hot[c].present)) ? uni(L.hot[c].nruns) : 0u);
     if (!nr) continue;
     const uint32_t vb = uni(L.hot[c].vbase);
-    for (uint32_t b = tid; b <= nblk; b += BLOCK) L.rblk[s][b] = uint8_t(find_run64(vruns(c), int(nr), vb + 64u * b));
+    for (uint32_t b = tid; b <= nblk; b += BLOCK) L.rblk[s][b] = uint8_t(find_run(vruns(c), int(nr), vb + 64u * b));
   }
 #pragma unroll
   for (int s = 0; s < NSTR; s++) {
@@ -349,7 +353,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         L.truth_l[i] = P.truth_late[i];
       }
   }
-  for (int i = tid; i < HCAP; i += BLOCK) {
+  for (int i = tid; i < hcap_v<NSTR>; i += BLOCK) {
     L.hkey[i] = EMPTY;
     L.hrows[i] = 0;
     L.hcnt[i] = 0;
@@ -914,7 +918,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   }
   lds_merge<AGG>(L, P, acc);
   __syncthreads();
-  for (int i = tid; i < HCAP; i += BLOCK) {
+  for (int i = tid; i < hcap_v<NSTR>; i += BLOCK) {
     if (L.hkey[i] == EMPTY) continue;
     global_merge<AGG>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
                       reinterpret_cast<unsigned long long*>(L.hhi)[i]);
