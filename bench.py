@@ -127,6 +127,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
+    launch_ms, sync_ms = [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -134,6 +135,8 @@ def main():
         total_ms.append(res.stats["total_ms"])
         plan_ms.append(res.stats["plan_ms"])
         device_ms.append(res.stats["device_ms"])
+        launch_ms.append(res.stats.get("launch_ms", 0.0))
+        sync_ms.append(res.stats.get("sync_ms", 0.0))
         alg_bytes = res.stats["algorithmic_bytes"]
         out_rows = len(res)
     torch.cuda.synchronize()
@@ -154,7 +157,8 @@ def main():
     achieved = alg_bytes / (scan_avg / 1e3) / 1e9
     log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
         f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows; in the call: plan {sum(plan_ms) / len(plan_ms):.2f} ms, "
-        f"device {sum(device_ms) / len(device_ms):.2f} ms, total {sum(total_ms) / len(total_ms):.2f} ms")
+        f"device {sum(device_ms) / len(device_ms):.2f} ms, total {sum(total_ms) / len(total_ms):.2f} ms "
+        f"(scan enqueued at {sum(launch_ms) / len(launch_ms):.2f} ms, device done at {sum(sync_ms) / len(sync_ms):.2f} ms)")
 
     traffic = None
     # PMC-measured HBM bytes per launch of the scan kernel, newest round's summary (scripts/gpu_bench_prof.sh)
@@ -182,6 +186,9 @@ def main():
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         # measured HBM rate (PMC bytes / kernel time): late materialization reads fewer bytes
+                         # than the algorithmic count, so this is the kernel's actual bandwidth use
+                         "traffic_gbs": traffic / (scan_avg / 1e3) / 1e9 if traffic else None,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

@@ -164,11 +164,14 @@ struct lk_result {
     std::vector<const char*> local;              // dim id -> string (nullptr: absent); empty: read `dict`
     const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id, or perm[dim id])
     std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
+    bool hidden = false;                         // tag name dropped by NoisyTagsDropper (tag queries)
   };
   std::vector<TagCol> tcols;
   // Commons.scala:450-452: a row whose own tags are all absent takes its glob head's queryTags
   std::vector<std::vector<std::pair<size_t, const char*>>> qt_of_glob;   // (tag column, value) per glob
   bool per_glob = false;
+  int count_col = -1;                            // tag queries: the "count" tag column
+  std::vector<std::string> count_str;            //   and its per-row value (COUNT(*) as text)
   std::deque<std::string> owned;                 // strings not owned by a dictionary
   std::string stats;
 
@@ -187,6 +190,7 @@ struct lk_result {
   }
 
   const char* tag(size_t row, size_t col) const {
+    if (int(col) == count_col) return count_str[row].c_str();
     if (col < tcols.size()) return own_tag(row, col);
     for (size_t c = 0; c < tcols.size(); c++)
       if (own_tag(row, c)) return nullptr;
@@ -197,6 +201,7 @@ struct lk_result {
   // S15 (Commons.scala:433): NULL, "null" and "" drop the tag
   const char* own_tag(size_t row, size_t c) const {
     const TagCol& t = tcols[c];
+    if (t.hidden) return nullptr;
     const uint32_t d = uint32_t((gid[row] / t.stride) % t.ndim);
     if (d == t.dim_null) return nullptr;
     if (!t.local.empty()) return t.local[d];

@@ -189,6 +189,19 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// NoisyTagsDropper.DO_NOT_DISPLAY_TAGS / DO_NOT_DISPLAY_TAG_PREFIXES (core/.../utils/NoisyTagsDropper.scala)
+bool noisy_tag(const std::string& t) {
+  static const char* const names[] = {
+      "day", "month", "hour", "minute", "year", "sketch", "_cardinalhq.tid", "_cardinalhq.would_filter",
+      "_cardinalhq.trace_has_error", "_cardinalhq.id", "_cardinalhq.telemetry_type", "_cardinalhq.filtered",
+      "_cardinalhq.is_root_span", "_cardinalhq.positive_counts", "_cardinalhq.negative_counts", "metric.stepTs",
+      "metric.tagName", "metric.metrics_type", "scope.telemetry.sdk.name", "metric.filter", "metric.dd.israte",
+      "metric.dd.rateinterval"};
+  for (const char* n : names)
+    if (t == n) return true;
+  return t.rfind("rollup_", 0) == 0;
+}
+
 }  // namespace
 
 int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
@@ -201,13 +214,21 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (n_paths != R.segments.size()) throw PlanError(LK_ERR_ARG, "paths must match segmentRequests");
 
   // ---- shape gate ----
-  if (R.is_tag_query || !R.has_chart) throw PlanError(LK_ERR_UNSUPPORTED, "tag / exemplar queries are not on the hot path");
+  // Tag query (isTagQuery with a tagDataType): BaseExpr.generateSql (BaseExpr.scala:127-143) emits
+  //   SELECT "<tag>", COUNT(*) AS count FROM {table} WHERE <filter> AND <window> GROUP BY "<tag>"
+  // i.e. the same scan with one group dim (the tag), one bucket and COUNT(*) (rows, NULL values included).
+  const bool tagq = R.is_tag_query && !R.tag_name.empty();
+  if (tagq && R.tag_data_type != "string")
+    throw PlanError(LK_ERR_UNSUPPORTED, "tag query over a " + R.tag_data_type + " tag");
+  if (!tagq && (R.is_tag_query || !R.has_chart))
+    throw PlanError(LK_ERR_UNSUPPORTED, "exemplar queries are not on the hot path");
   if (R.field_chart || R.has_extract || R.has_compute)
     throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute / field charts are not on the hot path");
   if (R.dataset != "logs" && R.dataset != "traces" && R.dataset != "metrics")
     throw PlanError(LK_ERR_ARG, "Invalid dataset: " + R.dataset);
   int agg;
-  if (R.aggregation == "sum") agg = AGG_SUM;
+  if (tagq) agg = AGG_ROWS;
+  else if (R.aggregation == "sum") agg = AGG_SUM;
   else if (R.aggregation == "min") agg = AGG_MIN;
   else if (R.aggregation == "max") agg = AGG_MAX;
   else if (R.aggregation == "count") agg = AGG_COUNT;
@@ -217,7 +238,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   // a {sum, count} map and divides (QueryEngineV2.scala:280-283, TimeGroupedSketchAggregator.scala:74-78,
   // BaseExpr.scala:88-91).  The table holds both, so one scan gives Σsum / Σcount (NaN when no value).
   if (dist && per_glob_rows) throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
-  const bool metrics = R.dataset == "metrics";
+  const bool metrics = R.dataset == "metrics" && !tagq;   // a tag query groups no timestamps
   const std::string vcol = value_column(R);
 
   std::vector<const FilterNode*> all_leaves;
@@ -254,7 +275,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     strs.back().name = name;
     return int(strs.size() - 1);
   };
-  str_index(kName);
+  str_index(tagq ? R.tag_name : kName);   // the first string column is the leading group dim
   for (auto* l : all_leaves) strs[str_index(l->k)].leaves.push_back(l);
   std::vector<std::string> gbs;
   for (auto& g : R.group_bys)
@@ -293,7 +314,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   // ---- globs ----
   const std::set<std::string> fset = field_set(R);
   std::vector<std::string> probe_cols(fset.begin(), fset.end());   // columns whose existence matters
-  for (auto& k : std::vector<std::string>{kTimestamp, kName, vcol})
+  for (auto& k : tagq ? std::vector<std::string>{kTimestamp, R.tag_name} : std::vector<std::string>{kTimestamp, kName, vcol})
     if (std::find(probe_cols.begin(), probe_cols.end(), k) == probe_cols.end()) probe_cols.push_back(k);
   for (auto* l : all_leaves)
     if (std::find(probe_cols.begin(), probe_cols.end(), l->k) == probe_cols.end()) probe_cols.push_back(l->k);
@@ -340,13 +361,21 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     for (auto& l : leaves)
       if (nonexist.count(l.node->k)) g.leaf_false |= 1u << l.index;
     // Binder Error: referenced column absent from the whole glob
-    if (!glob_has(gi, kTimestamp) || !glob_has(gi, kName) || !glob_has(gi, vcol)) g.skip = true;
+    if (tagq) {
+      if (!glob_has(gi, kTimestamp) || !glob_has(gi, R.tag_name)) g.skip = true;   // SELECT "<tag>": Binder Error
+    } else if (!glob_has(gi, kTimestamp) || !glob_has(gi, kName) || !glob_has(gi, vcol)) {
+      g.skip = true;
+    }
     for (auto& l : leaves)
       if (!nonexist.count(l.node->k) && !glob_has(gi, l.node->k)) g.skip = true;
+    if (tagq) continue;
     if (g.step <= 0) throw PlanError(LK_ERR_ARG, "stepInMillis must be positive");
     if (step < 0) step = g.step;
     else if (g.step != step) throw PlanError(LK_ERR_UNSUPPORTED, "globs with different steps");
   }
+
+  // A tag query's single bucket: ts - ts % 2^62 = 0 for every |ts| < 2^62, so bucket_base = 0 and one bucket.
+  if (tagq) step = int64_t(1) << 62;
 
   // ---- group dimensions ----
   const bool merged = !per_glob_rows;
@@ -539,7 +568,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       };
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
-      bind(1, vcol, false);
+      if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
       for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
       q.tile_begin = total_tiles;
       seg_begin.push_back(total_tiles);
@@ -645,7 +674,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   const size_t o_flags = reserve(sizeof(uint32_t) * 4);
   const size_t o_strp = reserve(strp.size() * sizeof(StrParam));
   std::vector<uint32_t> name_rank;
-  const bool collapse = merged && gbs.empty();
+  const bool collapse = merged && gbs.empty() && !tagq;
   if (collapse && strs[0].is_dim) {
     // "tags of the first input" (TimeGroupedSketchAggregator.scala:57-60) is arrival-order dependent in the
     // reference; we pick the smallest name string among the merged cells, deterministically.
@@ -702,7 +731,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   P.hi = reinterpret_cast<double*>(tb + nc * 16);
   P.lo = reinterpret_cast<double*>(tb + nc * 24);
   P.ext = reinterpret_cast<unsigned long long*>(tb + nc * 32);
-  const int kagg = agg == AGG_AVG ? AGG_SUM : agg;
+  const int kagg = agg == AGG_AVG ? AGG_SUM : (agg == AGG_ROWS ? AGG_COUNT : agg);
   HIP_TRY(hipMemsetAsync(tb, 0, nc * 16, st));
   if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + nc * 16, 0, nc * 16, st));
   if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, nc * 8, st));
@@ -713,6 +742,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     P.stamps = static_cast<unsigned long long*>(E.workspace("stamps", nstamp * 8));
     HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
   }
+  const double launch_ms = ms_since(t_start);   // host staging done, scan enqueued
   if (ncells) HIP_TRY(launch_scan(P, kagg, st));
   if (P.stamps) {
     std::vector<unsigned long long> h(nstamp);
@@ -821,6 +851,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   }
   HIP_TRY(hipMemcpyAsync(&hflags, P.flags, 4, hipMemcpyDeviceToHost, st));
   HIP_TRY(hipStreamSynchronize(st));
+  const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
   if (hflags & FLAG_METRICS_UNALIGNED)
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
@@ -838,17 +869,18 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
 
   // ---- tags: "name", groupBys (as written), then queryTags keys (rows whose own tags are all absent) ----
   std::vector<int> col_str;   // tag column -> string column index
-  res->tag_names.push_back("name");
+  res->tag_names.push_back(tagq ? R.tag_name : std::string("name"));
   col_str.push_back(0);
-  for (auto& g : R.group_bys) {
-    res->tag_names.push_back(g);
-    col_str.push_back(str_index(g));
-  }
+  if (!tagq)
+    for (auto& g : R.group_bys) {
+      res->tag_names.push_back(g);
+      col_str.push_back(str_index(g));
+    }
   const size_t nreg = res->tag_names.size();
   std::vector<std::string> qt_keys;
   for (auto& g : globs)
     for (auto& kv : g.query_tags)
-      if (std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
+      if (!tagq && std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
   for (auto& k : qt_keys) res->tag_names.push_back(k);
   // Per tag column: how a row's group id decodes to the tag string (lk_result::tag; nullptr: tag dropped,
   // Commons.scala:433).  Strings local to this call (filter candidates, the distributed union) move into the
@@ -882,6 +914,23 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       m[d] = res->owned.back().c_str();
     }
   }
+  if (tagq) {
+    // Tag-query rows (Commons.toDataPoint, Commons.scala:406-423): every column becomes a tag -- the tag and
+    // "count" (COUNT(*) via getString) -- then NoisyTagsDropper.remove (NoisyTagsDropper.scala) drops hidden
+    // tag names and NULL / "" / "null" values; timestamp = System.currentTimeMillis(), value 0.0 in the
+    // reference (unused downstream: the payload is the tag map, QueryEngineV2.scala:473-477).  Here `value`
+    // carries the count.
+    res->tcols[0].hidden = noisy_tag(R.tag_name);
+    res->tag_names.push_back("count");
+    res->count_col = int(res->tag_names.size() - 1);
+    res->count_str.reserve(nrows_out);
+    const int64_t now_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::system_clock::now().time_since_epoch()).count();
+    for (size_t r = 0; r < nrows_out; r++) {
+      res->ts[r] = now_ms;
+      res->count_str.push_back(std::to_string((unsigned long long)res->val[r]));
+    }
+  }
   res->qt_of_glob.resize(globs.size());
   for (size_t gi = 0; gi < globs.size(); gi++)
     for (auto& kv : globs[gi].query_tags) {
@@ -891,9 +940,10 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     }
   char buf[512];
   snprintf(buf, sizeof(buf),
-           "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"rows_scanned\":%llu,"
+           "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
+           "\"sync_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu}",
-           double(scan_ms), ms_since(t_start), plan_ms, device_ms, (unsigned long long)rows_scanned,
+           double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size());
   res->stats = buf;
   return LK_OK;

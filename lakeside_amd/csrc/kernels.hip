@@ -41,6 +41,7 @@ __device__ __forceinline__ double cell_value(const FParams& F, unsigned long lon
   unsigned long long cnt = F.cnt[cell];
   switch (F.agg) {
     case AGG_COUNT: return double(cnt);
+    case AGG_ROWS: return double(F.rows[cell]);
     case AGG_SUM: return cnt ? F.hi[cell] + F.lo[cell] : 0.0;     // NULL -> 0.0 (JDBC getDouble)
     case AGG_MIN:
     case AGG_MAX: return cnt ? order_dbl(F.ext[cell]) : 0.0;
@@ -65,7 +66,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   const unsigned long long g0 = F.collapse ? 0 : key % F.ngroups;
   const unsigned long long ng = F.collapse ? F.ngroups : 1;
   double hi = 0.0, lo = 0.0, ext = 0.0;
-  unsigned long long cnt = 0;
+  unsigned long long cnt = 0, nrows = 0;
   uint32_t best_rank = 0xffffffffu;
   for (uint32_t gs = 0; gs < F.nglob_slots; gs++) {
     for (unsigned long long g = g0; g < g0 + ng; g++) {
@@ -83,6 +84,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
         else ext = (F.agg == AGG_MIN) ? fmin(ext, v) : fmax(ext, v);
       }
       cnt += c;
+      nrows += F.rows[cell];
       uint32_t rank = F.name_rank ? F.name_rank[g / F.name_stride] : 0;
       if (!o.exists || rank < best_rank) {
         best_rank = rank;
@@ -95,6 +97,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   if (F.agg == AGG_SUM) o.value = hi + lo;
   else if (F.agg == AGG_AVG) o.value = (hi + lo) / double(cnt);   // merged {sum, count} map: 0/0 = NaN
   else if (F.agg == AGG_COUNT) o.value = double(cnt);
+  else if (F.agg == AGG_ROWS) o.value = double(nrows);
   else o.value = ext;
   return o;
 }

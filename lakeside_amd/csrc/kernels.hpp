@@ -28,6 +28,7 @@ struct FParams {
 };
 
 constexpr int AGG_AVG = 4;
+constexpr int AGG_ROWS = 5;        // COUNT(*): passing rows, NULL values included (tag queries)
 
 struct RParams {                   // rekey_minmax: per-glob uncollapsed table -> merged collapsed table
   const unsigned long long* in_rows;

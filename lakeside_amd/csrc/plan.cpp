@@ -95,6 +95,10 @@ Request parse_request(const std::string& text) {
   if (!f || f->is_null()) throw PlanError(LK_ERR_ARG, "No filter provided!");
   r.filter = handle_filter(*f);
   if (const Json* x = p.get("isTagQuery"); x && x->kind == Json::Bool) r.is_tag_query = x->b;
+  if (const Json* td = p.get("tagDataType"); td && td->is_obj()) {   // TagDataType(tagName, dataType)
+    if (const Json* n = td->get("tagName"); n && n->is_str()) r.tag_name = n->str;
+    if (const Json* d = td->get("dataType"); d && d->is_str()) r.tag_data_type = d->str;
+  }
   if (const Json* x = p.get("reverseSort"); x && x->kind == Json::Bool) r.reverse_sort = x->b;
   const Json* segs = p.get("segmentRequests");
   if (!segs || !segs->is_arr()) throw PlanError(LK_ERR_ARG, "missing segmentRequests");

@@ -50,6 +50,7 @@ struct Request {
   std::string rollup;            // empty = none
   bool field_chart = false, has_extract = false, has_compute = false;
   bool is_tag_query = false, reverse_sort = false;
+  std::string tag_name, tag_data_type = "string";   // PushDownRequest.tagDataType (SegmentRequest.scala:55-58)
   std::vector<SegmentReq> segments;
 };
 

@@ -602,6 +602,99 @@ def evaluate_merged(pr: PushDownRequest, paths: Sequence[str], glob_size: int = 
     return merge_glob_cells(pr, evaluate_glob_cells(pr, glob_size, paths, sources))
 
 
+# ----------------------------------------------------------------------------------------------
+# Tag queries (isTagQuery + tagDataType): BaseExpr.generateSql tag branch (BaseExpr.scala:127-143)
+# ----------------------------------------------------------------------------------------------
+# NoisyTagsDropper (core/src/main/scala/com/cardinal/utils/NoisyTagsDropper.scala): hidden tag names / prefixes
+NOISY_TAGS = {"day", "month", "hour", "minute", "year", "sketch", "_cardinalhq.tid", "_cardinalhq.would_filter",
+              "_cardinalhq.trace_has_error", "_cardinalhq.id", "_cardinalhq.telemetry_type", "_cardinalhq.filtered",
+              "_cardinalhq.is_root_span", "_cardinalhq.positive_counts", "_cardinalhq.negative_counts",
+              "metric.stepTs", "metric.tagName", "metric.metrics_type", "scope.telemetry.sdk.name", "metric.filter",
+              "metric.dd.israte", "metric.dd.rateinterval"}
+
+
+def noisy_tag(name: str) -> bool:
+    return name in NOISY_TAGS or name.startswith("rollup_")
+
+
+def tag_row_tags(tag: str, value: Optional[str], count: int) -> Dict[str, str]:
+    """Commons.toDataPoint's tag branch (Commons.scala:406-423): every column becomes a tag, then
+    NoisyTagsDropper.remove drops hidden names and NULL / "" / "null" values."""
+    tags = {"count": str(count)}
+    if value is not None and value != "" and value != "null" and not noisy_tag(tag):
+        tags[tag] = value
+    return tags
+
+
+def parse_tag_data_type(text: str) -> Optional[str]:
+    """PushDownRequest.fromJson's tagDataType (SegmentRequest.scala:55-58) -> tagName (None: no tag query)."""
+    p = json.loads(text)
+    td = p.get("tagDataType")
+    return td.get("tagName") if p.get("isTagQuery") and isinstance(td, dict) else None
+
+
+def evaluate_tag_glob(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], paths: Sequence[str], sources=None):
+    """One glob of a tag query:  SELECT "<tag>", COUNT(*) AS count FROM {table} WHERE <filter> AND <window>
+    GROUP BY "<tag>"  (BaseExpr.scala:127-143; the filter/nonExistentFields compile as for charts, 170-180).
+    Returns [(raw tag value or None, COUNT(*))] sorted by value (None first); the SQL has no ORDER BY."""
+    be = pr.baseExpr
+    if any(f.extracted or f.computed for f in _leaves(be.filter)):
+        raise NotImplementedError("synthetic (extracted/computed) tag queries are outside the hot path")
+    segs = [pr.segmentRequests[i] for i in seg_idx]
+    fs = filter_field_set(be.filter) | set(be.chart.groupBys if be.chart else [])
+    strings = sorted(set(_leaf_columns(be.filter)) | {tag})
+    union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources)
+    nonexistent = fs - set(union)
+    referenced = (set(_leaf_columns(be.filter)) - nonexistent) | {TIMESTAMP, tag}
+    if not referenced <= set(union):                                  # Binder Error -> empty glob
+        return []
+    start = min(s.startTs for s in segs)
+    end = max(s.endTs for s in segs)
+    ts, ts_valid = nums[TIMESTAMP]
+    ts = ts.astype(np.int64)
+    n = len(ts)
+    t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    keep = ts_valid & (ts >= start) & (ts < end) & t
+    col = strs[tag]
+    codes = col.codes[keep]
+    if len(codes) == 0:
+        return []
+    u, cnt = np.unique(codes, return_counts=True)
+    out = [(col.dictionary[c] if c >= 0 else None, int(k)) for c, k in zip(u, cnt)]
+    out.sort(key=lambda r: (r[0] is not None, r[0] or ""))
+    return out
+
+
+def _leaves(q):
+    if isinstance(q, Filter):
+        return [q]
+    if isinstance(q, NotClause):
+        return _leaves(q.inner)
+    return _leaves(q.q1) + _leaves(q.q2)
+
+
+def evaluate_tag_per_glob(pr: PushDownRequest, tag: str, paths: Sequence[str], glob_size: int = 10, sources=None):
+    """Worker rows of a tag query per glob: [[tags map]] (values: the DataPoint tags; timestamp =
+    System.currentTimeMillis() and value 0.0 in the reference, not compared)."""
+    out = []
+    for g in globs_of(pr, glob_size):
+        rows = evaluate_tag_glob(pr, tag, g, [paths[i] for i in g], None if sources is None else [sources[i] for i in g])
+        out.append([tag_row_tags(tag, v, c) for v, c in rows])
+    return out
+
+
+def evaluate_tag_merged(pr: PushDownRequest, tag: str, paths: Sequence[str], glob_size: int = 10, sources=None):
+    """Counts summed per tag value over the globs (the engine's LK_MERGED for tag queries; query-api streams the
+    per-glob rows unmerged, its TagQueryUtils.aggregate is commented out, QueryEngineV2.scala:487).  NULL, "" and
+    "null" give the same tag map and merge into one row."""
+    acc: Dict[Optional[str], int] = {}
+    for g in globs_of(pr, glob_size):
+        for v, c in evaluate_tag_glob(pr, tag, g, [paths[i] for i in g], None if sources is None else [sources[i] for i in g]):
+            k = None if (v is None or v == "" or v == "null") else v
+            acc[k] = acc.get(k, 0) + c
+    return [tag_row_tags(tag, v, c) for v, c in sorted(acc.items(), key=lambda r: (r[0] is not None, r[0] or ""))]
+
+
 def rows_to_jsonable(rows):
     return [[int(ts), float(v).hex(), dict(sorted(tags.items()))] for ts, v, tags in rows]
 

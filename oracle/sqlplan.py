@@ -91,13 +91,9 @@ def generate_sql(pr: PushDownRequest, start: int, end: int, step: int, nonexiste
             f" GROUP BY {STEP_TS} {gb}, name ORDER BY {STEP_TS} ASC")
 
 
-def run_sql(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str]):
-    """Run the reference's generated SQL for one glob on SQLite; returns rows materialized as
-    Commons.toDataPoint does (Commons.scala:399-462): [(ts, value, tags)]."""
-    import pyarrow as pa
+def _load_glob(paths: Sequence[str]):
+    """The glob's rows (union_by_name) in an in-memory SQLite table `t`, with regexp_matches bound to RE2."""
     import pyarrow.parquet as pq
-
-    segs = [pr.segmentRequests[i] for i in seg_idx]
     tables, union = [], []
     for p in paths:
         t = pq.read_table(p)
@@ -105,19 +101,6 @@ def run_sql(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str]):
             if c not in union:
                 union.append(c)
         tables.append(t)
-    nonexistent = field_set(pr.baseExpr) - set(union)
-    start = min(s.startTs for s in segs)
-    end = max(s.endTs for s in segs)
-    step = segs[0].stepInMillis
-    sql = generate_sql(pr, start, end, step, nonexistent).replace("{tableName}", "t")
-    # SQLite reads an unknown double-quoted identifier as a string literal; DuckDB raises a Binder Error
-    # that the worker turns into an empty glob (Commons.scala:249-253).  Mirror DuckDB.
-    import re
-    idents = set(re.findall(r'"([^"]+)"', sql)) | {"rollup_" + (pr.baseExpr.chart.rollup or SUM)
-                                                   if pr.baseExpr.dataset == METRICS else VALUE}
-    if not idents <= set(union):
-        return []
-
     con = sqlite3.connect(":memory:")
     cache: Dict[tuple, Optional[bool]] = {}
 
@@ -137,6 +120,59 @@ def run_sql(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str]):
         data = {c: (t.column(c).to_pylist() if c in t.column_names else [None] * t.num_rows) for c in union}
         rows = list(zip(*[data[c] for c in union])) if union else []
         con.executemany(f"INSERT INTO t VALUES ({', '.join('?' * len(union))})", rows)
+    return con, union
+
+
+def generate_tag_sql(pr: PushDownRequest, tag: str, start: int, end: int, nonexistent: set) -> str:
+    """BaseExpr.generateSql tag branch for a non-synthetic tag (BaseExpr.scala:127-143)."""
+    fsql = filter_sql(pr.baseExpr.filter, nonexistent)
+    return (f'SELECT "{tag}" as "{tag}", COUNT(*) AS count FROM {{tableName}} WHERE {fsql} AND '
+            f'{timestamp_filter(start, end)} GROUP BY "{tag}"')
+
+
+def run_tag_sql(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], paths: Sequence[str]):
+    """Run the reference's tag-query SQL for one glob on SQLite -> [(raw tag value or None, count)] sorted as
+    oracle.dataexpr.evaluate_tag_glob sorts."""
+    segs = [pr.segmentRequests[i] for i in seg_idx]
+    con, union = _load_glob(paths)
+    be = pr.baseExpr
+    fs = field_set(be) if be.chart is not None else _filter_fields(be.filter)
+    nonexistent = fs - set(union)
+    sql = generate_tag_sql(pr, tag, min(s.startTs for s in segs), max(s.endTs for s in segs),
+                           nonexistent).replace("{tableName}", "t")
+    import re
+    if not set(re.findall(r'"([^"]+)"', sql)) <= set(union):   # DuckDB Binder Error -> empty glob
+        con.close()
+        return []
+    out = [(v, int(c)) for v, c in con.execute(sql).fetchall()]
+    con.close()
+    out.sort(key=lambda r: (r[0] is not None, r[0] or ""))
+    return out
+
+
+def _filter_fields(q) -> set:
+    from oracle.dataexpr import filter_field_set
+    return filter_field_set(q)
+
+
+def run_sql(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str]):
+    """Run the reference's generated SQL for one glob on SQLite; returns rows materialized as
+    Commons.toDataPoint does (Commons.scala:399-462): [(ts, value, tags)]."""
+    segs = [pr.segmentRequests[i] for i in seg_idx]
+    con, union = _load_glob(paths)
+    nonexistent = field_set(pr.baseExpr) - set(union)
+    start = min(s.startTs for s in segs)
+    end = max(s.endTs for s in segs)
+    step = segs[0].stepInMillis
+    sql = generate_sql(pr, start, end, step, nonexistent).replace("{tableName}", "t")
+    # SQLite reads an unknown double-quoted identifier as a string literal; DuckDB raises a Binder Error
+    # that the worker turns into an empty glob (Commons.scala:249-253).  Mirror DuckDB.
+    import re
+    idents = set(re.findall(r'"([^"]+)"', sql)) | {"rollup_" + (pr.baseExpr.chart.rollup or SUM)
+                                                   if pr.baseExpr.dataset == METRICS else VALUE}
+    if not idents <= set(union):
+        con.close()
+        return []
     cur = con.execute(sql)
     names = [d[0] for d in cur.description]
     out = []

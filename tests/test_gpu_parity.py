@@ -60,6 +60,36 @@ def test_golden_merged(golden_engine, case):
     assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, case["name"])
 
 
+def _tag_cases():
+    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
+        return json.load(f)
+
+
+def _tag_key(t):
+    return sorted(t.items())
+
+
+@pytest.mark.parametrize("case", _tag_cases(), ids=lambda c: c["name"])
+def test_golden_tag_query(golden_engine, case):
+    """Tag queries (isTagQuery + tagDataType; BaseExpr.scala:127-143): per-glob rows {tag, count} and merged
+    counts equal the golden rows (oracle pinned by the reference's tag SQL on SQLite)."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    for p in paths:
+        if not _cached(golden_engine, p):
+            golden_engine.load_segment(p)
+    req = json.dumps(case["request"])
+    tag = case["request"]["tagDataType"]["tagName"]
+    res = golden_engine.eval_pushdown(req, paths, case["glob_size"], LK_PER_GLOB_ROWS)
+    assert res.tag_names == [tag, "count"]
+    assert all(int(v) == int(t["count"]) for v, t in zip(res.values, res.tags))
+    got = res.per_glob(len(case["expected_per_glob"]))
+    for gi, (g, w) in enumerate(zip(got, case["expected_per_glob"])):
+        assert sorted((r[2] for r in g), key=_tag_key) == sorted(w, key=_tag_key), f"{case['name']} glob {gi}"
+    res = golden_engine.eval_pushdown(req, paths, case["glob_size"], LK_MERGED)
+    assert sorted(res.tags, key=_tag_key) == sorted(case["expected_merged"], key=_tag_key)
+
+
 def test_no_segments_sentinel(engine):
     from lakeside_amd.evaluator import evaluate_push_down_request
     req = {"baseExpr": {"id": "A", "dataset": "logs", "filter": {"k": "_cardinalhq.name", "v": ["x"], "op": "eq"},

@@ -33,11 +33,7 @@ def test_sql_plan_matches_reference_test_strings(case):
     pr = dx.PushDownRequest(baseExpr=be, segmentRequests=[])
     exp = case["expected"]
     if case["kind"] == "tag_filter_sql":
-        fsql = sqlplan.filter_sql(be.filter, set())
-        ts = sqlplan.timestamp_filter(case["start"], case["end"])
-        tag = "resource.container.name"
-        got = (f'SELECT "{tag}" as "{tag}", COUNT(*) AS count FROM {{tableName}} WHERE {fsql} AND {ts} '
-               f'GROUP BY "{tag}"')
+        got = sqlplan.generate_tag_sql(pr, "resource.container.name", case["start"], case["end"], set())
         assert got == exp
     else:
         lo = exp.index("FROM (") + len("FROM (")
@@ -97,3 +93,32 @@ def test_binary_clause_folds_left_in_json_order():
     assert isinstance(f, dx.BinaryClause) and f.op == "or"
     assert isinstance(f.q1, dx.BinaryClause) and f.q2.k == "c"
     assert sqlplan.filter_sql(f, {"b"}) == "((a = '1' or false) or c = '3')"
+
+
+def _tag_cases():
+    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", _tag_cases(), ids=lambda c: c["name"])
+def test_tag_query_oracle_matches_golden(case):
+    """Tag queries (BaseExpr.scala:127-143): the oracle reproduces the committed rows, and for every glob agrees
+    with the reference's tag SQL run on SQLite."""
+    text = json.dumps(case["request"])
+    pr = dx.parse_pushdown(text)
+    tag = dx.parse_tag_data_type(text)
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    assert dx.evaluate_tag_per_glob(pr, tag, paths, case["glob_size"]) == case["expected_per_glob"]
+    assert dx.evaluate_tag_merged(pr, tag, paths, case["glob_size"]) == case["expected_merged"]
+    g = dx.globs_of(pr, case["glob_size"])[-1]
+    assert dx.evaluate_tag_glob(pr, tag, g, [paths[i] for i in g]) == sqlplan.run_tag_sql(pr, tag, g, [paths[i] for i in g])
+
+
+def test_tag_row_noisy_tags_dropped():
+    """NoisyTagsDropper.remove: hidden names / rollup_ prefix / NULL, "" and "null" values drop the tag; the count
+    column stays (Commons.scala:406-423)."""
+    assert dx.tag_row_tags("resource.service.name", "svc-001", 7) == {"resource.service.name": "svc-001", "count": "7"}
+    for name in ("_cardinalhq.id", "hour", "rollup_sum", "metric.filter"):
+        assert dx.tag_row_tags(name, "x", 3) == {"count": "3"}
+    for v in (None, "", "null"):
+        assert dx.tag_row_tags("a", v, 1) == {"count": "1"}
