@@ -127,7 +127,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
-    launch_ms, sync_ms = [], []
+    launch_ms, sync_ms, alloc_ms, copy_ms = [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -137,6 +137,8 @@ def main():
         device_ms.append(res.stats["device_ms"])
         launch_ms.append(res.stats.get("launch_ms", 0.0))
         sync_ms.append(res.stats.get("sync_ms", 0.0))
+        alloc_ms.append(res.stats.get("alloc_ms", 0.0))
+        copy_ms.append(res.stats.get("copy_ms", 0.0))
         alg_bytes = res.stats["algorithmic_bytes"]
         out_rows = len(res)
     torch.cuda.synchronize()
@@ -158,7 +160,8 @@ def main():
     log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
         f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows; in the call: plan {sum(plan_ms) / len(plan_ms):.2f} ms, "
         f"device {sum(device_ms) / len(device_ms):.2f} ms, total {sum(total_ms) / len(total_ms):.2f} ms "
-        f"(scan enqueued at {sum(launch_ms) / len(launch_ms):.2f} ms, device done at {sum(sync_ms) / len(sync_ms):.2f} ms)")
+        f"(scan enqueued at {sum(launch_ms) / len(launch_ms):.2f} ms, device done at {sum(sync_ms) / len(sync_ms):.2f} ms, "
+        f"rows allocated at {sum(alloc_ms) / len(alloc_ms):.2f} ms, copied at {sum(copy_ms) / len(copy_ms):.2f} ms)")
 
     traffic = None
     # PMC-measured HBM bytes per launch of the scan kernel, newest round's summary (scripts/gpu_bench_prof.sh)

@@ -846,7 +846,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   uint32_t nrows_out = 0;
   uint32_t hflags = 0;
   if (emit && F.nkeys) {
-    HIP_TRY(launch_finalize(F, d_counts, d_ts, d_val, d_gid, d_glob, st));
+    HIP_TRY(launch_finalize_count(F, d_counts, st));
     HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
   }
   HIP_TRY(hipMemcpyAsync(&hflags, P.flags, 4, hipMemcpyDeviceToHost, st));
@@ -856,14 +856,23 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
   res->alloc_rows(nrows_out);
+  const double alloc_ms = ms_since(t_start);
   if (nrows_out) {
-    HIP_TRY(hipMemcpyAsync(res->ts, d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->val, d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->gid, d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    if (res->blk.pinned) {
+      // Rows written by the kernel straight into the mapped pinned result block: no device->host copies (small
+      // async D2H copies cost ~1 ms of completion latency each call on this stack, measured in bench C4).
+      HIP_TRY(launch_finalize_write(F, d_counts, res->ts, res->val, res->gid, res->glob, st));
+    } else {
+      HIP_TRY(launch_finalize_write(F, d_counts, d_ts, d_val, d_gid, d_glob, st));
+      HIP_TRY(hipMemcpyAsync(res->ts, d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->val, d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->gid, d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    }
     HIP_TRY(hipStreamSynchronize(st));
   }
-  const double device_ms = ms_since(t_start) - plan_ms;
+  const double copy_ms = ms_since(t_start);
+  const double device_ms = copy_ms - plan_ms;
   float scan_ms = 0;
   HIP_TRY(hipEventElapsedTime(&scan_ms, E.ev_scan0, E.ev_scan1));
 
@@ -941,9 +950,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   char buf[512];
   snprintf(buf, sizeof(buf),
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
-           "\"sync_ms\":%.6f,\"rows_scanned\":%llu,"
+           "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu}",
-           double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, (unsigned long long)rows_scanned,
+           double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size());
   res->stats = buf;
   return LK_OK;

@@ -289,14 +289,27 @@ uint32_t finalize_blocks(unsigned long long nkeys) {
   return uint32_t((nkeys + FB * FITEMS - 1) / (FB * FITEMS));
 }
 
-hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
-                           uint32_t* glob, hipStream_t stream) {
+hipError_t launch_finalize_count(const FParams& F, uint32_t* d_counts, hipStream_t stream) {
   uint32_t nb = finalize_blocks(F.nkeys);
   if (nb == 0) return hipMemsetAsync(d_counts, 0, sizeof(uint32_t), stream);
   hipLaunchKernelGGL(finalize_count, dim3(nb), dim3(FB), 0, stream, F, d_counts);
   hipLaunchKernelGGL(finalize_scan, dim3(1), dim3(1024), 0, stream, d_counts, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int64_t* ts, double* val,
+                                 unsigned long long* gid, uint32_t* glob, hipStream_t stream) {
+  uint32_t nb = finalize_blocks(F.nkeys);
+  if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_write, dim3(nb), dim3(FB), 0, stream, F, d_counts, ts, val, gid, glob);
   return hipGetLastError();
+}
+
+hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
+                           uint32_t* glob, hipStream_t stream) {
+  hipError_t e = launch_finalize_count(F, d_counts, stream);
+  if (e != hipSuccess) return e;
+  return launch_finalize_write(F, d_counts, ts, val, gid, glob, stream);
 }
 
 }  // namespace lk

@@ -62,6 +62,11 @@ hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* part
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
 uint32_t finalize_blocks(unsigned long long nkeys);
 // d_counts must hold finalize_blocks(nkeys) + 1 entries; the row total lands in d_counts[nblocks].
+// Split form: count + scan (row total at d_counts[nblocks]), then write -- the write may target mapped pinned host
+// memory (hipHostMalloc) directly, so no device->host copy follows.
+hipError_t launch_finalize_count(const FParams& F, uint32_t* d_counts, hipStream_t stream);
+hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int64_t* ts, double* val,
+                                 unsigned long long* gid, uint32_t* glob, hipStream_t stream);
 hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
                            uint32_t* glob, hipStream_t stream);
 
