@@ -44,6 +44,12 @@ QUERIES = {
                        "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.container.id"],
                step=3600000, hour=0, highcard_n=10_000_000, segments=8,
                desc=":eq _cardinalhq.name=metric_07 :sum :by resource.container.id (10M-value dictionary), step 1h"),
+    # tag query (§8(f) f4) on C2 data: values of resource.service.name among metric_07's rows, with COUNT(*)
+    # (query-api's `IS NOT NULL` on the tag included); reads the name + service columns only
+    "tag": dict(filter={"op": "and", "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
+                        "q2": {"k": "resource.service.name", "v": [], "op": "exists"}},
+                agg="count", group_bys=[], tag="resource.service.name",
+                desc="tag query resource.service.name where :eq _cardinalhq.name=metric_07, COUNT(*)"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
@@ -114,7 +120,7 @@ def main():
         f"{eng.segment_bytes / 1e9:.1f} GB, load {time.time() - t0:.0f}s")
 
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(total)]
-    req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"]))
+    req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag")))
 
     def step():
         if world > 1:
@@ -217,9 +223,12 @@ def cpu_baseline(args, q, synth):
         s.free()
     keys = [f"cpu/{i}" for i in range(n)]
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
-    pr = dx.parse_pushdown(json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"])))
+    pr = dx.parse_pushdown(json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag"))))
     t = time.perf_counter()
-    dx.evaluate_merged(pr, keys, 10, sources=blobs)
+    if q.get("tag"):
+        dx.evaluate_tag_merged(pr, q["tag"], keys, 10, sources=blobs)
+    else:
+        dx.evaluate_merged(pr, keys, 10, sources=blobs)
     dt = time.perf_counter() - t
     log(f"cpu baseline: {n} segments in {dt:.1f}s")
     return {"value": n * args.rows / dt, "unit": "rows/s", "cores": 1, "kind": "port",

@@ -599,13 +599,24 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       for (auto* l : ls) m |= 1u << str_index(l->k);
       return m;
     };
+    // A conjunct of only `exists`/`has` leaves (IS NOT NULL: passes nearly every row, e.g. the one query-api adds
+    // to a tag query) is a poor early filter: it is chosen only when no other single-column conjunct exists.
+    auto weak = [&](const FilterNode* n) {
+      std::vector<const FilterNode*> ls;
+      collect_leaves(n, ls);
+      return std::all_of(ls.begin(), ls.end(), [](const FilterNode* l) { return l->op == "exists" || l->op == "has"; });
+    };
     int early = -1;
+    bool early_weak = true;
     for (auto* c : conj) {
       const uint32_t m = cols_of(c);
       if (__builtin_popcount(m) != 1) continue;
       const int col = __builtin_ctz(m);
-      if (early < 0 || col == 0) early = col;
-      if (col == 0) break;
+      const bool w = weak(c);
+      if (early < 0 || (early_weak && !w) || (w == early_weak && col == 0)) {
+        early = col;
+        early_weak = w;
+      }
     }
     // The late pass sees only the late columns' leaves: a conjunct mixing the early column with others keeps
     // every column early (no late pass).

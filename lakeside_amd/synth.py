@@ -76,11 +76,18 @@ def segment_request(index: int, step: int = 60000, hour: int = None, query_tags=
             "collectorId": "k", "bucketName": "b", "cName": "", "startTs": start, "endTs": start + HOUR}
 
 
-def pushdown(filter_, segs, agg="sum", group_bys=(), dataset="logs") -> dict:
-    return {"baseExpr": {"id": "A", "dataset": dataset, "filter": filter_,
-                         "chart": {"aggregation": agg, "groupBys": list(group_bys), "type": "count"},
-                         "limit": 1000, "order": "DESC", "metricType": "gauge", "returnResults": True},
-            "segmentRequests": list(segs), "reverseSort": False, "isTagQuery": False}
+def pushdown(filter_, segs, agg="sum", group_bys=(), dataset="logs", tag=None) -> dict:
+    """A PushDownRequest; with `tag`, a tag query (no chart, isTagQuery + tagDataType, as
+    QueryEngineV2.evaluateTagQuery sends it)."""
+    be = {"id": "A", "dataset": dataset, "filter": filter_,
+          "chart": {"aggregation": agg, "groupBys": list(group_bys), "type": "count"},
+          "limit": 1000, "order": "DESC", "metricType": "gauge", "returnResults": True}
+    req = {"baseExpr": be, "segmentRequests": list(segs), "reverseSort": False, "isTagQuery": False}
+    if tag is not None:
+        del be["chart"]
+        req["isTagQuery"] = True
+        req["tagDataType"] = {"tagName": tag, "dataType": "string"}
+    return req
 
 
 def leaf(k, op, *v):

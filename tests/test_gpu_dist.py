@@ -24,6 +24,11 @@ def _cases():
         return [c for c in json.load(f) if c["expected_merged"] is not None]
 
 
+def _tag_cases():
+    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
+        return json.load(f)
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -57,6 +62,16 @@ def _worker(rank, world, port):
                     agg = case["request"]["baseExpr"]["chart"]["aggregation"]
                     assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg,
                                       f"world {world} {rule} {case['name']}")
+                else:
+                    assert len(res) == 0
+            for case in _tag_cases():   # tag queries: counts per tag value, merged over the shards
+                paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, _shard(rule, len(paths), world),
+                                             case["glob_size"])
+                if rank == 0:
+                    key = lambda t: sorted(t.items())   # noqa: E731
+                    assert sorted(res.tags, key=key) == sorted(case["expected_merged"], key=key), \
+                        f"world {world} {rule} tag {case['name']}"
                 else:
                     assert len(res) == 0
             print(f"rank {rank}: {rule} ok", flush=True)

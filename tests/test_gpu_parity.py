@@ -361,3 +361,35 @@ def test_plain_string_pages(engine, tmp_path):
             assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"plain glob {gi}")
         merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
         assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "plain merged")
+
+
+def test_tag_query_synthetic_with_nulls(engine):
+    """Tag query over synthetic segments (NULL tags, a window cutting tiles, globs of 2): per-glob {tag, count}
+    rows and merged counts equal the oracle on the same bytes."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    keys, blobs, segs = [], [], []
+    for i in range(3):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 20, null_frac=0.05, rg_rows=1 << 18,
+                                                  page_rows=1 << 15))
+        key = f"synth-tag/{i}"
+        engine.put_segment_ptr(key, s.ptr, s.size)
+        blobs.append(s.bytes())
+        s.free()
+        keys.append(key)
+        segs.append(synth.segment_request(i))
+        segs[-1]["startTs"] += 123_457
+        segs[-1]["endTs"] -= 654_321
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_03", "metric_07"),
+            "q2": {"not": synth.leaf(synth.NAMESPACE, "eq", "ns-03")}}
+    for tag in (synth.SERVICE, synth.NAME):
+        req = json.dumps(synth.pushdown(filt, segs, tag=tag))
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_tag_per_glob(pr, tag, keys, 2, sources=blobs)
+        got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS).per_glob(len(want))
+        key = lambda t: sorted(t.items())   # noqa: E731
+        for gi, (g, w) in enumerate(zip(got, want)):
+            assert sorted((r[2] for r in g), key=key) == sorted(w, key=key), f"{tag} glob {gi}"
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert sorted(merged.tags, key=key) == sorted(dx.evaluate_tag_merged(pr, tag, keys, 2, sources=blobs), key=key)
