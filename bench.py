@@ -177,6 +177,21 @@ def main():
         with open(profs[-1]) as f:
             traffic = json.load(f).get("hbm_bytes_per_launch")
 
+    # measured device-to-device copy rate on this GPU (a stream-copy peak beside the spec peak)
+    copy_gbs = None
+    if rank == 0:
+        a = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        b = torch.empty_like(a)
+        b.copy_(a)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(10):
+            b.copy_(a)
+        e1.record()
+        torch.cuda.synchronize()
+        copy_gbs = 2 * 10 * a.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9   # read + write bytes
+        del a, b
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_sample > 0:
         cpu = cpu_baseline(args, q, synth)
@@ -198,6 +213,7 @@ def main():
                          # measured HBM rate (PMC bytes / kernel time): late materialization reads fewer bytes
                          # than the algorithmic count, so this is the kernel's actual bandwidth use
                          "traffic_gbs": traffic / (scan_avg / 1e3) / 1e9 if traffic else None,
+                         "stream_copy_gbs": copy_gbs,
                          "algorithmic_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
         }

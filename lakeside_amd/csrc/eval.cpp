@@ -710,7 +710,6 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   const size_t stage_bytes = off;
   uint8_t* hbuf = static_cast<uint8_t*>(E.pinned_buf(stage_bytes));
   uint8_t* dbuf = static_cast<uint8_t*>(E.workspace("query", stage_bytes));
-  for (auto& q : qsegs) (void)q;
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
   if (late_mask) {
@@ -806,7 +805,6 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     RP.nbuckets = nbuckets;
     RP.ngroups = ngroups;
     RP.agg = kagg;
-    size_t moff = 0;
     std::vector<uint32_t> flat;
     std::vector<size_t> map_off(strs.size(), SIZE_MAX);
     for (size_t s = 0; s < strs.size(); s++)
@@ -823,7 +821,6 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       RP.map[RP.ndims] = map_off[s] == SIZE_MAX ? nullptr : dmaps + map_off[s];
       RP.ndims++;
     }
-    (void)moff;
     HIP_TRY(hipMemsetAsync(t2, 0, n2 * 16, st));
     HIP_TRY(hipMemsetAsync(RP.out_ext, kagg == AGG_MIN ? 0xff : 0, n2 * 8, st));
     HIP_TRY(launch_rekey_minmax(RP, st));

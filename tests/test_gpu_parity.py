@@ -393,3 +393,50 @@ def test_tag_query_synthetic_with_nulls(engine):
             assert sorted((r[2] for r in g), key=key) == sorted(w, key=key), f"{tag} glob {gi}"
         merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
         assert sorted(merged.tags, key=key) == sorted(dx.evaluate_tag_merged(pr, tag, keys, 2, sources=blobs), key=key)
+
+
+def test_concurrent_calls_from_threads(golden_engine):
+    """The ABI is called from several dispatcher threads at once (re-entrant, thread-safe):
+    four threads evaluate golden chart and tag cases concurrently on one engine, while another thread re-puts a
+    segment into the HBM cache; every result equals the golden rows."""
+    import threading
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    cases = [c for c in _cases() if c["expected_merged"] is not None]
+    tag_cases = _tag_cases()
+    errors = []
+
+    def worker(k):
+        try:
+            for it in range(3):
+                for case in cases[k::4]:
+                    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                    res = golden_engine.eval_pushdown(json.dumps(case["request"]), paths, case["glob_size"], LK_MERGED)
+                    agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+                    assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"thread {k} {case['name']}")
+                for case in tag_cases[k::4]:
+                    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                    res = golden_engine.eval_pushdown(json.dumps(case["request"]), paths, case["glob_size"],
+                                                      LK_PER_GLOB_ROWS)
+                    got = sorted((sorted(t.items()) for t in res.tags))
+                    want = sorted(sorted(t.items()) for g in case["expected_per_glob"] for t in g)
+                    assert got == want, f"thread {k} tag {case['name']}"
+        except Exception as e:   # noqa: BLE001 - reported below
+            errors.append(e)
+
+    def loader():
+        try:
+            p = os.path.join(GOLDEN, "segments", "seg13.parquet")
+            with open(p, "rb") as f:
+                data = f.read()
+            for _ in range(5):
+                golden_engine.put_segment("concurrent/seg13", data)
+        except Exception as e:   # noqa: BLE001
+            errors.append(e)
+
+    ts = [threading.Thread(target=worker, args=(k,)) for k in range(4)] + [threading.Thread(target=loader)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert not any(t.is_alive() for t in ts), "a thread did not finish"
+    assert not errors, errors[0]
