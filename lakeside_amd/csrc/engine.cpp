@@ -98,6 +98,21 @@ HostBlock pinned_acquire(size_t bytes) {
   return b;
 }
 
+std::shared_ptr<void> zero_block(size_t bytes) {
+  static std::mutex mu;
+  static std::shared_ptr<void> blk;
+  static size_t cap = 0;
+  std::lock_guard<std::mutex> g(mu);
+  if (!blk || cap < bytes) {
+    const size_t n = std::max<size_t>(align_up(bytes, size_t(1) << 20), size_t(1) << 20);
+    void* p = std::calloc(n, 1);
+    if (!p) throw std::bad_alloc();
+    blk = std::shared_ptr<void>(p, [](void* q) { std::free(q); });   // earlier results keep the old block alive
+    cap = n;
+  }
+  return blk;
+}
+
 void pinned_release(HostBlock b) {
   if (!b.p) return;
   std::lock_guard<std::mutex> g(g_pool_mu);

@@ -863,19 +863,19 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (hflags & FLAG_METRICS_UNALIGNED)
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
-  res->alloc_rows(nrows_out);
+  res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
   if (nrows_out) {
     if (res->blk.pinned) {
       // Rows written by the kernel straight into the mapped pinned result block: no device->host copies (small
       // async D2H copies cost ~1 ms of completion latency each call on this stack, measured in bench C4).
-      HIP_TRY(launch_finalize_write(F, d_counts, res->ts, res->val, res->gid, res->glob, st));
+      HIP_TRY(launch_finalize_write(F, d_counts, res->ts, res->val, res->gid, per_glob_rows ? res->glob : nullptr, st));
     } else {
       HIP_TRY(launch_finalize_write(F, d_counts, d_ts, d_val, d_gid, d_glob, st));
       HIP_TRY(hipMemcpyAsync(res->ts, d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->val, d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->gid, d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+      if (per_glob_rows) HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
   }

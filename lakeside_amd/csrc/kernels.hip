@@ -175,7 +175,7 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
       out_ts[pos] = F.bucket_base + (int64_t)b * F.step;
       out_val[pos] = r.value;
       out_gid[pos] = r.gid;
-      out_glob[pos] = r.glob;
+      if (out_glob) out_glob[pos] = r.glob;   // null: merged rows (glob 0, a shared zero block on the host)
     }
     off += tot;
     __syncthreads();
