@@ -189,6 +189,53 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
+// DuckDB's regexp_matches(col, pat, 'i') is RE2; the host matcher is std::regex ECMAScript
+// with icase.  Rewrite the RE2 spellings ECMAScript lacks but whose meaning it has: a leading case-insensitive
+// flag group `(?i)` (already implied by 'i'), `\A` / `\z` (text start / end = `^` / `$` without multiline) and
+// named groups `(?P<name>...)`.  Anything else RE2-only makes std::regex throw -> LK_ERR_UNSUPPORTED.
+std::string re2_to_ecmascript(const std::string& p) {
+  std::string out;
+  size_t i = 0;
+  if (p.compare(0, 4, "(?i)") == 0) i = 4;
+  bool cls = false;   // inside [...]
+  for (; i < p.size(); i++) {
+    const char c = p[i];
+    if (c == '\\' && i + 1 < p.size()) {
+      const char n = p[i + 1];
+      if (!cls && n == 'A') out += '^';
+      else if (!cls && n == 'z') out += '$';
+      else { out += c; out += n; }
+      i++;
+      continue;
+    }
+    if (cls) {
+      if (c == ']') cls = false;
+      out += c;
+      continue;
+    }
+    if (c == '[') {
+      cls = true;
+      out += c;
+      if (i + 1 < p.size() && p[i + 1] == '^') out += p[++i];
+      if (i + 1 < p.size() && p[i + 1] == ']') {   // RE2: a leading ']' is a literal; ECMAScript: escape it
+        out += "\\]";
+        i++;
+      }
+      continue;
+    }
+    if (c == '(' && p.compare(i, 4, "(?P<") == 0) {
+      const size_t e = p.find('>', i + 4);
+      if (e != std::string::npos) {
+        out += '(';
+        i = e;
+        continue;
+      }
+    }
+    out += c;
+  }
+  return out;
+}
+
 // NoisyTagsDropper.DO_NOT_DISPLAY_TAGS / DO_NOT_DISPLAY_TAG_PREFIXES (core/.../utils/NoisyTagsDropper.scala)
 bool noisy_tag(const std::string& t) {
   static const char* const names[] = {
@@ -462,7 +509,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     for (size_t j = 0; j < sc.leaves.size(); j++) {
       const FilterNode* l = sc.leaves[j];
       if (l->op == "regex" || l->op == "contains") {
-        std::string pat = l->op == "contains" ? ".*" + l->v[0] + ".*" : l->v[0];
+        std::string pat = re2_to_ecmascript(l->op == "contains" ? ".*" + l->v[0] + ".*" : l->v[0]);
         try {
           res[j] = std::regex(pat, std::regex::ECMAScript | std::regex::icase | std::regex::optimize);
         } catch (const std::regex_error& e) {

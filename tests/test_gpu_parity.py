@@ -440,3 +440,20 @@ def test_concurrent_calls_from_threads(golden_engine):
         t.join(timeout=240)
     assert not any(t.is_alive() for t in ts), "a thread did not finish"
     assert not errors, errors[0]
+
+
+@pytest.mark.parametrize("pattern", ["(?i)^SVC-0[0-4]", "\\Asvc-0[0-4]", "(?P<id>svc-0[1-3])[0-9]\\z", "[]x]|svc-09"])
+def test_regex_re2_spellings(golden_engine, pattern):
+    """RE2 spellings std::regex lacks ((?i) prefix, \\A, \\z, named groups) match exactly as RE2 does (oracle:
+    pyarrow's RE2, the engine behind DuckDB's regexp_matches)."""
+    from lakeside_amd import LK_MERGED
+    from oracle import dataexpr as dx
+    case = next(c for c in _cases() if c["name"] == "c3_and_regex_by2_max")
+    req = json.loads(json.dumps(case["request"]))
+    req["baseExpr"]["filter"]["q2"]["v"] = [pattern]
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    text = json.dumps(req)
+    got = golden_engine.eval_pushdown(text, paths, case["glob_size"], LK_MERGED)
+    want = dx.evaluate_merged(dx.parse_pushdown(text), paths, case["glob_size"])
+    assert len(want) > 0
+    assert_rows_equal(got.rows(), want, "max", pattern)
