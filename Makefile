@@ -10,13 +10,14 @@ SRC     = lakeside_amd/csrc
 OBJDIR  = build/obj
 LIB     = lakeside_amd/liblakeside_gpu.so
 SYNTH   = lakeside_amd/liblakeside_synth.so
+RELIB   = lakeside_amd/liblakeside_regex.so
 
-HOST_SRCS = $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_SRCS = $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o
-HDRS = $(wildcard $(SRC)/*.hpp) include/lakeside_gpu.h
+HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
 
-all: $(LIB) $(SYNTH)
+all: $(LIB) $(SYNTH) $(RELIB)
 
 $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -29,6 +30,10 @@ $(OBJDIR)/kernels.o: $(SRC)/kernels.hip $(HDRS)
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
 
+# host-only RE2-semantics matcher (CPU differential tests against RE2; the evaluator links regex.cpp itself)
+$(RELIB): $(SRC)/regex.cpp $(SRC)/regex_capi.cpp $(SRC)/regex.hpp $(SRC)/unicode_tables.inc include/lakeside_regex.h
+	g++ $(CXXFLAGS_HOST) -shared -o $@ $(SRC)/regex.cpp $(SRC)/regex_capi.cpp
+
 $(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
 	g++ -O3 -std=c++17 -fPIC -shared -pthread -Wall -o $@ tools/synth.cpp
 
@@ -38,7 +43,14 @@ asm: $(SRC)/kernels.hip $(HDRS)
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o build/kernels.s
 
 clean:
-	rm -rf build $(LIB) $(SYNTH)
+	rm -rf build $(LIB) $(SYNTH) $(RELIB)
 
 
 .PHONY: all clean asm
+
+# CPU restatement of the evaluator (oracle: test / bench-baseline infrastructure only, never the product path)
+CPULIB = oracle/liblkcpu.so
+$(CPULIB): oracle/cpu/lkcpu.cpp
+	g++ -O3 -std=c++17 -fPIC -fopenmp -shared -Wall -Wextra -Wno-unused-parameter -o $@ $<
+
+all: $(CPULIB)

@@ -94,8 +94,16 @@ int lk_segment_evict(lk_engine* e, const char* key) {
   return LK_OK;
 }
 
-size_t lk_segment_count(const lk_engine* e) { return e ? e->e->cache.size() : 0; }
-size_t lk_segment_bytes(const lk_engine* e) { return e ? e->e->cache_bytes : 0; }
+size_t lk_segment_count(const lk_engine* e) {
+  if (!e) return 0;
+  std::lock_guard<std::mutex> g(e->e->cache_mu);
+  return e->e->cache.size();
+}
+size_t lk_segment_bytes(const lk_engine* e) {
+  if (!e) return 0;
+  std::lock_guard<std::mutex> g(e->e->cache_mu);
+  return e->e->cache_bytes;
+}
 
 static int eval_common(lk_engine* e, const char* json, const char* const* paths, size_t n_paths, const int32_t* shard,
                        int glob_size, unsigned flags, bool dist, lk_result** out) {
@@ -104,7 +112,6 @@ static int eval_common(lk_engine* e, const char* json, const char* const* paths,
   return guarded([&] {
     auto* r = new lk_result();
     try {
-      std::lock_guard<std::mutex> g(e->e->eval_mu);
       lk::evaluate(*e->e, json, paths, n_paths, glob_size, flags, shard, dist, r);
     } catch (...) {
       delete r;

@@ -49,10 +49,11 @@ struct Comm {
   int rank = 0;
   virtual ~Comm() = default;
   // host blobs of every rank, rank order
-  virtual std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) = 0;
-  // `bytes` of device memory from every rank into rank 0's `recv` (world * bytes; slot 0 is left untouched),
-  // ordered on E.stream
-  virtual void gather_table(Engine& E, const void* send, void* recv, size_t bytes) = 0;
+  virtual std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) = 0;
+  // `bytes[r]` of device memory from every rank r into rank 0's `recv` at offsets `off[r]` (slot 0 is left
+  // untouched), ordered on X.stream
+  virtual void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
+                              const std::vector<size_t>& off) = 0;
 };
 
 namespace {
@@ -63,11 +64,11 @@ struct RcclComm final : Comm {
     if (comm) ncclCommDestroy(comm);
   }
 
-  std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) override {
+  std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) override {
     if (world == 1) return {mine};
     HIP_TRY2(hipSetDevice(E.device));
-    hipStream_t st = E.stream;
-    uint64_t* dsz = static_cast<uint64_t*>(E.workspace("comm_sizes", size_t(world) * 8));
+    hipStream_t st = X.stream;
+    uint64_t* dsz = static_cast<uint64_t*>(X.workspace("comm_sizes", size_t(world) * 8));
     std::vector<uint64_t> sz(size_t(world), 0);
     sz[size_t(rank)] = mine.size();
     HIP_TRY2(hipMemcpyAsync(dsz + rank, &sz[size_t(rank)], 8, hipMemcpyHostToDevice, st));
@@ -76,7 +77,7 @@ struct RcclComm final : Comm {
     HIP_TRY2(hipStreamSynchronize(st));
     uint64_t mx = 1;
     for (uint64_t x : sz) mx = std::max(mx, x);
-    uint8_t* d = static_cast<uint8_t*>(E.workspace("comm_blobs", size_t(world) * mx));
+    uint8_t* d = static_cast<uint8_t*>(X.workspace("comm_blobs", size_t(world) * mx));
     if (!mine.empty())
       HIP_TRY2(hipMemcpyAsync(d + size_t(rank) * mx, mine.data(), mine.size(), hipMemcpyHostToDevice, st));
     NCCL_TRY(ncclAllGather(d + size_t(rank) * mx, d, mx, ncclUint8, comm, st));
@@ -88,14 +89,17 @@ struct RcclComm final : Comm {
     return out;
   }
 
-  void gather_table(Engine& E, const void* send, void* recv, size_t bytes) override {
+  void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
+                      const std::vector<size_t>& off) override {
     if (world == 1) return;
+    // grouped point-to-point: every peer streams into rank 0 over its own xGMI link at once
     NCCL_TRY(ncclGroupStart());
     if (rank == 0) {
       for (int r = 1; r < world; r++)
-        NCCL_TRY(ncclRecv(static_cast<uint8_t*>(recv) + size_t(r) * bytes, bytes, ncclUint8, r, comm, E.stream));
-    } else {
-      NCCL_TRY(ncclSend(send, bytes, ncclUint8, 0, comm, E.stream));
+        if (bytes[size_t(r)])
+          NCCL_TRY(ncclRecv(static_cast<uint8_t*>(recv) + off[size_t(r)], bytes[size_t(r)], ncclUint8, r, comm, X.stream));
+    } else if (bytes[size_t(rank)]) {
+      NCCL_TRY(ncclSend(send, bytes[size_t(rank)], ncclUint8, 0, comm, X.stream));
     }
     NCCL_TRY(ncclGroupEnd());
   }
@@ -109,7 +113,7 @@ struct HostComm final : Comm {
     if (fn(user, send, bytes, recv) != 0) throw PlanError(LK_ERR_DEVICE, "host transport: all-gather callback failed");
   }
 
-  std::vector<std::string> allgather_bytes(Engine& E, const std::string& mine) override {
+  std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) override {
     if (world == 1) return {mine};
     const uint64_t n = mine.size();
     std::vector<uint64_t> sz(static_cast<size_t>(world));
@@ -125,17 +129,24 @@ struct HostComm final : Comm {
     return out;
   }
 
-  void gather_table(Engine& E, const void* send, void* recv, size_t bytes) override {
+  void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
+                      const std::vector<size_t>& off) override {
     if (world == 1) return;
     HIP_TRY2(hipSetDevice(E.device));
-    std::vector<uint8_t> mine(bytes), all(size_t(world) * bytes);
-    HIP_TRY2(hipMemcpyAsync(mine.data(), send, bytes, hipMemcpyDeviceToHost, E.stream));
-    HIP_TRY2(hipStreamSynchronize(E.stream));
-    allgather(mine.data(), bytes, all.data());
+    size_t mx = 1;
+    for (size_t b : bytes) mx = std::max(mx, b);
+    std::vector<uint8_t> mine(mx, 0), all(size_t(world) * mx);
+    if (bytes[size_t(rank)]) {
+      HIP_TRY2(hipMemcpyAsync(mine.data(), send, bytes[size_t(rank)], hipMemcpyDeviceToHost, X.stream));
+      HIP_TRY2(hipStreamSynchronize(X.stream));
+    }
+    allgather(mine.data(), mx, all.data());
     if (rank == 0) {
-      HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + bytes, all.data() + bytes, size_t(world - 1) * bytes,
-                              hipMemcpyHostToDevice, E.stream));
-      HIP_TRY2(hipStreamSynchronize(E.stream));   // `all` is freed on return
+      for (int r = 1; r < world; r++)
+        if (bytes[size_t(r)])
+          HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * mx,
+                                  bytes[size_t(r)], hipMemcpyHostToDevice, X.stream));
+      HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed on return
     }
   }
 };
@@ -155,32 +166,116 @@ static Comm& need_comm(Engine& E) {
   return *E.comm;
 }
 
-void comm_allreduce_max_u8(Engine& E, uint8_t* host, size_t n) {
+void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n) {
   Comm& C = need_comm(E);
   if (C.world == 1) return;
-  std::vector<std::string> all = C.allgather_bytes(E, std::string(reinterpret_cast<const char*>(host), n));
+  std::vector<std::string> all = C.allgather_bytes(E, X, std::string(reinterpret_cast<const char*>(host), n));
   for (auto& b : all) {
     if (b.size() != n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
     for (size_t i = 0; i < n; i++) host[i] = std::max(host[i], uint8_t(b[i]));
   }
 }
 
-std::vector<std::string> comm_allgather_bytes(Engine& E, const std::string& mine) {
-  return need_comm(E).allgather_bytes(E, mine);
+std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) {
+  return need_comm(E).allgather_bytes(E, X, mine);
 }
 
-void comm_reduce_table(Engine& E, const QParams& P, int agg, size_t nc) {
+void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg) {
+  Comm& C = need_comm(E);
+  std::string mine;
+  if (code != 0) {
+    mine.resize(4);
+    memcpy(&mine[0], &code, 4);
+    mine += msg;
+  }
+  if (C.world == 1) {
+    if (code) throw PlanError(code, msg);
+    return;
+  }
+  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
+  for (int r = 0; r < C.world; r++) {
+    const std::string& b = all[size_t(r)];
+    if (b.size() < 4) continue;
+    int c;
+    memcpy(&c, b.data(), 4);
+    throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(4));
+  }
+}
+
+void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc) {
   Comm& C = need_comm(E);
   if (C.world == 1) return;
   // the table is one contiguous block [rows | cnt | hi | lo | ext] (eval.cpp)
   const size_t bytes = nc * 8 * 5;
   unsigned long long* parts =
-      C.rank == 0 ? static_cast<unsigned long long*>(E.workspace("comm_parts", size_t(C.world) * bytes)) : nullptr;
-  C.gather_table(E, P.rows, parts, bytes);
+      C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_parts", size_t(C.world) * bytes)) : nullptr;
+  std::vector<size_t> sz(size_t(C.world), bytes), off(size_t(C.world));
+  for (int r = 0; r < C.world; r++) off[size_t(r)] = size_t(r) * bytes;
+  C.gather_to_root(E, X, P.rows, parts, sz, off);
   if (C.rank == 0) {
     TableRef T{P.rows, P.cnt, P.hi, P.lo, P.ext};
-    HIP_TRY2(launch_merge_tables(T, parts, C.world, nc, agg, E.stream));
+    HIP_TRY2(launch_merge_tables(T, parts, C.world, nc, agg, X.stream));
   }
+}
+
+void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long long& cap) {
+  Comm& C = need_comm(E);
+  if (C.world == 1) return;
+  // this rank's occupied slots -> compact records [key | rows | cnt | hi | lo | ext]
+  SParams S{};
+  S.keys = P.hkeys;
+  S.rows = P.rows;
+  S.cnt = P.cnt;
+  S.hi = P.hi;
+  S.lo = P.lo;
+  S.ext = P.ext;
+  S.cap = cap;
+  const uint32_t nb = sparse_blocks(cap);
+  uint32_t* counts = static_cast<uint32_t*>(X.workspace("comm_rec_counts", (size_t(nb) + 2) * 4));
+  HIP_TRY2(launch_sparse_count(S, counts, X.stream));
+  uint32_t n = 0;
+  HIP_TRY2(hipMemcpyAsync(&n, counts + nb, 4, hipMemcpyDeviceToHost, X.stream));
+  HIP_TRY2(hipStreamSynchronize(X.stream));
+  unsigned long long* recs = static_cast<unsigned long long*>(X.workspace("comm_recs", size_t(n) * 48 + 64));
+  HIP_TRY2(launch_table_records(P, cap, counts, recs, n, X.stream));
+  // record counts of every rank, then the records into rank 0 (rank order)
+  std::string mine(8, '\0');
+  const uint64_t n64 = n;
+  memcpy(&mine[0], &n64, 8);
+  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
+  std::vector<size_t> sz(size_t(C.world)), off(size_t(C.world));
+  size_t total = 0, nrec = 0;
+  for (int r = 0; r < C.world; r++) {
+    uint64_t x;
+    memcpy(&x, all[size_t(r)].data(), 8);
+    sz[size_t(r)] = size_t(x) * 48;
+    off[size_t(r)] = total;
+    total += sz[size_t(r)];
+    nrec += size_t(x);
+  }
+  unsigned long long* parts =
+      C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_rec_parts", total + 64)) : nullptr;
+  HIP_TRY2(hipStreamSynchronize(X.stream));   // records complete before they are sent
+  C.gather_to_root(E, X, recs, parts, sz, off);
+  if (C.rank != 0) return;
+  // rank 0: a fresh table for the union (at most nrec distinct keys, load factor <= 1/2)
+  unsigned long long cap0 = 1 << 16;
+  while (cap0 < 2 * nrec) cap0 <<= 1;
+  uint8_t* tb = static_cast<uint8_t*>(X.workspace("table_merged", size_t(cap0) * 48 + 1024));
+  P.rows = reinterpret_cast<unsigned long long*>(tb);
+  P.cnt = reinterpret_cast<unsigned long long*>(tb + cap0 * 8);
+  P.hi = reinterpret_cast<double*>(tb + cap0 * 16);
+  P.lo = reinterpret_cast<double*>(tb + cap0 * 24);
+  P.ext = reinterpret_cast<unsigned long long*>(tb + cap0 * 32);
+  P.hkeys = reinterpret_cast<unsigned long long*>(tb + cap0 * 40);
+  P.hmask = cap0 - 1;
+  HIP_TRY2(hipMemsetAsync(tb, 0, size_t(cap0) * 32, X.stream));
+  HIP_TRY2(hipMemsetAsync(P.ext, agg == AGG_MIN ? 0xff : 0, size_t(cap0) * 8, X.stream));
+  HIP_TRY2(hipMemsetAsync(P.hkeys, 0xff, size_t(cap0) * 8, X.stream));
+  HIP_TRY2(launch_merge_records(P, recs, n, agg, X.stream));
+  for (int r = 1; r < C.world; r++)
+    HIP_TRY2(launch_merge_records(P, parts + off[size_t(r)] / 8, sz[size_t(r)] / 48, agg, X.stream));
+  cap = cap0;
 }
 
 }  // namespace lk

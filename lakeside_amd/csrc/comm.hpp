@@ -13,12 +13,19 @@ namespace lk {
 int comm_world(const Engine& E);
 int comm_rank(const Engine& E);
 // Element-wise max of a small host byte array across ranks (glob column unions, null flags).
-void comm_allreduce_max_u8(Engine& E, uint8_t* host, size_t n);
+void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n);
 // Concatenation, in rank order, of every rank's byte blob (variable length): one all-gather of the sizes,
 // one of the blobs padded to the largest.
-std::vector<std::string> comm_allgather_bytes(Engine& E, const std::string& mine);
-// Reduce the partial aggregation table (P.rows/cnt/hi/lo/ext, nc cells) onto rank 0: counts by sum,
-// min/max by min/max on order-preserving bits (exact), compensated sums gathered and added in rank order.
-void comm_reduce_table(Engine& E, const QParams& P, int agg, size_t nc);
+std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::string& mine);
+// Every rank reports its local status (0 = ok); if any rank failed, every rank throws the first failure
+// (PlanError with that rank's code), so no rank is left waiting in a later collective.
+void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg);
+// Dense mode: reduce the partial aggregation table (P.rows/cnt/hi/lo/ext, nc cells) onto rank 0: counts by
+// sum, min/max by min/max on order-preserving bits (exact), compensated sums gathered and added in rank order.
+void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc);
+// Hash mode: every rank compacts its occupied slots into records; rank 0 gathers them and inserts every rank's
+// records, in rank order, into a fresh table sized for their union (launch_merge_records).  On rank 0, P's table
+// pointers and `cap` (slots) are replaced by the merged table's.
+void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long long& cap);
 
 }  // namespace lk

@@ -113,11 +113,41 @@ __device__ __forceinline__ void acc_reset(Acc& a, unsigned long long key) {
   a.ext = (AGG == AGG_MIN) ? ~0ull : 0ull;
 }
 
+__device__ __forceinline__ unsigned long long mix64(unsigned long long x) {   // splitmix64 finalizer
+  x ^= x >> 30;
+  x *= 0xbf58476d1ce4e5b9ull;
+  x ^= x >> 27;
+  x *= 0x94d049bb133111ebull;
+  return x ^ (x >> 31);
+}
+
+// Slot of cell key `cell` in a hash-mode table (linear probing; the key is claimed by CAS).  ~0 when the probe
+// limit is reached: FLAG_HASH_FULL is raised and the host re-runs the query with a larger table.
+__device__ __forceinline__ unsigned long long hash_slot(unsigned long long* keys, unsigned long long mask,
+                                                       uint32_t* flags, unsigned long long cell) {
+  unsigned long long h = mix64(cell) & mask;
+  for (uint32_t p = 0; p < HASH_MAX_PROBE; p++) {
+    unsigned long long k = __hip_atomic_load(&keys[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k == EMPTY) {
+      k = atomicCAS(&keys[h], EMPTY, cell);
+      if (k == EMPTY) return h;
+    }
+    if (k == cell) return h;
+    h = (h + 1) & mask;
+  }
+  atomicOr(flags, FLAG_HASH_FULL);
+  return EMPTY;
+}
+
 // Merge a partial cell into the global table (device-scope atomics).
 template <int AGG>
 __device__ __forceinline__ void global_merge(const QParams& P, unsigned long long cell, uint32_t rows,
                                              uint32_t cnt, double hi, double lo, unsigned long long ext) {
   if (rows == 0) return;
+  if (P.hkeys) {
+    cell = hash_slot(P.hkeys, P.hmask, P.flags, cell);
+    if (cell == EMPTY) return;
+  }
   atomicAdd(&P.rows[cell], (unsigned long long)rows);
   if (cnt == 0) return;
   atomicAdd(&P.cnt[cell], (unsigned long long)cnt);

@@ -20,7 +20,6 @@
 #include <map>
 #include <memory>
 #include <mutex>
-#include <regex>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -679,37 +678,109 @@ Engine::Engine(int dev) : device(dev) {
   if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) throw DeviceError("no HIP device available");
   if (dev < 0 || dev >= n) throw DeviceError("device index out of range");
   HIP_CHECK(hipSetDevice(device));
+  ctx_free.push_back(std::make_unique<CallCtx>(device));   // one context up front: fail here, not mid-query
+  ctx_made = 1;
+}
+
+Engine::~Engine() {
+  (void)hipSetDevice(device);
+  comm_destroy();
+  ctx_free.clear();
+  cache.clear();
+}
+
+std::unique_ptr<CallCtx> Engine::acquire_ctx() {
+  std::unique_lock<std::mutex> g(ctx_mu);
+  for (;;) {
+    if (!ctx_free.empty()) {
+      auto c = std::move(ctx_free.back());
+      ctx_free.pop_back();
+      return c;
+    }
+    if (ctx_made < max_calls) {
+      ctx_made++;
+      g.unlock();
+      try {
+        return std::make_unique<CallCtx>(device);
+      } catch (...) {
+        std::lock_guard<std::mutex> g2(ctx_mu);
+        ctx_made--;
+        throw;
+      }
+    }
+    ctx_cv.wait(g);
+  }
+}
+
+void Engine::release_ctx(std::unique_ptr<CallCtx> c) {
+  if (!c) return;
+  {
+    std::lock_guard<std::mutex> g(ctx_mu);
+    ctx_free.push_back(std::move(c));
+  }
+  ctx_cv.notify_one();
+}
+
+std::shared_ptr<LeafBits> Engine::leaf_bits(const std::string& key) {
+  std::lock_guard<std::mutex> g(leaf_mu);
+  auto& slot = leaf_cache[key];
+  if (!slot) {
+    slot = std::make_shared<LeafBits>();
+    if (leaf_cache.size() > 256) {   // bounded: drop entries nobody holds (a query re-fills what it needs)
+      for (auto it = leaf_cache.begin(); it != leaf_cache.end() && leaf_cache.size() > 128;) {
+        if (it->first != key && it->second.use_count() == 1) it = leaf_cache.erase(it);
+        else ++it;
+      }
+    }
+  }
+  return slot;
+}
+
+CallCtx::CallCtx(int dev) : device(dev) {
+  HIP_CHECK(hipSetDevice(device));
   HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreate(&ev_scan0));
   HIP_CHECK(hipEventCreate(&ev_scan1));
   HIP_CHECK(hipHostMalloc(&pinned, pinned_cap = 1 << 20));
 }
 
-Engine::~Engine() {
+CallCtx::~CallCtx() {
   (void)hipSetDevice(device);
-  cache.clear();
+  if (stream) (void)hipStreamSynchronize(stream);
   for (auto& w : ws)
     if (w.second.p) (void)hipFree(w.second.p);
   if (pinned) (void)hipHostFree(pinned);
   if (ev_scan0) (void)hipEventDestroy(ev_scan0);
   if (ev_scan1) (void)hipEventDestroy(ev_scan1);
   if (stream) (void)hipStreamDestroy(stream);
-  comm_destroy();
 }
 
-void* Engine::workspace(const std::string& name, size_t bytes) {
+void* CallCtx::workspace(const std::string& name, size_t bytes) {
   auto& w = ws[name];
   if (w.cap < bytes) {
-    if (w.p) HIP_CHECK(hipFree(w.p));
-    w.cap = align_up(std::max(bytes, w.cap * 3 / 2), 1 << 20);
-    HIP_CHECK(hipMalloc(&w.p, w.cap));
+    if (w.p) {
+      HIP_CHECK(hipStreamSynchronize(stream));   // earlier work of this call may still read it
+      HIP_CHECK(hipFree(w.p));
+      w.p = nullptr;
+      w.cap = 0;
+    }
+    const size_t cap = align_up(std::max(bytes, w.cap * 3 / 2), 1 << 20);
+    hipError_t e = hipMalloc(&w.p, cap);
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      w.p = nullptr;
+      throw PlanError(LK_ERR_MEMORY, "HBM: cannot allocate " + std::to_string(cap) + " bytes of workspace '" + name + "'");
+    }
+    w.cap = cap;
   }
   return w.p;
 }
 
-void* Engine::pinned_buf(size_t bytes) {
+void* CallCtx::pinned_buf(size_t bytes) {
   if (pinned_cap < bytes) {
+    HIP_CHECK(hipStreamSynchronize(stream));
     HIP_CHECK(hipHostFree(pinned));
+    pinned = nullptr;
     pinned_cap = align_up(bytes, 1 << 20);
     HIP_CHECK(hipHostMalloc(&pinned, pinned_cap));
   }

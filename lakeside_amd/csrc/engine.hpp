@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <condition_variable>
 #include <deque>
 #include <map>
 #include <memory>
@@ -90,6 +91,24 @@ struct Workspace {
   size_t cap = 0;
 };
 
+// Device resources of one evaluation in flight: its own stream, timing events, device workspaces and pinned
+// staging.  The engine keeps a small pool, so calls from several dispatcher threads run concurrently on their own
+// streams (the reference keeps up to 8 glob queries in flight, Commons.scala:371-372).
+struct CallCtx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev_scan0 = nullptr, ev_scan1 = nullptr;
+  std::map<std::string, Workspace> ws;
+  void* pinned = nullptr;
+  size_t pinned_cap = 0;
+  explicit CallCtx(int dev);
+  ~CallCtx();
+  CallCtx(const CallCtx&) = delete;
+  CallCtx& operator=(const CallCtx&) = delete;
+  void* workspace(const std::string& name, size_t bytes);
+  void* pinned_buf(size_t bytes);
+};
+
 struct Comm;   // comm.cpp
 
 // The sorted order of a column's engine dictionary (its first n values) and a 128-bit fingerprint of the sorted
@@ -113,20 +132,31 @@ HostBlock pinned_acquire(size_t bytes);
 std::shared_ptr<void> zero_block(size_t bytes);
 void pinned_release(HostBlock b);
 
+// Per (column, leaf) cache of leaf outcomes over the column's engine dictionary: bit j of byte i = leaf j of the
+// column on dictionary value i.  Extended incrementally as the dictionary grows, so a regex over a 10M-value
+// dictionary is matched once per value, not once per value per query.
+struct LeafBits {
+  std::mutex mu;
+  std::vector<uint8_t> hit;   // one byte per evaluated dictionary value
+};
+
 struct Engine {
   int device = 0;
-  hipStream_t stream = nullptr;
-  hipEvent_t ev_scan0 = nullptr, ev_scan1 = nullptr;
-  std::mutex eval_mu;                            // one evaluation at a time per engine (round 1)
-  std::mutex dev_mu;
+  size_t max_calls = 4;                          // evaluation contexts (streams) in flight
+  std::mutex ctx_mu;
+  std::condition_variable ctx_cv;
+  std::vector<std::unique_ptr<CallCtx>> ctx_free;
+  size_t ctx_made = 0;
+  std::mutex comm_mu;                            // distributed calls: collectives in one order on every rank
+  std::mutex dev_mu;                             // segment upload
   std::mutex cache_mu;
   std::unordered_map<std::string, std::shared_ptr<Segment>> cache;
   size_t cache_bytes = 0;
   std::mutex dict_mu;
   std::unordered_map<std::string, std::unique_ptr<GlobalDict>> dicts;
-  std::map<std::string, Workspace> ws;
-  void* pinned = nullptr;
-  size_t pinned_cap = 0;
+  std::mutex leaf_mu;
+  std::map<std::string, std::shared_ptr<LeafBits>> leaf_cache;   // key: column \x1f op \x1f values
+  std::shared_ptr<LeafBits> leaf_bits(const std::string& key);
   Comm* comm = nullptr;
   std::mutex order_mu;
   std::unordered_map<std::string, std::shared_ptr<const DictOrder>> orders;   // per column, latest size
@@ -138,9 +168,22 @@ struct Engine {
   std::shared_ptr<Segment> build_segment(const std::string& key, const uint8_t* data, size_t size);
   int put_segment(const std::string& key, const uint8_t* data, size_t size);
   std::shared_ptr<Segment> get_segment(const std::string& key, bool load_on_miss);
-  void* workspace(const std::string& name, size_t bytes);
-  void* pinned_buf(size_t bytes);
+  std::unique_ptr<CallCtx> acquire_ctx();
+  void release_ctx(std::unique_ptr<CallCtx> c);
   void comm_destroy();
+};
+
+// RAII: a call context for the duration of one evaluation.
+class CtxLease {
+ public:
+  explicit CtxLease(Engine& e) : e_(e), c_(e.acquire_ctx()) {}
+  ~CtxLease() { e_.release_ctx(std::move(c_)); }
+  CallCtx& operator*() { return *c_; }
+  CallCtx* operator->() { return c_.get(); }
+
+ private:
+  Engine& e_;
+  std::unique_ptr<CallCtx> c_;
 };
 
 }  // namespace lk

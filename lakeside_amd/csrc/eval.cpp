@@ -15,7 +15,7 @@
 #include <climits>
 #include <cmath>
 #include <cstring>
-#include <regex>
+#include <unordered_set>
 #include <string>
 #include <vector>
 
@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "layout.hpp"
 #include "plan.hpp"
+#include "regex.hpp"
 
 namespace lk {
 
@@ -101,15 +102,29 @@ struct GlobInfo {
   std::vector<std::pair<std::string, std::string>> query_tags;   // glob head's queryTags
 };
 
-bool leaf_eval(const FilterNode& f, const std::string& s, const std::regex* re) {
+// One leaf on one dictionary value (BaseExpr.scala:470-501).  `re`: the compiled RE2-semantics matcher of a
+// regex / contains leaf; `set`: the value list of a large in / not_in.
+bool leaf_eval(const FilterNode& f, const std::string& s, re::Regex* re, const std::unordered_set<std::string>* set) {
   const std::string& op = f.op;
   if (op == "eq") return s == f.v[0];
   if (op == "!=") return s != f.v[0];
-  if (op == "in") return std::find(f.v.begin(), f.v.end(), s) != f.v.end();
-  if (op == "not_in") return std::find(f.v.begin(), f.v.end(), s) == f.v.end();
+  if (op == "in") return set ? set->count(s) != 0 : std::find(f.v.begin(), f.v.end(), s) != f.v.end();
+  if (op == "not_in") return set ? set->count(s) == 0 : std::find(f.v.begin(), f.v.end(), s) == f.v.end();
   if (op == "has" || op == "exists") return true;
-  if (op == "regex" || op == "contains") return std::regex_search(s, *re);
+  if (op == "regex" || op == "contains") return re->search(s);
   throw PlanError(LK_ERR_UNSUPPORTED, "operator " + op);
+}
+
+// regexp_matches(label, p, 'i') (BaseExpr.scala:485-486) / regexp_matches(label, '.*p.*', 'i') (500-501).  A pattern
+// RE2 rejects makes DuckDB fail the glob's query, which Commons.toGlobResultSet turns into an empty result
+// (Commons.scala:249-253): LK_ERR_ARG, which the shim maps to the same empty source.
+re::Regex compile_leaf_regex(const FilterNode& l) {
+  const std::string pat = l.op == "contains" ? ".*" + l.v[0] + ".*" : l.v[0];
+  try {
+    return re::Regex(pat, true);
+  } catch (const re::RegexError& e) {
+    throw PlanError(e.unsupported ? LK_ERR_UNSUPPORTED : LK_ERR_ARG, std::string("regex '") + pat + "': " + e.what());
+  }
 }
 
 void postfix(const FilterNode* n, const std::vector<LeafInfo>& leaves, std::vector<uint8_t>& prog) {
@@ -189,53 +204,6 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
   return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
-// DuckDB's regexp_matches(col, pat, 'i') is RE2; the host matcher is std::regex ECMAScript
-// with icase.  Rewrite the RE2 spellings ECMAScript lacks but whose meaning it has: a leading case-insensitive
-// flag group `(?i)` (already implied by 'i'), `\A` / `\z` (text start / end = `^` / `$` without multiline) and
-// named groups `(?P<name>...)`.  Anything else RE2-only makes std::regex throw -> LK_ERR_UNSUPPORTED.
-std::string re2_to_ecmascript(const std::string& p) {
-  std::string out;
-  size_t i = 0;
-  if (p.compare(0, 4, "(?i)") == 0) i = 4;
-  bool cls = false;   // inside [...]
-  for (; i < p.size(); i++) {
-    const char c = p[i];
-    if (c == '\\' && i + 1 < p.size()) {
-      const char n = p[i + 1];
-      if (!cls && n == 'A') out += '^';
-      else if (!cls && n == 'z') out += '$';
-      else { out += c; out += n; }
-      i++;
-      continue;
-    }
-    if (cls) {
-      if (c == ']') cls = false;
-      out += c;
-      continue;
-    }
-    if (c == '[') {
-      cls = true;
-      out += c;
-      if (i + 1 < p.size() && p[i + 1] == '^') out += p[++i];
-      if (i + 1 < p.size() && p[i + 1] == ']') {   // RE2: a leading ']' is a literal; ECMAScript: escape it
-        out += "\\]";
-        i++;
-      }
-      continue;
-    }
-    if (c == '(' && p.compare(i, 4, "(?P<") == 0) {
-      const size_t e = p.find('>', i + 4);
-      if (e != std::string::npos) {
-        out += '(';
-        i = e;
-        continue;
-      }
-    }
-    out += c;
-  }
-  return out;
-}
-
 // NoisyTagsDropper.DO_NOT_DISPLAY_TAGS / DO_NOT_DISPLAY_TAG_PREFIXES (core/.../utils/NoisyTagsDropper.scala)
 bool noisy_tag(const std::string& t) {
   static const char* const names[] = {
@@ -254,6 +222,11 @@ bool noisy_tag(const std::string& t) {
 int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
              unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
   auto t_start = std::chrono::steady_clock::now();
+  // Distributed calls issue collectives: one at a time per engine, in the same order on every rank.  Every call
+  // runs on its own context (stream, workspaces), so local calls from several threads overlap.
+  std::unique_lock<std::mutex> comm_lock;
+  if (dist) comm_lock = std::unique_lock<std::mutex>(E.comm_mu);
+  CtxLease X(E);
   Request R = parse_request(json);
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
   if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
@@ -355,8 +328,25 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   if (dist)
     for (size_t i = 0; i < n_paths; i++) mine[i] = (shard ? shard[i] : int32_t(i % size_t(world))) == rank;
   std::vector<std::shared_ptr<Segment>> segs(n_paths);
-  for (size_t i = 0; i < n_paths; i++)
-    if (mine[i]) segs[i] = E.get_segment(paths[i], true);
+  {
+    // A rank-local failure (I/O, Parquet, HBM) must not leave the other ranks waiting in the next collective:
+    // the ranks agree on a status first and fail together.
+    int err = 0;
+    std::string msg;
+    try {
+      for (size_t i = 0; i < n_paths; i++)
+        if (mine[i]) segs[i] = E.get_segment(paths[i], true);
+    } catch (const PlanError& e) {
+      if (!dist) throw;
+      err = e.code;
+      msg = e.what();
+    } catch (const std::exception& e) {
+      if (!dist) throw;
+      err = LK_ERR_IO;
+      msg = e.what();
+    }
+    if (dist) comm_agree(E, *X, err, msg);
+  }
 
   // ---- globs ----
   const std::set<std::string> fset = field_set(R);
@@ -383,7 +373,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
       if (vc < 0 || segs[si]->cols[vc].any_nulls) exists.back() = 1;
     }
-  if (dist) comm_allreduce_max_u8(E, exists.data(), exists.size());   // every rank sees every glob's union
+  if (dist) comm_allreduce_max_u8(E, *X, exists.data(), exists.size());   // every rank sees every glob's union
   const bool value_nulls = exists.back() != 0;
   auto glob_has = [&](size_t gi, const std::string& c) {
     size_t k = size_t(std::find(probe_cols.begin(), probe_cols.end(), c) - probe_cols.begin());
@@ -452,7 +442,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
                  sc.order = E.dict_order(sc.name, sc.dict_n);
                  uint64_t key[3] = {uint64_t(sc.order->n), sc.order->fp[0], sc.order->fp[1]};
                  const std::string mine(reinterpret_cast<const char*>(key), sizeof(key));
-                 for (const std::string& b : comm_allgather_bytes(E, mine))
+                 for (const std::string& b : comm_allgather_bytes(E, *X, mine))
                    if (b != mine) return false;
                  return true;
                }()) {
@@ -469,7 +459,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
         std::lock_guard<std::mutex> g(gd.mu);
         mine = pack_strings(gd.vals, sc.dict_n);
       }
-      for (const std::string& blob : comm_allgather_bytes(E, mine)) unpack_strings(blob, sc.uvals);
+      for (const std::string& blob : comm_allgather_bytes(E, *X, mine)) unpack_strings(blob, sc.uvals);
       std::sort(sc.uvals.begin(), sc.uvals.end());
       sc.uvals.erase(std::unique(sc.uvals.begin(), sc.uvals.end()), sc.uvals.end());
       if (sc.uvals.size() + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
@@ -491,7 +481,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     if (!strs[s].is_dim) continue;
     strs[s].stride = ngroups;
     ngroups *= strs[s].ndim;
-    if (ngroups > (1ull << 40)) throw PlanError(LK_ERR_UNSUPPORTED, "group space too large");
+    if (ngroups > 0xffffffffull) throw PlanError(LK_ERR_UNSUPPORTED, "group space beyond 2^32 groups");
   }
 
   // ---- lookup tables: global id -> leaf bits << 24 | dim id ----
@@ -500,30 +490,52 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   for (size_t s = 0; s < strs.size(); s++) {
     StrCol& sc = strs[s];
     GlobalDict& gd = E.dict(sc.name);
-    std::lock_guard<std::mutex> g(gd.mu);
-    bool null_like_present = gd.ids.count("null") || gd.ids.count("");
+    bool null_like_present;
+    {
+      std::lock_guard<std::mutex> g(gd.mu);
+      null_like_present = gd.ids.count("null") || gd.ids.count("");
+    }
     need_tab[s] = !sc.leaves.empty() || sc.restricted || sc.exchanged ||
                   (sc.is_dim && collapse_in_table && null_like_present) || (!sc.is_dim && sc.leaves.empty());
     if (!need_tab[s]) continue;
-    std::vector<std::regex> res(sc.leaves.size());
-    for (size_t j = 0; j < sc.leaves.size(); j++) {
-      const FilterNode* l = sc.leaves[j];
-      if (l->op == "regex" || l->op == "contains") {
-        std::string pat = re2_to_ecmascript(l->op == "contains" ? ".*" + l->v[0] + ".*" : l->v[0]);
-        try {
-          res[j] = std::regex(pat, std::regex::ECMAScript | std::regex::icase | std::regex::optimize);
-        } catch (const std::regex_error& e) {
-          throw PlanError(LK_ERR_UNSUPPORTED, "regex '" + pat + "': " + e.what());
+    // Leaf outcomes over the column's dictionary (values [0, dict_n) are immutable: StableStrs), cached per
+    // (column, leaves) and extended only over values added since: a regex runs once per distinct value.
+    std::shared_ptr<LeafBits> lb;
+    std::unique_lock<std::mutex> lb_guard;
+    if (!sc.leaves.empty()) {
+      std::string key = sc.name;
+      for (const FilterNode* l : sc.leaves) {
+        key += '\x1f';
+        key += l->op;
+        for (auto& v : l->v) {
+          key += '\x1e';
+          key += v;
         }
+      }
+      std::vector<std::unique_ptr<re::Regex>> res(sc.leaves.size());
+      std::vector<std::unique_ptr<std::unordered_set<std::string>>> sets(sc.leaves.size());
+      for (size_t j = 0; j < sc.leaves.size(); j++) {
+        const FilterNode* l = sc.leaves[j];
+        if (l->op == "regex" || l->op == "contains") res[j] = std::make_unique<re::Regex>(compile_leaf_regex(*l));
+        if ((l->op == "in" || l->op == "not_in") && l->v.size() > 8)
+          sets[j] = std::make_unique<std::unordered_set<std::string>>(l->v.begin(), l->v.end());
+      }
+      lb = E.leaf_bits(key);
+      lb_guard = std::unique_lock<std::mutex>(lb->mu);
+      lb->hit.reserve(sc.dict_n);
+      for (uint32_t gid = uint32_t(lb->hit.size()); gid < sc.dict_n; gid++) {
+        const std::string& v = gd.vals[gid];
+        uint8_t bits = 0;
+        for (size_t j = 0; j < sc.leaves.size(); j++)
+          if (leaf_eval(*sc.leaves[j], v, res[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
+        lb->hit.push_back(bits);
       }
     }
     auto& tab = tabs[s];
     tab.resize(std::max<uint32_t>(sc.dict_n, 1));
     for (uint32_t gid = 0; gid < sc.dict_n; gid++) {
       const std::string& v = gd.vals[gid];
-      uint32_t bits = 0;
-      for (size_t j = 0; j < sc.leaves.size(); j++)
-        if (leaf_eval(*sc.leaves[j], v, &res[j])) bits |= 1u << j;
+      const uint32_t bits = lb ? lb->hit[gid] : 0u;
       uint32_t dim = 0;
       if (sc.is_dim) {
         if (sc.restricted) {
@@ -575,14 +587,18 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     }
   }
   const uint32_t nslots = per_glob_cells ? uint32_t(globs.size()) : 1u;
+  if (nbuckets && (double(nslots) * double(nbuckets) * double(ngroups) > 9.0e18))
+    throw PlanError(LK_ERR_UNSUPPORTED, "cell key space beyond 64 bits");
   const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
-  if (ncells > (1ull << 28)) throw PlanError(LK_ERR_UNSUPPORTED, "aggregation table too large (" + std::to_string(ncells) + " cells)");
 
   // ---- per-segment query descriptors ----
   std::vector<QSeg> qsegs;
   std::vector<uint32_t> seg_begin;
   uint32_t total_tiles = 0;
   uint64_t rows_scanned = 0, alg_bytes = 0;
+  int local_err = 0;          // distributed: a rank-local failure, agreed on with the other ranks after the scan
+  std::string local_msg;
+  try {
   for (size_t gi = 0; gi < globs.size() && nbuckets; gi++) {
     const GlobInfo& g = globs[gi];
     if (g.skip) continue;
@@ -625,6 +641,14 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   }
 
   if (seg_begin.size() > 65535) throw PlanError(LK_ERR_UNSUPPORTED, "more than 65535 segments in one evaluation");
+  if (total_tiles >= (1u << 31)) throw PlanError(LK_ERR_UNSUPPORTED, "too many tiles");
+  } catch (const PlanError& e) {
+    if (!dist) throw;
+    local_err = e.code;
+    local_msg = e.what();
+    qsegs.clear();
+    total_tiles = 0;
+  }
   uint32_t max_tiles = 0;
   for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
   // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
@@ -686,13 +710,29 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
         if (int(sidx) != early) late_mask |= 1u << sidx;
     }
   }
-  if (total_tiles >= (1u << 31)) throw PlanError(LK_ERR_UNSUPPORTED, "too many tiles");
+  // ---- table mode ----
+  // Dense: array index = cell key = (glob slot, bucket, group).  Hash (SURVEY §2.2 K4 spill, high cardinality):
+  // an open-addressing table keyed by the cell key, first sized from a bound on the distinct cells and grown
+  // (the scan re-run) when the bound was optimistic.  Every passing row lands in one cell, so the distinct cells
+  // never exceed the rows scanned.
+  const uint64_t dense_max = getenv("LK_DENSE_MAX_CELLS") ? uint64_t(atoll(getenv("LK_DENSE_MAX_CELLS")))
+                                                          : (uint64_t(1) << 26);
+  const bool hash_mode = ncells > dense_max;
+  auto pow2 = [](uint64_t x) {
+    uint64_t p = 1;
+    while (p < x) p <<= 1;
+    return p;
+  };
+  const uint64_t hash_bound = std::max<uint64_t>(1, std::min<uint64_t>(ncells, rows_scanned));
+  const uint64_t cap_max = std::max<uint64_t>(pow2(2 * hash_bound), 1 << 16);
+  uint64_t cap = hash_mode ? std::min<uint64_t>(cap_max, std::max<uint64_t>(1 << 16, std::min<uint64_t>(pow2(2 * hash_bound), 1 << 25))) : 0;
+  if (hash_mode && getenv("LK_HASH_INIT_SLOTS"))   // tests only: a deliberately small first table (regrowth path)
+    cap = std::min<uint64_t>(cap_max, pow2(std::max<uint64_t>(64, uint64_t(atoll(getenv("LK_HASH_INIT_SLOTS"))))));
 
   // ---- device: upload, zero table, scan ----
   const double plan_ms = ms_since(t_start);
-  std::lock_guard<std::mutex> dev_guard(E.dev_mu);
   HIP_TRY(hipSetDevice(E.device));
-  hipStream_t st = E.stream;
+  hipStream_t st = X->stream;
   QParams P{};
   P.nsegs = uint32_t(qsegs.size());
   P.total_tiles = total_tiles;
@@ -754,9 +794,19 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     for (uint32_t r = 0; r < order.size(); r++) name_rank[order[r].second] = r;
   }
   const size_t o_rank = reserve(name_rank.size() * 4);
+  // null-like group values folded after per-glob aggregation (merged min/max over NULL-able values)
+  std::vector<uint32_t> flat;
+  std::vector<size_t> map_off(strs.size(), SIZE_MAX);
+  if (rekey)
+    for (size_t s = 0; s < strs.size(); s++)
+      if (!fold_maps[s].empty()) {
+        map_off[s] = flat.size();
+        flat.insert(flat.end(), fold_maps[s].begin(), fold_maps[s].end());
+      }
+  const size_t o_maps = reserve(flat.size() * 4);
   const size_t stage_bytes = off;
-  uint8_t* hbuf = static_cast<uint8_t*>(E.pinned_buf(stage_bytes));
-  uint8_t* dbuf = static_cast<uint8_t*>(E.workspace("query", stage_bytes));
+  uint8_t* hbuf = static_cast<uint8_t*>(X->pinned_buf(stage_bytes));
+  uint8_t* dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
   if (late_mask) {
@@ -771,6 +821,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   memcpy(hbuf + o_strp, strp.data(), strp.size() * sizeof(StrParam));
   memset(hbuf + o_flags, 0, 16);
   if (!name_rank.empty()) memcpy(hbuf + o_rank, name_rank.data(), name_rank.size() * 4);
+  if (!flat.empty()) memcpy(hbuf + o_maps, flat.data(), flat.size() * 4);
   HIP_TRY(hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st));
   P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
   P.flags = reinterpret_cast<uint32_t*>(dbuf + o_flags);
@@ -779,157 +830,266 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   P.truth_early = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_e) : nullptr;
   P.truth_late = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_l) : nullptr;
   P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
-
-  // aggregation table (SoA)
-  const size_t nc = size_t(std::max<uint64_t>(ncells, 1));
-  uint8_t* tb = static_cast<uint8_t*>(E.workspace("table", nc * 8 * 5 + 4 * 256));
-  P.rows = reinterpret_cast<unsigned long long*>(tb);
-  P.cnt = reinterpret_cast<unsigned long long*>(tb + nc * 8);
-  P.hi = reinterpret_cast<double*>(tb + nc * 16);
-  P.lo = reinterpret_cast<double*>(tb + nc * 24);
-  P.ext = reinterpret_cast<unsigned long long*>(tb + nc * 32);
+  const uint32_t* d_maps = reinterpret_cast<const uint32_t*>(dbuf + o_maps);
   const int kagg = agg == AGG_AVG ? AGG_SUM : (agg == AGG_ROWS ? AGG_COUNT : agg);
-  HIP_TRY(hipMemsetAsync(tb, 0, nc * 16, st));
-  if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + nc * 16, 0, nc * 16, st));
-  if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, nc * 8, st));
-  if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, nc * 8, st));
-  HIP_TRY(hipEventRecord(E.ev_scan0, st));
-  const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
-  if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
-    P.stamps = static_cast<unsigned long long*>(E.workspace("stamps", nstamp * 8));
-    HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
-  }
-  const double launch_ms = ms_since(t_start);   // host staging done, scan enqueued
-  if (ncells) HIP_TRY(launch_scan(P, kagg, st));
-  if (P.stamps) {
-    std::vector<unsigned long long> h(nstamp);
-    HIP_TRY(hipMemcpyAsync(h.data(), P.stamps, nstamp * 8, hipMemcpyDeviceToHost, st));
+
+  // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
+  size_t nc = 0;
+  double launch_ms = 0;
+  auto zero_table = [&](size_t ncl, bool hashed) {
+    uint8_t* tb = static_cast<uint8_t*>(X->workspace("table", ncl * 8 * (hashed ? 6 : 5) + 4 * 256));
+    P.rows = reinterpret_cast<unsigned long long*>(tb);
+    P.cnt = reinterpret_cast<unsigned long long*>(tb + ncl * 8);
+    P.hi = reinterpret_cast<double*>(tb + ncl * 16);
+    P.lo = reinterpret_cast<double*>(tb + ncl * 24);
+    P.ext = reinterpret_cast<unsigned long long*>(tb + ncl * 32);
+    P.hkeys = hashed ? reinterpret_cast<unsigned long long*>(tb + ncl * 40) : nullptr;
+    P.hmask = hashed ? ncl - 1 : 0;
+    HIP_TRY(hipMemsetAsync(tb, 0, ncl * 16, st));
+    if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + ncl * 16, 0, ncl * 16, st));
+    if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, ncl * 8, st));
+    if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, ncl * 8, st));
+    if (hashed) HIP_TRY(hipMemsetAsync(P.hkeys, 0xff, ncl * 8, st));
+  };
+  auto run_scan = [&]() -> uint32_t {
+    nc = hash_mode ? size_t(cap) : size_t(std::max<uint64_t>(ncells, 1));
+    zero_table(nc, hash_mode);
+    HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));
+    HIP_TRY(hipEventRecord(X->ev_scan0, st));
+    const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
+    if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
+      P.stamps = static_cast<unsigned long long*>(X->workspace("stamps", nstamp * 8));
+      HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
+    }
+    launch_ms = ms_since(t_start);   // host staging done, scan enqueued
+    if (ncells) HIP_TRY(launch_scan(P, kagg, st));
+    HIP_TRY(hipEventRecord(X->ev_scan1, st));
+    if (P.stamps) {
+      std::vector<unsigned long long> h(nstamp);
+      HIP_TRY(hipMemcpyAsync(h.data(), P.stamps, nstamp * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      static const char* names[LK_NSTAMP] = {"prologue", "defs", "decode", "fold", "filter", "compact", "prefetch", "stream"};
+      double sm[LK_NSTAMP] = {};
+      size_t n = 0;
+      for (size_t i = 0; i < nstamp; i += LK_NSTAMP) {
+        if (!(h[i] >> 63)) continue;   // block exited early (zone map / past the segment's tiles)
+        h[i] &= ~(1ull << 63);
+        for (int k = 0; k < LK_NSTAMP; k++) sm[k] += double(h[i + k]);
+        n++;
+      }
+      if (n) {
+        double tot = 0;
+        std::string line;
+        for (int k = 0; k < LK_NSTAMP; k++) {
+          tot += sm[k] / n;
+          line += std::string(" ") + names[k] + "=" + std::to_string(long(sm[k] / n));
+        }
+        fprintf(stderr, "[lk stamps] blocks=%zu mean cycles:%s total=%.0f\n", n, line.c_str(), tot);
+      }
+    }
+    uint32_t fl = 0;
+    HIP_TRY(hipMemcpyAsync(&fl, P.flags, 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    static const char* names[LK_NSTAMP] = {"prologue", "defs", "decode", "fold", "filter", "compact", "prefetch", "stream"};
-    double s[LK_NSTAMP] = {};
-    size_t n = 0;
-    for (size_t i = 0; i < nstamp; i += LK_NSTAMP) {
-      if (!(h[i] >> 63)) continue;   // block exited early (zone map / past the segment's tiles)
-      h[i] &= ~(1ull << 63);
-      for (int k = 0; k < LK_NSTAMP; k++) s[k] += double(h[i + k]);
-      n++;
+    return fl;
+  };
+  // Every rank reports (error, flags); a failure anywhere fails every rank (no rank is left in a collective),
+  // and every rank sees the OR of the flags (so they re-run a too-small hash table together).
+  auto agree = [&](int err, const std::string& msg, uint32_t fl) -> uint32_t {
+    if (!dist) {
+      if (err) throw PlanError(err, msg);
+      return fl;
     }
-    if (n) {
-      double tot = 0;
-      std::string line;
-      for (int k = 0; k < LK_NSTAMP; k++) {
-        tot += s[k] / n;
-        line += std::string(" ") + names[k] + "=" + std::to_string(long(s[k] / n));
-      }
-      fprintf(stderr, "[lk stamps] blocks=%zu mean cycles:%s total=%.0f\n", n, line.c_str(), tot);
+    std::string mine(8, '\0');
+    memcpy(&mine[0], &err, 4);
+    memcpy(&mine[4], &fl, 4);
+    mine += msg;
+    uint32_t all_fl = 0;
+    const std::vector<std::string> all = comm_allgather_bytes(E, *X, mine);
+    for (size_t r = 0; r < all.size(); r++) {
+      int e;
+      uint32_t f;
+      memcpy(&e, all[r].data(), 4);
+      memcpy(&f, all[r].data() + 4, 4);
+      if (e) throw PlanError(e, (int(r) == rank ? std::string() : "rank " + std::to_string(r) + ": ") + all[r].substr(8));
+      all_fl |= f;
     }
-  }
-  HIP_TRY(hipEventRecord(E.ev_scan1, st));
-
-  // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
-  if (dist) comm_reduce_table(E, P, kagg, nc);
-  const bool emit = !dist || rank == 0;
-
-  // ---- merged min/max with NULL-able values: fold null-like group values per glob-cell SQL value ----
-  FParams F{};
-  F.rows = P.rows;
-  F.cnt = P.cnt;
-  F.hi = P.hi;
-  F.lo = P.lo;
-  F.ext = P.ext;
-  uint32_t fslots = nslots;
-  if (rekey && emit && ncells) {
-    const size_t n2 = size_t(nbuckets * ngroups);
-    uint8_t* t2 = static_cast<uint8_t*>(E.workspace("table2", n2 * 24 + 256));
-    RParams RP{};
-    RP.in_rows = P.rows;
-    RP.in_cnt = P.cnt;
-    RP.in_ext = P.ext;
-    RP.ncells_in = ncells;
-    RP.out_rows = reinterpret_cast<unsigned long long*>(t2);
-    RP.out_cnt = reinterpret_cast<unsigned long long*>(t2 + n2 * 8);
-    RP.out_ext = reinterpret_cast<unsigned long long*>(t2 + n2 * 16);
-    RP.nbuckets = nbuckets;
-    RP.ngroups = ngroups;
-    RP.agg = kagg;
-    std::vector<uint32_t> flat;
-    std::vector<size_t> map_off(strs.size(), SIZE_MAX);
-    for (size_t s = 0; s < strs.size(); s++)
-      if (!fold_maps[s].empty()) {
-        map_off[s] = flat.size();
-        flat.insert(flat.end(), fold_maps[s].begin(), fold_maps[s].end());
-      }
-    uint32_t* dmaps = static_cast<uint32_t*>(E.workspace("foldmaps", flat.size() * 4 + 16));
-    HIP_TRY(hipMemcpyAsync(dmaps, flat.data(), flat.size() * 4, hipMemcpyHostToDevice, st));
-    for (size_t s = 0; s < strs.size(); s++) {
-      if (!strs[s].is_dim) continue;
-      RP.stride[RP.ndims] = strs[s].stride;
-      RP.ndim[RP.ndims] = strs[s].ndim;
-      RP.map[RP.ndims] = map_off[s] == SIZE_MAX ? nullptr : dmaps + map_off[s];
-      RP.ndims++;
-    }
-    HIP_TRY(hipMemsetAsync(t2, 0, n2 * 16, st));
-    HIP_TRY(hipMemsetAsync(RP.out_ext, kagg == AGG_MIN ? 0xff : 0, n2 * 8, st));
-    HIP_TRY(launch_rekey_minmax(RP, st));
-    HIP_TRY(hipStreamSynchronize(st));   // flat / maps staging is host memory owned by this frame
-    F.rows = RP.out_rows;
-    F.cnt = RP.out_cnt;
-    F.ext = RP.out_ext;
-    fslots = 1;
-  }
-
-  // ---- finalize + compaction ----
-  F.ngroups = ngroups;
-  F.nbuckets = nbuckets;
-  F.nglob_slots = fslots;
-  F.agg = agg;
-  F.per_glob = per_glob_rows ? 1 : 0;
-  F.collapse = collapse ? 1 : 0;
-  F.name_stride = strs[0].stride ? strs[0].stride : 1;
-  F.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
-  F.bucket_base = bucket_base;
-  F.step = P.step;
-  F.nkeys = ncells == 0 ? 0 : (per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups));
-  uint32_t nfb = finalize_blocks(F.nkeys);
-  const size_t nk = size_t(std::max<uint64_t>(F.nkeys, 1));
-  uint8_t* ob = static_cast<uint8_t*>(E.workspace("out", nk * (8 + 8 + 8 + 4) + (nfb + 1) * 4 + 1024));
-  int64_t* d_ts = reinterpret_cast<int64_t*>(ob);
-  double* d_val = reinterpret_cast<double*>(ob + nk * 8);
-  unsigned long long* d_gid = reinterpret_cast<unsigned long long*>(ob + nk * 16);
-  uint32_t* d_glob = reinterpret_cast<uint32_t*>(ob + nk * 24);
-  uint32_t* d_counts = reinterpret_cast<uint32_t*>(ob + nk * 28);
-  uint32_t nrows_out = 0;
+    return all_fl;
+  };
   uint32_t hflags = 0;
-  if (emit && F.nkeys) {
-    HIP_TRY(launch_finalize_count(F, d_counts, st));
-    HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
+  int attempts = 0;
+  for (;;) {
+    attempts++;
+    int err = local_err;
+    std::string msg = local_msg;
+    uint32_t fl = 0;
+    if (!err) {
+      try {
+        fl = run_scan();
+      } catch (const PlanError& e) {
+        if (!dist) throw;
+        err = e.code;
+        msg = e.what();
+      }
+    }
+    hflags = agree(err, msg, fl);
+    if (hash_mode && (hflags & FLAG_HASH_FULL) && cap < cap_max) {
+      cap = std::min<uint64_t>(cap_max, cap * 4);
+      continue;
+    }
+    break;
   }
-  HIP_TRY(hipMemcpyAsync(&hflags, P.flags, 4, hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
   if (hflags & FLAG_METRICS_UNALIGNED)
     throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
+  if (hflags & FLAG_HASH_FULL) throw PlanError(LK_ERR_MEMORY, "aggregation hash table full at its bound");
+
+  // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
+  if (dist) {
+    if (hash_mode) {
+      unsigned long long cap0 = cap;
+      comm_reduce_hash(E, *X, P, kagg, cap0);
+      cap = cap0;
+      nc = size_t(cap);
+    } else {
+      comm_reduce_table(E, *X, P, kagg, nc);
+    }
+  }
+  const bool emit = !dist || rank == 0;
+
+  uint32_t nrows_out = 0;
+  FParams F{};
+  SParams S{};
+  uint32_t nfb = 0;
+  uint32_t* d_counts = nullptr;
+  void* sws = nullptr;
+  unsigned long long nocc = 0;
+  if (!hash_mode) {
+    // ---- merged min/max with NULL-able values: fold null-like group values per glob-cell SQL value ----
+    F.rows = P.rows;
+    F.cnt = P.cnt;
+    F.hi = P.hi;
+    F.lo = P.lo;
+    F.ext = P.ext;
+    uint32_t fslots = nslots;
+    if (rekey && emit && ncells) {
+      const size_t n2 = size_t(nbuckets * ngroups);
+      uint8_t* t2 = static_cast<uint8_t*>(X->workspace("table2", n2 * 24 + 256));
+      RParams RP{};
+      RP.in_rows = P.rows;
+      RP.in_cnt = P.cnt;
+      RP.in_ext = P.ext;
+      RP.ncells_in = ncells;
+      RP.out_rows = reinterpret_cast<unsigned long long*>(t2);
+      RP.out_cnt = reinterpret_cast<unsigned long long*>(t2 + n2 * 8);
+      RP.out_ext = reinterpret_cast<unsigned long long*>(t2 + n2 * 16);
+      RP.nbuckets = nbuckets;
+      RP.ngroups = ngroups;
+      RP.agg = kagg;
+      for (size_t s = 0; s < strs.size(); s++) {
+        if (!strs[s].is_dim) continue;
+        RP.stride[RP.ndims] = strs[s].stride;
+        RP.ndim[RP.ndims] = strs[s].ndim;
+        RP.map[RP.ndims] = map_off[s] == SIZE_MAX ? nullptr : d_maps + map_off[s];
+        RP.ndims++;
+      }
+      HIP_TRY(hipMemsetAsync(t2, 0, n2 * 16, st));
+      HIP_TRY(hipMemsetAsync(RP.out_ext, kagg == AGG_MIN ? 0xff : 0, n2 * 8, st));
+      HIP_TRY(launch_rekey_minmax(RP, st));
+      F.rows = RP.out_rows;
+      F.cnt = RP.out_cnt;
+      F.ext = RP.out_ext;
+      fslots = 1;
+    }
+
+    // ---- finalize + compaction ----
+    F.ngroups = ngroups;
+    F.nbuckets = nbuckets;
+    F.nglob_slots = fslots;
+    F.agg = agg;
+    F.per_glob = per_glob_rows ? 1 : 0;
+    F.collapse = collapse ? 1 : 0;
+    F.name_stride = strs[0].stride ? strs[0].stride : 1;
+    F.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
+    F.bucket_base = bucket_base;
+    F.step = P.step;
+    F.nkeys = ncells == 0 ? 0 : (per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups));
+    nfb = finalize_blocks(F.nkeys);
+    d_counts = static_cast<uint32_t*>(X->workspace("counts", (size_t(nfb) + 2) * 4));
+    if (emit && F.nkeys) {
+      HIP_TRY(launch_finalize_count(F, d_counts, st));
+      HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
+    }
+  } else if (emit) {
+    // ---- sparse finalize: occupied slots -> (output key, slot) -> radix sort -> one row per output key ----
+    S.keys = P.hkeys;
+    S.rows = P.rows;
+    S.cnt = P.cnt;
+    S.hi = P.hi;
+    S.lo = P.lo;
+    S.ext = P.ext;
+    S.cap = cap;
+    S.ngroups = ngroups;
+    S.nbuckets = nbuckets;
+    S.nslots = nslots;
+    S.agg = agg;
+    S.per_glob = per_glob_rows ? 1 : 0;
+    S.collapse = collapse ? 1 : 0;
+    S.rekey = rekey ? 1 : 0;
+    for (size_t s = 0; s < strs.size() && rekey; s++) {
+      if (!strs[s].is_dim) continue;
+      S.stride[S.ndims] = strs[s].stride;
+      S.ndim[S.ndims] = strs[s].ndim;
+      S.map[S.ndims] = map_off[s] == SIZE_MAX ? nullptr : d_maps + map_off[s];
+      S.ndims++;
+    }
+    S.name_stride = strs[0].stride ? strs[0].stride : 1;
+    S.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
+    S.bucket_base = bucket_base;
+    S.step = P.step;
+    const uint32_t nsb = sparse_blocks(cap);
+    uint32_t* occ = static_cast<uint32_t*>(X->workspace("occ_counts", (size_t(nsb) + 2) * 4));
+    HIP_TRY(launch_sparse_count(S, occ, st));
+    uint32_t n32 = 0;
+    HIP_TRY(hipMemcpyAsync(&n32, occ + nsb, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    nocc = n32;
+    const unsigned long long max_key =
+        per_glob_rows ? nbuckets * nslots * ngroups : (collapse ? nbuckets : nbuckets * ngroups);
+    int end_bit = 1;
+    while (end_bit < 64 && (1ull << end_bit) < max_key) end_bit++;
+    sws = X->workspace("sparse", sparse_workspace_bytes(nocc, end_bit));
+    uint32_t* d_nrows = nullptr;
+    HIP_TRY(launch_sparse_sort(S, occ, nocc, end_bit, sws, &d_nrows, st));
+    HIP_TRY(hipMemcpyAsync(&nrows_out, d_nrows, 4, hipMemcpyDeviceToHost, st));
+  }
+  HIP_TRY(hipStreamSynchronize(st));
+  const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
   res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
   if (nrows_out) {
-    if (res->blk.pinned) {
-      // Rows written by the kernel straight into the mapped pinned result block: no device->host copies (small
-      // async D2H copies cost ~1 ms of completion latency each call on this stack, measured in bench C4).
-      HIP_TRY(launch_finalize_write(F, d_counts, res->ts, res->val, res->gid, per_glob_rows ? res->glob : nullptr, st));
-    } else {
-      HIP_TRY(launch_finalize_write(F, d_counts, d_ts, d_val, d_gid, d_glob, st));
-      HIP_TRY(hipMemcpyAsync(res->ts, d_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(res->val, d_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(res->gid, d_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-      if (per_glob_rows) HIP_TRY(hipMemcpyAsync(res->glob, d_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    // Rows written by the kernel straight into the mapped pinned result block when it is pinned: no device->host
+    // copies (small async D2H copies cost ~1 ms of completion latency each call on this stack, measured in C4).
+    const bool direct = res->blk.pinned;
+    const size_t nk = direct ? 1 : nrows_out;
+    uint8_t* ob = static_cast<uint8_t*>(X->workspace("out", nk * (8 + 8 + 8 + 4) + 1024));
+    int64_t* o_ts = direct ? res->ts : reinterpret_cast<int64_t*>(ob);
+    double* o_val = direct ? res->val : reinterpret_cast<double*>(ob + nk * 8);
+    unsigned long long* o_gid = direct ? res->gid : reinterpret_cast<unsigned long long*>(ob + nk * 16);
+    uint32_t* o_glob = per_glob_rows ? (direct ? res->glob : reinterpret_cast<uint32_t*>(ob + nk * 24)) : nullptr;
+    if (hash_mode) HIP_TRY(launch_sparse_write(S, nocc, sws, o_ts, o_val, o_gid, o_glob, st));
+    else HIP_TRY(launch_finalize_write(F, d_counts, o_ts, o_val, o_gid, o_glob, st));
+    if (!direct) {
+      HIP_TRY(hipMemcpyAsync(res->ts, o_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->val, o_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->gid, o_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      if (per_glob_rows) HIP_TRY(hipMemcpyAsync(res->glob, o_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));
   }
   const double copy_ms = ms_since(t_start);
   const double device_ms = copy_ms - plan_ms;
   float scan_ms = 0;
-  HIP_TRY(hipEventElapsedTime(&scan_ms, E.ev_scan0, E.ev_scan1));
+  if (!local_err && ncells) HIP_TRY(hipEventElapsedTime(&scan_ms, X->ev_scan0, X->ev_scan1));
 
   // ---- tags: "name", groupBys (as written), then queryTags keys (rows whose own tags are all absent) ----
   std::vector<int> col_str;   // tag column -> string column index
@@ -1002,13 +1162,15 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
       res->owned.push_back(kv.second);
       res->qt_of_glob[gi].emplace_back(c, res->owned.back().c_str());
     }
-  char buf[512];
+  char buf[768];
   snprintf(buf, sizeof(buf),
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
-           "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu}",
+           "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"table\":\"%s\","
+           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d}",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
-           (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size());
+           (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size(),
+           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts);
   res->stats = buf;
   return LK_OK;
 }

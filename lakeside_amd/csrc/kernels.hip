@@ -25,6 +25,8 @@
 #include "layout.hpp"
 #include "scan_kernel.hpp"
 
+#include <hipcub/device/device_radix_sort.hpp>
+
 namespace lk {
 
 // ------------------------------------------------------------------------------------------------
@@ -53,13 +55,15 @@ __device__ __forceinline__ double cell_value(const FParams& F, unsigned long lon
 // when the name dimension collapses (no groupBys).
 __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   OutRow o{false, 0.0, 0, 0};
-  if (F.per_glob) {
-    unsigned long long cell = key;
+  if (F.per_glob) {   // key = (bucket, glob, group): rows ascending in time, ties by glob (Commons.scala:391-392)
+    const unsigned long long g = key % F.ngroups, t = key / F.ngroups;
+    const unsigned long long gs = t % F.nglob_slots, b = t / F.nglob_slots;
+    const unsigned long long cell = (gs * F.nbuckets + b) * F.ngroups + g;
     if (F.rows[cell] == 0) return o;
     o.exists = true;
     o.value = cell_value(F, cell);
-    o.gid = cell % F.ngroups;
-    o.glob = uint32_t(cell / (F.ngroups * F.nbuckets));
+    o.gid = g;
+    o.glob = uint32_t(gs);
     return o;
   }
   const unsigned long long b = F.collapse ? key : key / F.ngroups;
@@ -171,7 +175,7 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
     }
     if (r.exists) {
       uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
-      unsigned long long b = F.per_glob ? (key / F.ngroups) % F.nbuckets : (F.collapse ? key : key / F.ngroups);
+      unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
       out_ts[pos] = F.bucket_base + (int64_t)b * F.step;
       out_val[pos] = r.value;
       out_gid[pos] = r.gid;
@@ -239,6 +243,224 @@ __global__ __launch_bounds__(256) void rekey_minmax(RParams R) {
   else atomicMax(&R.out_ext[o], v);
 }
 
+
+// ------------------------------------------------------------------------------------------------
+// Hash mode: record exchange (multi-GPU) and sparse finalize
+// ------------------------------------------------------------------------------------------------
+constexpr int SB = 256;
+constexpr int SITEMS = 8;
+
+__device__ __forceinline__ bool slot_live(const SParams& S, unsigned long long i) {
+  return S.keys[i] != EMPTY && S.rows[i] != 0;
+}
+
+__global__ __launch_bounds__(SB) void sparse_count(SParams S, uint32_t* block_counts) {
+  __shared__ uint32_t ws[SB / 64];
+  uint32_t n = 0;
+  const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
+  for (int i = 0; i < SITEMS; i++) {
+    const unsigned long long k = base + (unsigned long long)i * SB + threadIdx.x;
+    if (k < S.cap && slot_live(S, k)) n++;
+  }
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// Output key of a cell key (see SParams): per-glob (bucket, glob, group); merged (bucket, group) with the group
+// folded under the rekey maps, or (bucket) when the name dimension collapses.
+__device__ __forceinline__ unsigned long long out_key(const SParams& S, unsigned long long cell) {
+  const unsigned long long g = cell % S.ngroups, t = cell / S.ngroups;
+  const unsigned long long b = t % S.nbuckets, gs = t / S.nbuckets;
+  if (S.per_glob) return (b * S.nslots + gs) * S.ngroups + g;
+  if (S.collapse) return b;
+  if (!S.rekey) return b * S.ngroups + g;
+  unsigned long long cg = 0;
+  for (int d = 0; d < S.ndims; d++) {
+    unsigned long long v = (g / S.stride[d]) % S.ndim[d];
+    if (S.map[d]) v = S.map[d][v];
+    cg += v * S.stride[d];
+  }
+  return b * S.ngroups + cg;
+}
+
+// Compact (output key, slot) of occupied slots at their block's scanned offset.
+__global__ __launch_bounds__(SB) void sparse_emit(SParams S, const uint32_t* block_offsets, unsigned long long* okey,
+                                                  uint32_t* oslot) {
+  __shared__ uint32_t ws[SB / 64];
+  const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
+  uint32_t off = block_offsets[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = 0; i < SITEMS; i++) {
+    const unsigned long long k = base + (unsigned long long)i * SB + threadIdx.x;
+    const bool live = k < S.cap && slot_live(S, k);
+    const unsigned long long m = __ballot(live);
+    if (lane == 0) ws[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (int w = 0; w < SB / 64; w++) {
+      wb += (w < wave) ? ws[w] : 0;
+      tot += ws[w];
+    }
+    if (live) {
+      const uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
+      okey[pos] = out_key(S, S.keys[k]);
+      oslot[pos] = uint32_t(k);
+    }
+    off += tot;
+    __syncthreads();
+  }
+}
+
+// Run heads of the sorted output keys, counted per block.
+__global__ __launch_bounds__(SB) void runs_count(const unsigned long long* k, unsigned long long n, uint32_t* block_counts) {
+  __shared__ uint32_t ws[SB / 64];
+  uint32_t c = 0;
+  const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
+  for (int i = 0; i < SITEMS; i++) {
+    const unsigned long long j = base + (unsigned long long)i * SB + threadIdx.x;
+    if (j < n && (j == 0 || k[j] != k[j - 1])) c++;
+  }
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_down(c, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) block_counts[blockIdx.x] = ws[0] + ws[1] + ws[2] + ws[3];
+}
+
+// One row per run of equal output keys: the run's cells combined as make_row combines dense cells.
+__global__ __launch_bounds__(SB) void runs_write(SParams S, const unsigned long long* k, const uint32_t* slot,
+                                                 unsigned long long n, const uint32_t* block_offsets, int64_t* out_ts,
+                                                 double* out_val, unsigned long long* out_gid, uint32_t* out_glob) {
+  __shared__ uint32_t ws[SB / 64];
+  const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
+  uint32_t off = block_offsets[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = 0; i < SITEMS; i++) {
+    const unsigned long long j = base + (unsigned long long)i * SB + threadIdx.x;
+    const bool head = j < n && (j == 0 || k[j] != k[j - 1]);
+    const unsigned long long m = __ballot(head);
+    if (lane == 0) ws[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (int w = 0; w < SB / 64; w++) {
+      wb += (w < wave) ? ws[w] : 0;
+      tot += ws[w];
+    }
+    if (head) {
+      const unsigned long long key = k[j];
+      double hi = 0.0, lo = 0.0, ext = 0.0;
+      unsigned long long cnt = 0, nrows = 0, oext = (S.agg == AGG_MIN) ? ~0ull : 0ull, gid = 0;
+      uint32_t best_rank = 0xffffffffu, glob = 0;
+      bool any = false;
+      for (unsigned long long e = j; e < n && k[e] == key; e++) {
+        const uint32_t c = slot[e];
+        const unsigned long long cell = S.keys[c];
+        const unsigned long long g = cell % S.ngroups;
+        const unsigned long long cc = S.cnt[c];
+        if (S.agg == AGG_SUM || S.agg == AGG_AVG) {
+          double s2, e2;
+          two_sum(hi, S.hi[c], s2, e2);
+          hi = s2;
+          lo += e2 + S.lo[c];
+        } else if (S.agg == AGG_MIN || S.agg == AGG_MAX) {
+          if (S.rekey) {   // per-glob SQL value: NULL cell -> 0.0 (Commons.scala:427), exact min/max on order bits
+            const unsigned long long v = cc ? S.ext[c] : dbl_order(0.0);
+            oext = (S.agg == AGG_MIN) ? (v < oext ? v : oext) : (v > oext ? v : oext);
+          } else {
+            const double v = cc ? order_dbl(S.ext[c]) : 0.0;
+            if (!any) ext = v;
+            else ext = (S.agg == AGG_MIN) ? fmin(ext, v) : fmax(ext, v);
+          }
+        }
+        cnt += cc;
+        nrows += S.rows[c];
+        const uint32_t rank = (S.collapse && S.name_rank) ? S.name_rank[g / S.name_stride] : 0u;
+        if (!any || rank < best_rank) {
+          best_rank = rank;
+          gid = S.rekey ? key % S.ngroups : g;
+          glob = uint32_t(cell / S.ngroups / S.nbuckets);
+        }
+        any = true;
+      }
+      double value;
+      if (S.agg == AGG_COUNT) value = double(cnt);
+      else if (S.agg == AGG_ROWS) value = double(nrows);
+      else if (S.agg == AGG_SUM) value = cnt ? hi + lo : 0.0;
+      else if (S.agg == AGG_AVG) value = S.per_glob ? (cnt ? (hi + lo) / double(cnt) : 0.0) : (hi + lo) / double(cnt);
+      else if (S.rekey) value = order_dbl(oext);
+      else value = ext;
+      const unsigned long long b = S.per_glob ? key / S.ngroups / S.nslots : (S.collapse ? key : key / S.ngroups);
+      const uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
+      out_ts[pos] = S.bucket_base + (int64_t)b * S.step;
+      out_val[pos] = value;
+      out_gid[pos] = gid;
+      if (out_glob) out_glob[pos] = S.per_glob ? glob : 0u;
+    }
+    off += tot;
+    __syncthreads();
+  }
+}
+
+// Rank 0: fold records [key | rows | cnt | hi | lo | ext] of another rank's hash table into its own.
+template <int AGG>
+__global__ __launch_bounds__(256) void merge_records(QParams P, const unsigned long long* recs, size_t n) {
+  const size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= n) return;
+  const unsigned long long rows = recs[n + i];
+  if (!rows) return;
+  const unsigned long long slot = hash_slot(P.hkeys, P.hmask, P.flags, recs[i]);
+  if (slot == EMPTY) return;
+  atomicAdd(&P.rows[slot], rows);
+  const unsigned long long cnt = recs[2 * n + i];
+  if (!cnt) return;
+  atomicAdd(&P.cnt[slot], cnt);
+  if (AGG == AGG_SUM) {
+    const double h = __longlong_as_double((long long)recs[3 * n + i]);
+    const double l = __longlong_as_double((long long)recs[4 * n + i]);
+    const double old = atomicAdd(&P.hi[slot], h);
+    double s, e;
+    two_sum(old, h, s, e);
+    atomicAdd(&P.lo[slot], l + e);
+  } else if (AGG == AGG_MIN) {
+    atomicMin(&P.ext[slot], recs[5 * n + i]);
+  } else if (AGG == AGG_MAX) {
+    atomicMax(&P.ext[slot], recs[5 * n + i]);
+  }
+}
+
+// Occupied slots of a hash-mode table -> compact records (offsets from the sparse count + scan).
+__global__ __launch_bounds__(SB) void table_records(SParams S, const uint32_t* block_offsets, unsigned long long* recs,
+                                                    size_t n) {
+  __shared__ uint32_t ws[SB / 64];
+  const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
+  uint32_t off = block_offsets[blockIdx.x];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int i = 0; i < SITEMS; i++) {
+    const unsigned long long k = base + (unsigned long long)i * SB + threadIdx.x;
+    const bool live = k < S.cap && slot_live(S, k);
+    const unsigned long long m = __ballot(live);
+    if (lane == 0) ws[wave] = __popcll(m);
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (int w = 0; w < SB / 64; w++) {
+      wb += (w < wave) ? ws[w] : 0;
+      tot += ws[w];
+    }
+    if (live) {
+      const size_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
+      recs[pos] = S.keys[k];
+      recs[n + pos] = S.rows[k];
+      recs[2 * n + pos] = S.cnt[k];
+      recs[3 * n + pos] = (unsigned long long)__double_as_longlong(S.hi[k]);
+      recs[4 * n + pos] = (unsigned long long)__double_as_longlong(S.lo[k]);
+      recs[5 * n + pos] = S.ext[k];
+    }
+    off += tot;
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Host launchers
 // ------------------------------------------------------------------------------------------------
@@ -252,6 +474,107 @@ hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* part
                               hipStream_t stream) {
   if (nc == 0 || world <= 1) return hipSuccess;
   hipLaunchKernelGGL(merge_tables, dim3(uint32_t((nc + 255) / 256)), dim3(256), 0, stream, T, parts, world, nc, agg);
+  return hipGetLastError();
+}
+
+
+hipError_t launch_merge_records(const QParams& P, const unsigned long long* recs, size_t n, int agg, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const dim3 g(uint32_t((n + 255) / 256)), b(256);
+  switch (agg) {
+    case AGG_SUM: hipLaunchKernelGGL(merge_records<AGG_SUM>, g, b, 0, st, P, recs, n); break;
+    case AGG_MIN: hipLaunchKernelGGL(merge_records<AGG_MIN>, g, b, 0, st, P, recs, n); break;
+    case AGG_MAX: hipLaunchKernelGGL(merge_records<AGG_MAX>, g, b, 0, st, P, recs, n); break;
+    default: hipLaunchKernelGGL(merge_records<AGG_COUNT>, g, b, 0, st, P, recs, n); break;
+  }
+  return hipGetLastError();
+}
+
+uint32_t sparse_blocks(unsigned long long cap) { return uint32_t((cap + SB * SITEMS - 1) / (SB * SITEMS)); }
+
+hipError_t launch_sparse_count(const SParams& S, uint32_t* d_counts, hipStream_t st) {
+  const uint32_t nb = sparse_blocks(S.cap);
+  if (nb == 0) return hipMemsetAsync(d_counts, 0, sizeof(uint32_t), st);
+  hipLaunchKernelGGL(sparse_count, dim3(nb), dim3(SB), 0, st, S, d_counts);
+  hipLaunchKernelGGL(finalize_scan, dim3(1), dim3(1024), 0, st, d_counts, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_table_records(const QParams& P, unsigned long long cap, uint32_t* d_counts, unsigned long long* recs,
+                                size_t n, hipStream_t st) {
+  SParams S{};
+  S.keys = P.hkeys;
+  S.rows = P.rows;
+  S.cnt = P.cnt;
+  S.hi = P.hi;
+  S.lo = P.lo;
+  S.ext = P.ext;
+  S.cap = cap;
+  const uint32_t nb = sparse_blocks(cap);
+  if (nb == 0 || n == 0) return hipSuccess;
+  hipLaunchKernelGGL(table_records, dim3(nb), dim3(SB), 0, st, S, d_counts, recs, n);
+  return hipGetLastError();
+}
+
+// sparse workspace: okey[2n] | oslot[2n] | run counts | sort temp
+namespace {
+struct SparseWs {
+  unsigned long long *k0, *k1;
+  uint32_t *s0, *s1, *counts;
+  void* temp;
+  size_t temp_bytes;
+};
+size_t sort_temp_bytes(unsigned long long n, int end_bit) {
+  size_t t = 0;
+  (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (unsigned long long*)nullptr, (unsigned long long*)nullptr,
+                                           (uint32_t*)nullptr, (uint32_t*)nullptr, int(n), 0, end_bit, hipStream_t(0));
+  return t;
+}
+SparseWs carve(void* ws, unsigned long long n, int end_bit) {
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  uint8_t* p = static_cast<uint8_t*>(ws);
+  SparseWs w;
+  w.k0 = reinterpret_cast<unsigned long long*>(p);
+  p += al(n * 8);
+  w.k1 = reinterpret_cast<unsigned long long*>(p);
+  p += al(n * 8);
+  w.s0 = reinterpret_cast<uint32_t*>(p);
+  p += al(n * 4);
+  w.s1 = reinterpret_cast<uint32_t*>(p);
+  p += al(n * 4);
+  w.counts = reinterpret_cast<uint32_t*>(p);
+  p += al((size_t(sparse_blocks(n)) + 2) * 4);
+  w.temp = p;
+  w.temp_bytes = sort_temp_bytes(n, end_bit);
+  return w;
+}
+}  // namespace
+
+size_t sparse_workspace_bytes(unsigned long long n, int end_bit) {
+  auto al = [](size_t x) { return (x + 255) / 256 * 256; };
+  return al(n * 8) * 2 + al(n * 4) * 2 + al((size_t(sparse_blocks(n)) + 2) * 4) + al(sort_temp_bytes(n, end_bit)) + 256;
+}
+
+hipError_t launch_sparse_sort(const SParams& S, const uint32_t* d_counts, unsigned long long n, int end_bit, void* ws,
+                              uint32_t** d_nrows, hipStream_t st) {
+  SparseWs w = carve(ws, n, end_bit);
+  *d_nrows = w.counts + sparse_blocks(n);
+  if (n == 0) return hipMemsetAsync(*d_nrows, 0, 4, st);
+  hipLaunchKernelGGL(sparse_emit, dim3(sparse_blocks(S.cap)), dim3(SB), 0, st, S, d_counts, w.k0, w.s0);
+  size_t tb = w.temp_bytes;
+  hipError_t e = hipcub::DeviceRadixSort::SortPairs(w.temp, tb, w.k0, w.k1, w.s0, w.s1, int(n), 0, end_bit, st);
+  if (e != hipSuccess) return e;
+  const uint32_t nb = sparse_blocks(n);
+  hipLaunchKernelGGL(runs_count, dim3(nb), dim3(SB), 0, st, w.k1, n, w.counts);
+  hipLaunchKernelGGL(finalize_scan, dim3(1), dim3(1024), 0, st, w.counts, nb);
+  return hipGetLastError();
+}
+
+hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws, int64_t* ts, double* val,
+                               unsigned long long* gid, uint32_t* glob, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  SparseWs w = carve(ws, n, 64);
+  hipLaunchKernelGGL(runs_write, dim3(sparse_blocks(n)), dim3(SB), 0, st, S, w.k1, w.s1, n, w.counts, ts, val, gid, glob);
   return hipGetLastError();
 }
 

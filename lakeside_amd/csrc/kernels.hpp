@@ -57,6 +57,50 @@ struct TableRef {
   double* lo;
   unsigned long long* ext;
 };
+// Hash-mode table of a rank merged into rank 0's: `n` gathered records [key | rows | cnt | hi | lo | ext] (n each).
+hipError_t launch_merge_records(const QParams& P, const unsigned long long* recs, size_t n, int agg, hipStream_t stream);
+// Hash-mode table -> compact records [key | rows | cnt | hi | lo | ext] (cap = slots; count first with
+// launch_finalize_sparse's counting pass: rows land at d_counts offsets).
+hipError_t launch_table_records(const QParams& P, unsigned long long cap, uint32_t* d_counts, unsigned long long* recs,
+                                size_t n, hipStream_t stream);
+
+// Sparse finalize (hash mode): occupied slots -> (output key, slot) -> radix sort -> one row per output key,
+// cells of one key combined exactly as the dense finalize combines them.
+struct SParams {
+  const unsigned long long* keys;  // slot keys (EMPTY = ~0)
+  const unsigned long long* rows;
+  const unsigned long long* cnt;
+  const double* hi;
+  const double* lo;
+  const unsigned long long* ext;
+  unsigned long long cap;          // slots
+  unsigned long long ngroups, nbuckets;
+  uint32_t nslots;                 // glob slots of the cell keys
+  int agg;
+  int per_glob;                    // output key (bucket, glob, group)
+  int collapse;                    // output key (bucket): the name dimension folds (no groupBys, merged)
+  int rekey;                       // merged min/max with NULL-able values: per-glob SQL values fold under `map`
+  int ndims;
+  unsigned long long stride[MAXSTR];
+  unsigned long long ndim[MAXSTR];
+  const uint32_t* map[MAXSTR];
+  unsigned long long name_stride;
+  const uint32_t* name_rank;
+  int64_t bucket_base;
+  int64_t step;
+};
+// Workspace bytes launch_finalize_sparse needs for `n` occupied slots (sort buffers + scan + sort temp).
+size_t sparse_workspace_bytes(unsigned long long n, int end_bit);
+// Count occupied slots: total at d_counts[sparse_blocks(cap)] after the scan.
+uint32_t sparse_blocks(unsigned long long cap);
+hipError_t launch_sparse_count(const SParams& S, uint32_t* d_counts, hipStream_t stream);
+// Build + sort (output key, slot) pairs of the `n` occupied slots and count the output rows: the row total lands
+// at the returned device pointer (uint32).  `end_bit`: bits of the largest output key.
+hipError_t launch_sparse_sort(const SParams& S, const uint32_t* d_counts, unsigned long long n, int end_bit, void* ws,
+                              uint32_t** d_nrows, hipStream_t stream);
+hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws, int64_t* ts, double* val,
+                               unsigned long long* gid, uint32_t* glob, hipStream_t stream);
+
 hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
                                hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);

@@ -148,11 +148,16 @@ struct QParams {
   double* hi;                       // sum = hi + lo (compensated)
   double* lo;
   unsigned long long* ext;          // min/max as order-preserving u64
+  // hash mode (high cardinality, SURVEY §2.2 K4 spill): the SoA arrays above are slots of an open-addressing
+  // table whose slot keys are `hkeys` (EMPTY = ~0); null: dense mode (array index = cell key)
+  unsigned long long* hkeys;
+  unsigned long long hmask;         // slots - 1 (a power of two)
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
 };
 
-enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u };
+enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u };
+constexpr uint32_t HASH_MAX_PROBE = 4096;   // linear probes before a hash-mode insert reports the table full
 
 }  // namespace lk

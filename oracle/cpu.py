@@ -1,0 +1,234 @@
+"""ctypes wrapper of oracle/liblkcpu.so: the multi-core C++ restatement of the evaluator (TEST INFRASTRUCTURE ONLY).
+
+Same contract as oracle/dataexpr.py (per-glob rows at the worker, S17; merged rows at query-api, S19), computed by
+oracle/cpu/lkcpu.cpp over in-memory Parquet bytes on every host core.  Used by bench.py (timed CPU baseline,
+full-size validation of the GPU rows) and checked against oracle/dataexpr.py in tests/test_oracle_cpu.py.
+Only tests/, bench.py and __graft_entry__.smoke() may import it; the product path never does.
+"""
+import ctypes
+import math
+import os
+from typing import Dict, List, Optional, Sequence, Tuple
+from urllib.parse import quote
+
+import numpy as np
+
+from . import dataexpr as dx
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liblkcpu.so")
+_L = None
+
+
+def lib():
+    global _L
+    if _L is None:
+        L = ctypes.CDLL(LIB)
+        L.lkcpu_eval.restype = ctypes.c_void_p
+        L.lkcpu_eval.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                 ctypes.c_size_t, ctypes.c_int]
+        L.lkcpu_error.restype = ctypes.c_char_p
+        L.lkcpu_ncells.restype = ctypes.c_size_t
+        L.lkcpu_ncells.argtypes = [ctypes.c_void_p]
+        L.lkcpu_ncols.restype = ctypes.c_int
+        L.lkcpu_ncols.argtypes = [ctypes.c_void_p]
+        L.lkcpu_cells.argtypes = [ctypes.c_void_p] + [ctypes.c_void_p] * 10
+        L.lkcpu_key_string.restype = ctypes.c_char_p
+        L.lkcpu_key_string.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int32]
+        L.lkcpu_free.argtypes = [ctypes.c_void_p]
+        _L = L
+    return _L
+
+
+def _leaves(q, out):
+    if isinstance(q, dx.Filter):
+        out.append(q)
+    elif isinstance(q, dx.NotClause):
+        _leaves(q.inner, out)
+    else:
+        _leaves(q.q1, out)
+        _leaves(q.q2, out)
+    return out
+
+
+def _postfix(q, leaves, out):
+    if isinstance(q, dx.Filter):
+        out.append(next(i for i, l in enumerate(leaves) if l is q))
+    elif isinstance(q, dx.NotClause):
+        _postfix(q.inner, leaves, out)
+        out.append(-3)
+    else:
+        _postfix(q.q1, leaves, out)
+        _postfix(q.q2, leaves, out)
+        out.append(-1 if q.op == "and" else -2)
+    return out
+
+
+def plan_text(pr: dx.PushDownRequest, glob_size: int) -> Tuple[str, List[str], List[str]]:
+    """Flatten the parsed request into lkcpu's line format; returns (text, string columns, groupBys)."""
+    be = pr.baseExpr
+    dx.check_hot_path(pr)
+    leaves = _leaves(be.filter, [])
+    strcols = [dx.NAME]
+    for l in leaves:
+        if l.k not in strcols:
+            strcols.append(l.k)
+    gbs = []
+    for g in be.chart.groupBys:
+        if g not in gbs:
+            gbs.append(g)
+    for g in gbs:
+        if g not in strcols:
+            strcols.append(g)
+    if len(strcols) > 7:
+        raise NotImplementedError("lkcpu: at most 7 string columns")
+    t = ["metrics" if be.dataset == dx.METRICS else be.dataset, be.chart.aggregation, dx.value_column(be),
+         str(glob_size), str(len(pr.segmentRequests))]
+    for s in pr.segmentRequests:
+        t += [str(s.startTs), str(s.endTs), str(s.stepInMillis)]
+    t += [str(len(strcols))] + strcols
+    t += [str(len(gbs))] + [str(strcols.index(g)) for g in gbs]
+    t += [str(len(leaves))]
+    for l in leaves:
+        t += [str(strcols.index(l.k)), l.op, str(len(l.v))] + list(l.v)
+    prog = _postfix(be.filter, leaves, [])
+    t += [str(len(prog))] + [str(x) for x in prog]
+    fs = sorted(dx.field_set(be))
+    t += [str(len(fs))] + fs
+    return "\n".join(quote(x, safe="") for x in t) + "\n", strcols, gbs
+
+
+def _dd(*xs):
+    """Correctly rounded sum of double-double parts (IEEE propagation for non-finite values)."""
+    return math.fsum(xs) if all(math.isfinite(x) for x in xs) else float(np.sum(np.array(xs)))
+
+
+class CpuCell:
+    """One per-glob (bucket, group) cell of the CPU restatement."""
+    __slots__ = ("ts", "tags", "rows", "count", "hi", "lo", "vmin", "vmax", "glob")
+
+    def agg_value(self, agg: str) -> float:
+        if agg == dx.COUNT:
+            return float(self.count)
+        if self.count == 0:
+            return 0.0
+        if agg == dx.SUM:
+            return _dd(self.hi, self.lo)
+        if agg == dx.AVG:
+            return _dd(self.hi, self.lo) / self.count
+        return self.vmin if agg == dx.MIN else self.vmax
+
+
+def evaluate_glob_cells(pr: dx.PushDownRequest, glob_size: int, blobs: Sequence, threads: int = 0):
+    """Per-glob cells over in-memory Parquet `blobs` (bytes or (pointer, size)), in request order."""
+    text, strcols, gbs = plan_text(pr, glob_size)
+    n = len(blobs)
+    ptrs = (ctypes.c_void_p * max(1, n))()
+    sizes = (ctypes.c_size_t * max(1, n))()
+    keep = []
+    for i, b in enumerate(blobs):
+        if isinstance(b, (bytes, bytearray)):
+            buf = ctypes.create_string_buffer(bytes(b), len(b))
+            keep.append(buf)
+            ptrs[i] = ctypes.cast(buf, ctypes.c_void_p)
+            sizes[i] = len(b)
+        else:
+            ptrs[i] = ctypes.cast(b[0], ctypes.c_void_p)
+            sizes[i] = b[1]
+    L = lib()
+    h = L.lkcpu_eval(text.encode(), ptrs, sizes, n, threads)
+    if not h:
+        raise RuntimeError(L.lkcpu_error().decode())
+    try:
+        m = L.lkcpu_ncells(h)
+        nc = L.lkcpu_ncols(h)
+        glob = np.zeros(m, np.int32)
+        ts = np.zeros(m, np.int64)
+        rows = np.zeros(m, np.uint64)
+        cnt = np.zeros(m, np.uint64)
+        hi = np.zeros(m, np.float64)
+        lo = np.zeros(m, np.float64)
+        mn = np.zeros(m, np.float64)
+        mx = np.zeros(m, np.float64)
+        nanf = np.zeros(m, np.uint8)
+        keys = np.zeros(m * nc, np.int32)
+        L.lkcpu_cells(h, *[a.ctypes.data for a in (glob, ts, rows, cnt, hi, lo, mn, mx, nanf, keys)])
+        names = ["name"] + gbs
+        strings: List[Dict[int, Optional[str]]] = [dict() for _ in range(nc)]
+
+        def key_string(c, i):
+            d = strings[c]
+            if i not in d:
+                v = L.lkcpu_key_string(h, c, int(i))
+                d[i] = None if v is None else v.decode()
+            return d[i]
+
+        nglobs = (len(pr.segmentRequests) + glob_size - 1) // glob_size
+        out = [[] for _ in range(nglobs)]
+        globs = dx.globs_of(pr, glob_size)
+        qtags = [{k: (v if isinstance(v, str) else str(v)) for k, v in pr.segmentRequests[g[0]].queryTags.items()}
+                 for g in globs]
+        keys = keys.reshape(m, nc) if m else keys.reshape(0, nc)
+        for i in range(m):
+            c = CpuCell()
+            c.glob = int(glob[i])
+            c.ts = int(ts[i])
+            c.rows = int(rows[i])
+            c.count = int(cnt[i])
+            c.hi = float(hi[i])
+            c.lo = float(lo[i])
+            c.vmin = float(mn[i]) if nanf[i] & 2 else math.nan
+            c.vmax = math.nan if nanf[i] & 1 else float(mx[i])
+            tags = {}
+            for j in range(nc):
+                if keys[i, j] < 0:
+                    continue
+                sv = key_string(j, keys[i, j])
+                if sv is not None and sv != "null" and sv != "":   # Commons.scala:433 (S15)
+                    tags[names[j]] = sv
+            c.tags = tags if tags else dict(qtags[c.glob])          # Commons.scala:450-452
+            out[c.glob].append(c)
+        for cells in out:
+            cells.sort(key=lambda c: (c.ts, sorted(c.tags.items())))
+        return out
+    finally:
+        L.lkcpu_free(h)
+
+
+def merge_glob_cells(pr: dx.PushDownRequest, glob_cells) -> List[Tuple[int, float, Dict[str, str]]]:
+    """query-api merge (S19), as oracle/dataexpr.merge_glob_cells, over the CPU cells."""
+    agg = pr.baseExpr.chart.aggregation
+    has_gb = bool(pr.baseExpr.chart.groupBys)
+    merged: Dict = {}
+    for cells in glob_cells:
+        for c in cells:
+            k = (c.ts, tuple(sorted(c.tags.items()))) if has_gb else c.ts
+            merged.setdefault(k, []).append(c)
+    out = []
+    for k, cs in merged.items():
+        tags = min((c.tags for c in cs), key=lambda t: sorted(t.items()))
+        if agg == dx.SUM:
+            val = _dd(*[x for c in cs for x in (c.hi, c.lo)]) if any(c.count for c in cs) else 0.0
+        elif agg == dx.COUNT:
+            val = float(sum(c.count for c in cs))
+        elif agg == dx.AVG:
+            n = sum(c.count for c in cs)
+            s = _dd(*[x for c in cs for x in (c.hi, c.lo)])
+            val = s / n if n else math.nan
+        elif agg == dx.MIN:
+            val = min(c.agg_value(dx.MIN) for c in cs)
+        else:
+            val = max(c.agg_value(dx.MAX) for c in cs)
+        out.append((cs[0].ts, val, tags))
+    out.sort(key=lambda r: (r[0], sorted(r[2].items()), r[1]))
+    return out
+
+
+def evaluate_merged(pr: dx.PushDownRequest, blobs: Sequence, glob_size: int = 10, threads: int = 0):
+    return merge_glob_cells(pr, evaluate_glob_cells(pr, glob_size, blobs, threads))
+
+
+def evaluate_per_glob(pr: dx.PushDownRequest, blobs: Sequence, glob_size: int = 10, threads: int = 0):
+    agg = pr.baseExpr.chart.aggregation
+    return [[(c.ts, c.agg_value(agg), c.tags) for c in cells]
+            for cells in evaluate_glob_cells(pr, glob_size, blobs, threads)]

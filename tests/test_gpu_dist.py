@@ -113,3 +113,114 @@ def test_dist_world1_rccl_golden():
             assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"rccl world 1 {case['name']}")
     finally:
         eng.close()
+
+
+# ---------------------------------------------------------------------------------------------------------
+# 8 ranks on the one GPU (host transport): the C4 and C5 shapes with a different dictionary on every rank
+# ---------------------------------------------------------------------------------------------------------
+def _worker8(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd import synth
+    from lakeside_amd.evaluator import Engine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        results = {}
+        # (name, segments per rank, rows, highcard, step, hour, groupBys, env)
+        shapes = [("c4", 2, 1 << 20, 0, 60_000, None, [synth.SERVICE], {}),
+                  ("c5_1h", 1, 1 << 20, 10_000_000, 3_600_000, 0, [synth.CONTAINER], {}),
+                  ("c5_1m_hash", 1, 1 << 20, 10_000_000, 60_000, 0, [synth.CONTAINER], {})]
+        for name, per, rows, hc, step, hour, gbs, env in shapes:
+            n = per * world
+            keys = [f"d8/{name}/{i}" for i in range(n)]
+            shard = [i // per for i in range(n)]
+            for i in range(n):   # only this rank's shard: every rank's engine dictionary differs
+                if shard[i] == rank:
+                    s = synth.make_segment(synth.segment_spec(i, rows=rows, hour=hour, highcard_n=hc))
+                    eng.put_segment_ptr(keys[i], s.ptr, s.size)
+                    s.free()
+            segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
+            req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), segs, "sum", gbs))
+            res = eng.eval_pushdown_dist(req, keys, shard, 10)
+            if rank == 0:
+                results[name] = (req, res.rows(), res.stats)
+            else:
+                assert len(res) == 0
+        dist.barrier()
+        if rank == 0:
+            q.put(results)
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_dist_world8_host_transport_c4_c5_shapes():
+    """8 ranks (one GPU, host transport over gloo), each holding only its shard's segments, so the unrestricted
+    group dims (service / 10M-value container) go through the dictionary exchange; C5 at a 1m step runs the hash
+    table and its record exchange.  Rank 0's merged rows equal the oracle over every segment."""
+    import torch.multiprocessing as mp
+
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = mp.start_processes(_worker8, args=(8, _free_port(), q), nprocs=8, join=False, start_method="spawn")
+    results = q.get(timeout=800)
+    procs.join()
+    for name, (req, rows, stats) in results.items():
+        pr = dx.parse_pushdown(req)
+        per = 2 if name == "c4" else 1
+        n = per * 8
+        hour = None if name == "c4" else 0
+        hc = 0 if name == "c4" else 10_000_000
+        blobs = []
+        for i in range(n):
+            s = synth.make_segment(synth.segment_spec(i, rows=1 << 20, hour=hour, highcard_n=hc))
+            blobs.append(s.bytes())
+            s.free()
+        want = dx.evaluate_merged(pr, [f"k{i}" for i in range(n)], 10, sources=blobs)
+        assert_rows_equal(rows, want, "sum", f"world 8 {name}")
+        if name == "c5_1m_hash":
+            assert stats["table"] == "hash", stats
+
+
+def _worker_err(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd.evaluator import Engine, LakesideError
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        case = _cases()[0]
+        paths = [os.path.join(GOLDEN, p) for p in case["segments"]] + ["/nonexistent/segment.parquet"]
+        req = dict(case["request"])
+        req["segmentRequests"] = list(req["segmentRequests"]) + [req["segmentRequests"][0]]
+        shard = [0] * (len(paths) - 1) + [1]   # the missing file is rank 1's
+        with pytest.raises(LakesideError) as ei:
+            eng.eval_pushdown_dist(json.dumps(req), paths, shard, case["glob_size"])
+        assert "segment" in str(ei.value)
+        # the communicator is still usable afterwards: a good call succeeds on both ranks
+        ok = eng.eval_pushdown_dist(json.dumps(case["request"]), paths[:-1], None, case["glob_size"])
+        if rank == 0:
+            agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+            assert_rows_equal(ok.rows(), from_jsonable(case["expected_merged"]), agg, "after error")
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_dist_rank_local_error_fails_every_rank():
+    """A segment only rank 1 reads is missing: both ranks return an error (none waits in a collective) and the
+    next call works (agree on a status before each collective)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_worker_err, args=(2, _free_port()), nprocs=2, join=True)

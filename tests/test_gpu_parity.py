@@ -442,10 +442,13 @@ def test_concurrent_calls_from_threads(golden_engine):
     assert not errors, errors[0]
 
 
-@pytest.mark.parametrize("pattern", ["(?i)^SVC-0[0-4]", "\\Asvc-0[0-4]", "(?P<id>svc-0[1-3])[0-9]\\z", "[]x]|svc-09"])
+@pytest.mark.parametrize("pattern", ["(?i)^SVC-0[0-4]", "\\Asvc-0[0-4]", "(?P<id>svc-0[1-3])[0-9]\\z", "[]x]|svc-09",
+                                     "\\Qsvc-01\\E", "\\pL{3}-0[[:digit:]]1", "[[:digit:]a]\\z", "(?-i:SVC)|svc-0(?:0|4)7",
+                                     "^(svc-0[0-2]){1}\\d$", "\\bsvc\\B"])
 def test_regex_re2_spellings(golden_engine, pattern):
-    """RE2 spellings std::regex lacks ((?i) prefix, \\A, \\z, named groups) match exactly as RE2 does (oracle:
-    pyarrow's RE2, the engine behind DuckDB's regexp_matches)."""
+    """RE2 syntax (flags, \\A / \\z, named groups, \\Q..\\E, Unicode and POSIX classes, word boundaries) through
+    the evaluator's RE2-semantics matcher equals RE2 (oracle: pyarrow's RE2, the engine behind DuckDB's
+    regexp_matches)."""
     from lakeside_amd import LK_MERGED
     from oracle import dataexpr as dx
     case = next(c for c in _cases() if c["name"] == "c3_and_regex_by2_max")
@@ -457,3 +460,36 @@ def test_regex_re2_spellings(golden_engine, pattern):
     want = dx.evaluate_merged(dx.parse_pushdown(text), paths, case["glob_size"])
     assert len(want) > 0
     assert_rows_equal(got.rows(), want, "max", pattern)
+
+
+def test_regex_non_ascii_dictionary_values(engine, tmp_path):
+    """regex / contains over non-ASCII tag values (case-fold orbits: sigma, Kelvin sign, long s; accents; CJK):
+    the leaf outcome per dictionary value equals RE2's (pyarrow), so the GPU rows equal the oracle's."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(5)
+    vocab = ["Σίσυφος", "σίσυφος", "ΣΊΣΥΦΟΣ", "KELVIN-K", "kelvin-k", "ſtraße", "STRASSE", "école", "ÉCOLE",
+             "日本語", "naïve café", "svc-001", "İstanbul", "istanbul", "ǅungla", "null", ""]
+    n = 100_000
+    t0 = synth.T0
+    t = pa.table({
+        dx.TIMESTAMP: pa.array(np.sort(rng.integers(t0, t0 + synth.HOUR, n)), pa.int64()),
+        dx.VALUE: pa.array(rng.integers(0, 1000, n).astype(np.float64), pa.float64()),
+        synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 4, n)], pa.string()),
+        synth.SERVICE: pa.array([vocab[k] for k in rng.integers(0, len(vocab), n)], pa.string(),
+                                mask=rng.random(n) < 0.03),
+    })
+    path = str(tmp_path / "nonascii.parquet")
+    pq.write_table(t, path, compression="NONE", use_dictionary=[synth.NAME, synth.SERVICE],
+                   column_encoding={dx.TIMESTAMP: "PLAIN", dx.VALUE: "PLAIN"}, row_group_size=50_000)
+    engine.load_segment(path)
+    segs = [synth.segment_request(0)]
+    for op, pat in [("regex", "σίσυφος"), ("regex", "^kelvin"), ("regex", "STRASSE|ſtr"), ("contains", "É"),
+                    ("regex", "^.{3}$"), ("regex", "\\p{Lu}"), ("regex", "i̇|^ist"), ("contains", "ǆ"),
+                    ("regex", "[^\\x00-\\x7f]"), ("regex", "\\bcaf")]:
+        req = json.dumps(synth.pushdown(synth.leaf(synth.SERVICE, op, pat), segs, "count", [synth.SERVICE]))
+        got = engine.eval_pushdown(req, [path], 10, LK_MERGED)
+        want = dx.evaluate_merged(dx.parse_pushdown(req), [path], 10)
+        assert_rows_equal(got.rows(), want, "count", f"{op} {pat}")

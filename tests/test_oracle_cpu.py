@@ -1,0 +1,65 @@
+"""The multi-core C++ restatement (oracle/cpu) against the Python oracle (oracle/dataexpr.py) on the committed golden
+cases and on synthetic segments: it is the bench's CPU baseline and its full-size validator, so it must agree
+with the pinned oracle first.  CPU only."""
+import json
+import os
+
+import pytest
+
+from tests.parity import assert_rows_equal, from_jsonable
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+
+
+def _cases():
+    with open(os.path.join(GOLDEN, "cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", _cases(), ids=lambda c: c["name"])
+def test_cpu_restatement_golden(case):
+    from oracle import cpu, dataexpr as dx
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    blobs = [open(p, "rb").read() for p in paths]
+    pr = dx.parse_pushdown(json.dumps(case["request"]))
+    agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+    try:
+        got = cpu.evaluate_per_glob(pr, blobs, case["glob_size"], threads=4)
+    except RuntimeError as e:
+        if "compressed" in str(e):
+            pytest.skip("compressed fixture")
+        raise
+    for gi, (g, w) in enumerate(zip(got, case["expected_per_glob"])):
+        assert_rows_equal(g, from_jsonable(w), agg, f"cpu {case['name']} glob {gi}")
+    if case["expected_merged"] is not None:
+        assert_rows_equal(cpu.evaluate_merged(pr, blobs, case["glob_size"], threads=3),
+                          from_jsonable(case["expected_merged"]), agg, f"cpu {case['name']} merged")
+
+
+@pytest.mark.parametrize("agg,gbs,null_frac,value_mode", [("sum", [], 0.0, 0), ("max", ["svc", "ns"], 0.05, 1),
+                                                         ("avg", ["ns"], 0.05, 1), ("count", ["name"], 0.0, 1),
+                                                         ("min", [], 0.05, 1)])
+def test_cpu_restatement_synthetic(agg, gbs, null_frac, value_mode):
+    from lakeside_amd import synth
+    from oracle import cpu, dataexpr as dx
+    col = {"svc": synth.SERVICE, "ns": synth.NAMESPACE, "name": synth.NAME}
+    blobs = []
+    for i in range(5):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 17, value_mode=value_mode, null_frac=null_frac,
+                                                  rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        s.free()
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_07"),
+            "q2": {"op": "or", "q1": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]"),
+                   "q2": {"not": synth.leaf(synth.NAMESPACE, "eq", "ns-03")}}}
+    segs = [synth.segment_request(i) for i in range(5)]
+    req = json.dumps(synth.pushdown(filt, segs, agg, [col[g] for g in gbs]))
+    pr = dx.parse_pushdown(req)
+    keys = [f"s{i}" for i in range(5)]
+    want_pg = dx.evaluate_per_glob(pr, keys, 2, sources=blobs)
+    got_pg = cpu.evaluate_per_glob(pr, blobs, 2, threads=8)
+    for gi, (g, w) in enumerate(zip(got_pg, want_pg)):
+        assert_rows_equal(g, w, agg, f"glob {gi}")
+    assert_rows_equal(cpu.evaluate_merged(pr, blobs, 2, threads=8), dx.evaluate_merged(pr, keys, 2, sources=blobs), agg,
+                      "merged")
