@@ -14,7 +14,7 @@ RELIB   = lakeside_amd/liblakeside_regex.so
 
 HOST_SRCS = $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
-HIP_OBJS  = $(OBJDIR)/kernels.o
+HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
 
 all: $(LIB) $(SYNTH) $(RELIB)
@@ -23,7 +23,7 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS_HOST) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -c $< -o $@
 
-$(OBJDIR)/kernels.o: $(SRC)/kernels.hip $(HDRS)
+$(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 
@@ -41,6 +41,7 @@ $(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
 asm: $(SRC)/kernels.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o build/kernels.s
+	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(SRC)/scan_$$a.hip -o build/scan_$$a.s; done
 
 clean:
 	rm -rf build $(LIB) $(SYNTH) $(RELIB)

@@ -69,7 +69,8 @@ def main():
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default: the query's config)")
     ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
-    ap.add_argument("--cpu-sample", type=int, default=12, help="segments timed on the CPU oracle (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=-1,
+                    help="segments timed on the CPU restatement (-1: all = full-size validation; 0: skip)")
     ap.add_argument("--gen-workers", type=int, default=4)
     args = ap.parse_args()
 
@@ -106,6 +107,9 @@ def main():
         return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour,
                                                         highcard_n=highcard))
 
+    # The CPU baseline / validator (rank 0 at N=1) reads the same Parquet bytes: keep them in host memory.
+    keep_cpu = rank == 0 and world == 1 and args.cpu_sample != 0
+    kept = {}
     t0 = time.time()
     bytes_loaded = 0
     with cf.ThreadPoolExecutor(args.gen_workers) as ex:
@@ -113,7 +117,10 @@ def main():
             i, seg = fut.result()
             eng.put_segment_ptr(keys[i], seg.ptr, seg.size)
             bytes_loaded += seg.size
-            seg.free()
+            if keep_cpu:
+                kept[i] = seg
+            else:
+                seg.free()
             if n % 8 == 7:
                 log(f"rank {rank}: {n + 1}/{S} segments generated + loaded to HBM ({time.time() - t0:.0f}s)")
     log(f"rank {rank}: {S} segments ({bytes_loaded / 1e9:.1f} GB Parquet) resident, HBM cache "
@@ -133,7 +140,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
-    launch_ms, sync_ms, alloc_ms, copy_ms = [], [], [], []
+    launch_ms, sync_ms, alloc_ms, copy_ms, plan_bytes = [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -146,6 +153,7 @@ def main():
         alloc_ms.append(res.stats.get("alloc_ms", 0.0))
         copy_ms.append(res.stats.get("copy_ms", 0.0))
         alg_bytes = res.stats["algorithmic_bytes"]
+        plan_bytes.append(res.stats.get("plan_bytes", 0))
         out_rows = len(res)
     torch.cuda.synchronize()
     if world > 1:
@@ -162,20 +170,16 @@ def main():
     rows_total = total * args.rows
     value = rows_total / (ms_per_step / 1e3)
     scan_avg = sum(scan_ms) / len(scan_ms)
-    achieved = alg_bytes / (scan_avg / 1e3) / 1e9
+    # Roofline numerator: the bytes the late-materialized plan must read, counted by the scan kernel (streams it
+    # decodes in full + distinct 128-B lines of its per-row gathers + tile metadata), per launch.
+    pbytes = sum(plan_bytes) / len(plan_bytes)
+    achieved = pbytes / (scan_avg / 1e3) / 1e9
+    alg_gbs = alg_bytes / (scan_avg / 1e3) / 1e9
     log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
-        f"{achieved:.0f} GB/s algorithmic, {out_rows} output rows; in the call: plan {sum(plan_ms) / len(plan_ms):.2f} ms, "
-        f"device {sum(device_ms) / len(device_ms):.2f} ms, total {sum(total_ms) / len(total_ms):.2f} ms "
-        f"(scan enqueued at {sum(launch_ms) / len(launch_ms):.2f} ms, device done at {sum(sync_ms) / len(sync_ms):.2f} ms, "
-        f"rows allocated at {sum(alloc_ms) / len(alloc_ms):.2f} ms, copied at {sum(copy_ms) / len(copy_ms):.2f} ms)")
-
-    traffic = None
-    # PMC-measured HBM bytes per launch of the scan kernel, newest round's summary (scripts/gpu_bench_prof.sh)
-    import glob as _glob
-    profs = sorted(_glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_{args.query}.json")))
-    if profs:
-        with open(profs[-1]) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+        f"plan bytes {pbytes / 1e9:.2f} GB/launch -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.3f} of peak); "
+        f"SURVEY algorithmic {alg_bytes / 1e9:.2f} GB -> {alg_gbs:.0f} GB/s; {out_rows} output rows; in the call: "
+        f"plan {sum(plan_ms) / len(plan_ms):.2f} ms, device {sum(device_ms) / len(device_ms):.2f} ms, "
+        f"total {sum(total_ms) / len(total_ms):.2f} ms")
 
     # measured device-to-device copy rate on this GPU (a stream-copy peak beside the spec peak)
     copy_gbs = None
@@ -192,9 +196,11 @@ def main():
         copy_gbs = 2 * 10 * a.numel() / (e0.elapsed_time(e1) / 1e3) / 1e9   # read + write bytes
         del a, b
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_sample > 0:
-        cpu = cpu_baseline(args, q, synth)
+    cpu, validated = None, None
+    if keep_cpu and not q.get("tag"):
+        cpu, validated = cpu_baseline_and_validate(args, q, req, [kept[i] for i in mine], res)
+    for sgm in kept.values():
+        sgm.free()
 
     if rank == 0:
         line = {
@@ -209,12 +215,16 @@ def main():
             "rows_scanned": rows_total, "output_rows": out_rows,
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         # measured HBM rate (PMC bytes / kernel time): late materialization reads fewer bytes
-                         # than the algorithmic count, so this is the kernel's actual bandwidth use
-                         "traffic_gbs": traffic / (scan_avg / 1e3) / 1e9 if traffic else None,
-                         "stream_copy_gbs": copy_gbs,
-                         "algorithmic_bytes_per_launch": alg_bytes},
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "definition": "achieved = plan bytes per launch (counted by the scan kernel: streams "
+                                       "decoded in full + distinct 128-B lines of every per-row gather + tile "
+                                       "metadata) / scan-kernel time (HIP events on the call's stream)",
+                         "plan_bytes_per_launch": pbytes,
+                         "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_gbs": alg_gbs,
+                         "traffic_note": "PMC HBM bytes come from separate rocprofv3 --pmc passes "
+                                         "(profiles/r02_pmc_*.json); not measurable inside this run",
+                         "stream_copy_gbs": copy_gbs},
+            "validated": validated,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -223,33 +233,53 @@ def main():
     eng.close()
 
 
-def cpu_baseline(args, q, synth):
-    """The CPU restatement (oracle/dataexpr.py: pyarrow decode + numpy) on a bounded sample of the same
-    workload, single-threaded.  A reported baseline, not the target."""
-    import pyarrow as pa
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline_and_validate(args, q, req, segs, gpu_res):
+    """The CPU restatement (oracle/cpu: C++17 + OpenMP over the same in-memory Parquet bytes, every host core of
+    this job) timed on the workload, and the GPU's merged rows checked against its rows.  A reported baseline,
+    not the target (the reference's JVM + DuckDB cannot run here)."""
+    from oracle import cpu as lkcpu
     from oracle import dataexpr as dx
-    pa.set_cpu_count(1)
-    pa.set_io_thread_count(1)
-    n = args.cpu_sample
-    blobs = []
-    step, hour, highcard = q.get("step", 60000), q.get("hour"), q.get("highcard_n", 0)
-    for i in range(n):
-        s = synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour, highcard_n=highcard))
-        blobs.append(s.bytes())
-        s.free()
-    keys = [f"cpu/{i}" for i in range(n)]
-    segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
-    pr = dx.parse_pushdown(json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag"))))
-    t = time.perf_counter()
-    if q.get("tag"):
-        dx.evaluate_tag_merged(pr, q["tag"], keys, 10, sources=blobs)
-    else:
-        dx.evaluate_merged(pr, keys, 10, sources=blobs)
-    dt = time.perf_counter() - t
-    log(f"cpu baseline: {n} segments in {dt:.1f}s")
-    return {"value": n * args.rows / dt, "unit": "rows/s", "cores": 1, "kind": "port",
-            "sample": f"{n} of the workload's segments ({n * args.rows} rows), same query, oracle/dataexpr.py "
-                      f"(pyarrow decode + numpy, 1 thread)"}
+    from tests.parity import assert_rows_equal
+    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    n = len(segs) if args.cpu_sample < 0 else min(len(segs), args.cpu_sample)
+    blobs = [(s.ptr, s.size) for s in segs[:n]]
+    pr = dx.parse_pushdown(req)
+    if n < len(segs):   # a sample: the request over the sampled segments only
+        body = json.loads(req)
+        body["segmentRequests"] = body["segmentRequests"][:n]
+        pr = dx.parse_pushdown(json.dumps(body))
+    lkcpu.evaluate_merged(pr, blobs, 10, threads)   # warm (page-in, thread pool)
+    times = []
+    for _ in range(3):
+        t = time.perf_counter()
+        rows = lkcpu.evaluate_merged(pr, blobs, 10, threads)
+        times.append(time.perf_counter() - t)
+    dt = sorted(times)[1]
+    log(f"cpu baseline: {n} segments x {args.rows} rows in {dt:.2f}s (median of 3) on {threads} threads "
+        f"({_cpu_model()}, {os.cpu_count()} CPUs visible)")
+    validated = None
+    if n == len(segs):
+        try:
+            assert_rows_equal(gpu_res.rows(), rows, q["agg"], "bench GPU rows vs CPU restatement")
+            validated = {"ok": True, "rows": len(rows), "against": "oracle/cpu (C++ restatement), full workload"}
+        except AssertionError as e:
+            validated = {"ok": False, "rows": len(rows), "error": str(e)[:500]}
+        log(f"validation: {validated}")
+    return ({"value": n * args.rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+             "sample": f"{n} of the workload's {len(segs)} segments ({n * args.rows} rows), same query, "
+                       f"oracle/cpu/lkcpu.cpp (C++17 + OpenMP restatement, {threads} threads, median of 3)"},
+            validated)
 
 
 if __name__ == "__main__":

@@ -139,12 +139,13 @@ __device__ __forceinline__ unsigned long long hash_slot(unsigned long long* keys
   return EMPTY;
 }
 
-// Merge a partial cell into the global table (device-scope atomics).
-template <int AGG>
+// Merge a partial cell into the global table (device-scope atomics).  HASH: the table is the hash-mode table
+// (a compile-time choice: the probe loop would otherwise cost the dense kernels registers).
+template <int AGG, bool HASH = false>
 __device__ __forceinline__ void global_merge(const QParams& P, unsigned long long cell, uint32_t rows,
                                              uint32_t cnt, double hi, double lo, unsigned long long ext) {
   if (rows == 0) return;
-  if (P.hkeys) {
+  if (HASH) {
     cell = hash_slot(P.hkeys, P.hmask, P.flags, cell);
     if (cell == EMPTY) return;
   }

@@ -198,7 +198,7 @@ struct Builder {
   std::deque<std::vector<uint8_t>> plain;     // decompressed pages (host_vals point into them until tiling)
 
   size_t put(const uint8_t* p, size_t n) {
-    size_t off = align_up(stage.size(), 16);
+    size_t off = align_up(stage.size(), 128);   // every page stream starts on an HBM line (plan-bytes counting)
     stage.resize(off + n);
     if (n) memcpy(stage.data() + off, p, n);
     return off;

@@ -836,6 +836,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
   size_t nc = 0;
   double launch_ms = 0;
+  unsigned long long plan_bytes = 0;
   auto zero_table = [&](size_t ncl, bool hashed) {
     uint8_t* tb = static_cast<uint8_t*>(X->workspace("table", ncl * 8 * (hashed ? 6 : 5) + 4 * 256));
     P.rows = reinterpret_cast<unsigned long long*>(tb);
@@ -854,7 +855,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   auto run_scan = [&]() -> uint32_t {
     nc = hash_mode ? size_t(cap) : size_t(std::max<uint64_t>(ncells, 1));
     zero_table(nc, hash_mode);
-    HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));
+    HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));   // flags + the 64-bit plan-bytes counter behind them
+    P.plan_bytes = reinterpret_cast<unsigned long long*>(P.flags + 2);
     HIP_TRY(hipEventRecord(X->ev_scan0, st));
     const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
     if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
@@ -887,10 +889,11 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
         fprintf(stderr, "[lk stamps] blocks=%zu mean cycles:%s total=%.0f\n", n, line.c_str(), tot);
       }
     }
-    uint32_t fl = 0;
-    HIP_TRY(hipMemcpyAsync(&fl, P.flags, 4, hipMemcpyDeviceToHost, st));
+    uint32_t fl[4] = {0, 0, 0, 0};
+    HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
-    return fl;
+    memcpy(&plan_bytes, fl + 2, 8);
+    return fl[0];
   };
   // Every rank reports (error, flags); a failure anywhere fails every rank (no rank is left in a collective),
   // and every rank sees the OR of the flags (so they re-run a too-small hash table together).
@@ -1167,10 +1170,10 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"table\":\"%s\","
-           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d}",
+           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu}",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size(),
-           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts);
+           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes);
   res->stats = buf;
   return LK_OK;
 }

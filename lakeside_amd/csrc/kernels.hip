@@ -1,4 +1,5 @@
 // HIP kernels for gfx950 (MI355X): sealed-segment DataExpr scan + table finalize/compaction.
+// (The scan kernel's instantiations live in scan_<agg>.hip, one translation unit per aggregate, built in parallel.)
 //
 // scan_tiles<AGG, NSTR>: grid (tile, segment), one 256-thread workgroup per tile (a row range inside one page
 // of every column).  Per-tile column state (page stream offsets, run windows, flags) is read with scalar loads
@@ -23,7 +24,6 @@
 #include "device_common.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
-#include "scan_kernel.hpp"
 
 #include <hipcub/device/device_radix_sort.hpp>
 
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void merge_records(QParams P, const unsigned l
   if (i >= n) return;
   const unsigned long long rows = recs[n + i];
   if (!rows) return;
-  const unsigned long long slot = hash_slot(P.hkeys, P.hmask, P.flags, recs[i]);
+  const unsigned long long slot = hash_slot(P.hkeys, P.hmask, P.flags, recs[i]);   // merge target: hash table
   if (slot == EMPTY) return;
   atomicAdd(&P.rows[slot], rows);
   const unsigned long long cnt = recs[2 * n + i];
@@ -578,32 +578,15 @@ hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws,
   return hipGetLastError();
 }
 
-template <int AGG>
-static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
-  const dim3 block(BLOCK);
-  if (!P.truth) {   // > TT_MAX_LEAVES leaves: one generic instantiation interprets the Kleene program per row
-    hipLaunchKernelGGL((scan_tiles<AGG, MAXSTR, false>), grid, block, 0, st, P);
-    return;
-  }
-  switch (P.nstr) {
-    case 1: hipLaunchKernelGGL((scan_tiles<AGG, 1, true>), grid, block, 0, st, P); break;
-    case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2, true>), grid, block, 0, st, P); break;
-    case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true>), grid, block, 0, st, P); break;
-    case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true>), grid, block, 0, st, P); break;
-    case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true>), grid, block, 0, st, P); break;
-    default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true>), grid, block, 0, st, P); break;
-  }
-}
-
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream) {
   if (P.total_tiles == 0 || P.nsegs == 0) return hipSuccess;
   if (P.nstr < 1 || P.nstr > MAXSTR) return hipErrorInvalidValue;
   const dim3 grid(P.max_tiles, P.nsegs);
   switch (agg) {
-    case AGG_SUM: launch_agg<AGG_SUM>(P, grid, stream); break;
-    case AGG_MIN: launch_agg<AGG_MIN>(P, grid, stream); break;
-    case AGG_MAX: launch_agg<AGG_MAX>(P, grid, stream); break;
-    default: launch_agg<AGG_COUNT>(P, grid, stream); break;
+    case AGG_SUM: launch_scan_agg<AGG_SUM>(P, grid, stream); break;
+    case AGG_MIN: launch_scan_agg<AGG_MIN>(P, grid, stream); break;
+    case AGG_MAX: launch_scan_agg<AGG_MAX>(P, grid, stream); break;
+    default: launch_scan_agg<AGG_COUNT>(P, grid, stream); break;
   }
   return hipGetLastError();
 }

@@ -104,6 +104,9 @@ hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws,
 hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
                                hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
+// one aggregate's scan instantiations (scan_<agg>.hip)
+template <int AGG>
+void launch_scan_agg(const QParams& P, dim3 grid, hipStream_t st);
 uint32_t finalize_blocks(unsigned long long nkeys);
 // d_counts must hold finalize_blocks(nkeys) + 1 entries; the row total lands in d_counts[nblocks].
 // Split form: count + scan (row total at d_counts[nblocks]), then write -- the write may target mapped pinned host

@@ -155,6 +155,10 @@ struct QParams {
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
+  // Plan bytes (the roofline numerator): bytes the late-materialized plan must read from HBM, counted
+  // by the kernel: tile metadata + staged runs + dictionary lookups, every fully decoded stream of a tile, and the
+  // distinct 128-B lines touched by the per-row gathers (timestamps, values, late columns).
+  unsigned long long* plan_bytes;
 };
 
 enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u };

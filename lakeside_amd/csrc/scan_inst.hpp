@@ -1,0 +1,34 @@
+// Instantiations of the fused scan kernel (scan_kernel.hpp) for one aggregate; included by scan_<agg>.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "scan_kernel.hpp"
+
+namespace lk {
+
+template <int AGG, bool HASH>
+static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
+  const dim3 block(BLOCK);
+  if (!P.truth) {   // > TT_MAX_LEAVES leaves: one generic instantiation interprets the Kleene program per row
+    hipLaunchKernelGGL((scan_tiles<AGG, MAXSTR, false, HASH>), grid, block, 0, st, P);
+    return;
+  }
+  switch (P.nstr) {
+    case 1: hipLaunchKernelGGL((scan_tiles<AGG, 1, true, HASH>), grid, block, 0, st, P); break;
+    case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2, true, HASH>), grid, block, 0, st, P); break;
+    case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true, HASH>), grid, block, 0, st, P); break;
+    case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true, HASH>), grid, block, 0, st, P); break;
+    case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true, HASH>), grid, block, 0, st, P); break;
+    default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH>), grid, block, 0, st, P); break;
+  }
+}
+
+template <int AGG>
+void launch_scan_agg(const QParams& P, dim3 grid, hipStream_t st) {
+  if (P.hkeys) launch_agg<AGG, true>(P, grid, st);
+  else launch_agg<AGG, false>(P, grid, st);
+}
+
+}  // namespace lk

@@ -74,7 +74,7 @@ struct Lds {
   unsigned long long stamp[LK_NSTAMP];   // diagnostics only
 };
 
-template <int AGG, int NSTR>
+template <int AGG, int NSTR, bool HASH>
 __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const Acc& a) {
   if (a.rows == 0) return;
   uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (hcap_v<NSTR> - 1);
@@ -101,7 +101,7 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const 
     h = (h + 1) & (hcap_v<NSTR> - 1);
   }
   L.hfull = 1u;                                                     // benign race: any writer stores 1
-  global_merge<AGG>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
+  global_merge<AGG, HASH>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
 }
 
 // Kleene evaluation of the postfix program (filters with more than TT_MAX_LEAVES leaves).
@@ -137,6 +137,19 @@ __device__ __forceinline__ bool interpret(const QParams& P, uint32_t T, uint32_t
 template <class T>
 __device__ __forceinline__ const T* uptr(const T* p) {
   return reinterpret_cast<const T*>(uni_ptr(reinterpret_cast<const uint8_t*>(p)));
+}
+
+// Distinct 128-B lines among the wave's gather offsets (page streams start 128-B aligned, so a stream offset >> 7
+// is its HBM line; live lanes hold non-decreasing offsets, the listed rows being in row order), not counting the
+// line the wave's previous gather of the same stream ended on: the plan-bytes counter's unit for a per-row gather.
+__device__ __forceinline__ uint32_t new_lines(bool live, uint32_t off, uint32_t& last) {
+  const uint32_t line = off >> 7;
+  const uint32_t prev = __shfl_up(line, 1, 64);
+  const unsigned long long m = __ballot(live);
+  const bool fresh = live && (__lane_id() == 0 ? line != last : line != prev);
+  const uint32_t n = uint32_t(__popcll(__ballot(fresh)));
+  if (m) last = __builtin_amdgcn_readlane(line, 63 - __clzll(m));
+  return n;
 }
 
 // Exclusive prefix over the wave's lanes of a count in 0..15, and the wave total (uniform): one ballot per bit.
@@ -249,7 +262,7 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
   return bits;
 }
 
-template <int AGG, int NSTR, bool TT>
+template <int AGG, int NSTR, bool TT, bool HASH>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : (NSTR <= 3 ? 3 : 2)))) void scan_tiles(QParams P) {
   __shared__ Lds<NSTR> L;
   constexpr int NC = 2 + NSTR;
@@ -376,6 +389,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     L.stamp[k] += now_ - st_mark;                                  \
     st_mark = now_;                                                \
   }
+
+  // plan bytes of this wave (uniform): wave 0 accounts the tile's metadata reads (TileDesc, TileCols, staged
+  // runs, dictionary lookups); every wave its own gathers
+  uint64_t pbytes = 0;
+  if (wave == 0) {
+    pbytes += sizeof(TileDesc);
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+      if (!uni(L.hot[c].present)) continue;
+      pbytes += sizeof(TileCol) + uint64_t(c >= 2 ? uni(L.hot[c].nruns) : 0u) * sizeof(RunDesc) +
+                uint64_t(uni(L.hot[c].ndruns)) * sizeof(RunDesc) + (uni(L.hot[c].lut_on) ? uint64_t(uni(L.hot[c].dict_n)) * 8u : 0u);
+    }
+  }
+  uint32_t last_ts_line = ~0u, last_v_line = ~0u;
 
   // per-tile column flags as scalar bit masks (bit c): present, has NULLs, small-dictionary lookup in LDS
   uint32_t presm = 0, nullm = 0, lutm = 0;
@@ -513,8 +540,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const bool vok = live && ((en.y >> 22) & 1u);
       ch.vok |= uint32_t(vok) << j;
       ch.live |= uint32_t(live) << j;
-      if (!one_bucket) ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-      if (AGG != AGG_COUNT) ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
+      if (!one_bucket) {
+        ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+        pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
+      }
+      if (AGG != AGG_COUNT) {
+        ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
+        pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
+      }
     }
   };
   // One row per lane (the late stage's survivors, in place: no compaction), slot 0.
@@ -531,8 +564,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     const bool vok = live && ((ey >> 22) & 1u);
     ch.vok = uint32_t(vok);
     ch.live = uint32_t(live);
-    if (!one_bucket) ch.ts[0] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-    if (AGG != AGG_COUNT) ch.v[0] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
+    if (!one_bucket) {
+      ch.ts[0] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
+      pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
+    }
+    if (AGG != AGG_COUNT) {
+      ch.v[0] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
+      pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
+    }
   };
   auto consume = [&](const Chunk& ch) {
 #pragma unroll
@@ -574,7 +613,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       }
       const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
       if (cell != acc.key) {
-        lds_merge<AGG>(L, P, acc);
+        lds_merge<AGG, NSTR, HASH>(L, P, acc);
         acc_reset<AGG>(acc, cell);
       }
       const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
@@ -620,6 +659,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
       const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
       lp.w[k] = __builtin_amdgcn_raw_buffer_load_b64(vrs, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      uint32_t no_carry = ~0u;   // late columns' packed words: lines of this chunk (runs revisit lines rarely)
+      pbytes += 128u * new_lines(live && lit, byte & ~3u, no_carry);
       lp.meta[k] = lit ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : r.value;
     }
   };
@@ -784,6 +825,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       LK_STAMP(3)
     }
 
+    // plan bytes of the streams decoded in full for this sub-tile (wave 0): def levels, early string columns
+    if (wave == 0) {
+#pragma unroll
+      for (int c = 0; c < NC; c++)
+        if ((nullm >> c) & 1u) pbytes += (nsub + 7u) / 8u;
+#pragma unroll
+      for (int s2 = 0; s2 < NSTR; s2++) {
+        const int c = 2 + s2;
+        if (((skipm >> s2) & 1u) || !((presm >> c) & 1u) || !uni(L.hot[c].nruns)) continue;
+        pbytes += (uint64_t(ctot[c]) * uni(L.hot[c].bw) + 7u) / 8u;
+      }
+    }
+
     // ============ C. filter -> pass byte (NULL / absent timestamps fail the window) ============
     uint32_t passb = 0;
     if (fast) {
@@ -916,11 +970,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
 #pragma unroll
     for (int k = 0; k < LK_NSTAMP; k++) o[k] = L.stamp[k] | (k == 0 ? 1ull << 63 : 0ull);   // bit 63: block ran
   }
-  lds_merge<AGG>(L, P, acc);
+  if (P.plan_bytes && lane == 0 && pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
+  lds_merge<AGG, NSTR, HASH>(L, P, acc);
   __syncthreads();
   for (int i = tid; i < hcap_v<NSTR>; i += BLOCK) {
     if (L.hkey[i] == EMPTY) continue;
-    global_merge<AGG>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
+    global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
                       reinterpret_cast<unsigned long long*>(L.hhi)[i]);
   }
 }
