@@ -832,6 +832,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
   const uint32_t* d_maps = reinterpret_cast<const uint32_t*>(dbuf + o_maps);
   const int kagg = agg == AGG_AVG ? AGG_SUM : (agg == AGG_ROWS ? AGG_COUNT : agg);
+  // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
+  if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
+    P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
 
   // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
   size_t nc = 0;
@@ -856,7 +859,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     nc = hash_mode ? size_t(cap) : size_t(std::max<uint64_t>(ncells, 1));
     zero_table(nc, hash_mode);
     HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));   // flags + the 64-bit plan-bytes counter behind them
-    P.plan_bytes = reinterpret_cast<unsigned long long*>(P.flags + 2);
+    P.plan_bytes = getenv("LK_NO_PLANBYTES") ? nullptr : reinterpret_cast<unsigned long long*>(P.flags + 2);
     HIP_TRY(hipEventRecord(X->ev_scan0, st));
     const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
     if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals
@@ -866,6 +869,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     launch_ms = ms_since(t_start);   // host staging done, scan enqueued
     if (ncells) HIP_TRY(launch_scan(P, kagg, st));
     HIP_TRY(hipEventRecord(X->ev_scan1, st));
+    if (ncells) HIP_TRY(launch_fixup_table(P, nc, kagg, st));
     if (P.stamps) {
       std::vector<unsigned long long> h(nstamp);
       HIP_TRY(hipMemcpyAsync(h.data(), P.stamps, nstamp * 8, hipMemcpyDeviceToHost, st));

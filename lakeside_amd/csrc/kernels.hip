@@ -461,6 +461,22 @@ __global__ __launch_bounds__(SB) void table_records(SParams S, const uint32_t* b
   }
 }
 
+// Lean tables (LEAN_*): restore rows / cnt after the scan.  NO_ROWS (min/max, no NULL values): a cell exists iff
+// its extreme left the identity; its SQL count is then >= 1 (only existence is read downstream).  NO_CNT: cnt = rows.
+__global__ __launch_bounds__(256) void fixup_table(QParams P, unsigned long long nc, int agg) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= nc) return;
+  if (P.hkeys && P.hkeys[i] == EMPTY) return;
+  if (P.lean & LEAN_NO_ROWS) {
+    const unsigned long long ident = agg == AGG_MIN ? ~0ull : 0ull;
+    const unsigned long long e = P.ext[i] != ident ? 1ull : 0ull;
+    P.rows[i] = e;
+    P.cnt[i] = e;
+  } else if (P.lean & LEAN_NO_CNT) {
+    P.cnt[i] = P.rows[i];
+  }
+}
+
 // ------------------------------------------------------------------------------------------------
 // Host launchers
 // ------------------------------------------------------------------------------------------------
@@ -487,6 +503,12 @@ hipError_t launch_merge_records(const QParams& P, const unsigned long long* recs
     case AGG_MAX: hipLaunchKernelGGL(merge_records<AGG_MAX>, g, b, 0, st, P, recs, n); break;
     default: hipLaunchKernelGGL(merge_records<AGG_COUNT>, g, b, 0, st, P, recs, n); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_fixup_table(const QParams& P, unsigned long long nc, int agg, hipStream_t st) {
+  if (!P.lean || nc == 0) return hipSuccess;
+  hipLaunchKernelGGL(fixup_table, dim3(uint32_t((nc + 255) / 256)), dim3(256), 0, st, P, nc, agg);
   return hipGetLastError();
 }
 

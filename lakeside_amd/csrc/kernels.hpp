@@ -104,6 +104,8 @@ hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws,
 hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
                                hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
+// lean tables: restore the rows / cnt fields the scan did not accumulate (LEAN_* in layout.hpp)
+hipError_t launch_fixup_table(const QParams& P, unsigned long long nc, int agg, hipStream_t stream);
 // one aggregate's scan instantiations (scan_<agg>.hip)
 template <int AGG>
 void launch_scan_agg(const QParams& P, dim3 grid, hipStream_t st);

@@ -152,6 +152,7 @@ struct QParams {
   // table whose slot keys are `hkeys` (EMPTY = ~0); null: dense mode (array index = cell key)
   unsigned long long* hkeys;
   unsigned long long hmask;         // slots - 1 (a power of two)
+  uint32_t lean;                    // LEAN_* bits: table fields the scan leaves to the fix-up pass (fewer atomics)
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
@@ -162,6 +163,11 @@ struct QParams {
 };
 
 enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u };
-constexpr uint32_t HASH_MAX_PROBE = 4096;   // linear probes before a hash-mode insert reports the table full
+constexpr uint32_t HASH_MAX_PROBE = 4096;
+// Lean tables: with no NULL value in the query's value column, a cell's non-NULL count equals its row count
+// (LEAN_NO_CNT: `cnt` is not accumulated), and for min/max a cell exists iff its extreme left the identity
+// (LEAN_NO_ROWS: neither `rows` nor `cnt` is accumulated).  fixup_table restores both after the scan, so every
+// later stage (merge, finalize) reads an ordinary table.  Each dropped field is one memory-side atomic per flush.
+constexpr uint32_t LEAN_NO_CNT = 1u, LEAN_NO_ROWS = 2u;   // linear probes before a hash-mode insert reports the table full
 
 }  // namespace lk

@@ -393,7 +393,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   // plan bytes of this wave (uniform): wave 0 accounts the tile's metadata reads (TileDesc, TileCols, staged
   // runs, dictionary lookups); every wave its own gathers
   uint64_t pbytes = 0;
-  if (wave == 0) {
+  const bool count_plan = P.plan_bytes != nullptr;   // uniform
+  if (wave == 0 && count_plan) {
     pbytes += sizeof(TileDesc);
 #pragma unroll
     for (int c = 0; c < NC; c++) {
@@ -542,11 +543,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       ch.live |= uint32_t(live) << j;
       if (!one_bucket) {
         ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-        pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
+        if (count_plan) pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
       }
       if (AGG != AGG_COUNT) {
         ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
-        pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
+        if (count_plan) pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
       }
     }
   };
@@ -566,11 +567,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     ch.live = uint32_t(live);
     if (!one_bucket) {
       ch.ts[0] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
-      pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
+      if (count_plan) pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
     }
     if (AGG != AGG_COUNT) {
       ch.v[0] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
-      pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
+      if (count_plan) pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
     }
   };
   auto consume = [&](const Chunk& ch) {
@@ -660,7 +661,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const __amdgpu_buffer_rsrc_t vrs = make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8);
       lp.w[k] = __builtin_amdgcn_raw_buffer_load_b64(vrs, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
       uint32_t no_carry = ~0u;   // late columns' packed words: lines of this chunk (runs revisit lines rarely)
-      pbytes += 128u * new_lines(live && lit, byte & ~3u, no_carry);
+      if (count_plan) pbytes += 128u * new_lines(live && lit, byte & ~3u, no_carry);
       lp.meta[k] = lit ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : r.value;
     }
   };
@@ -826,7 +827,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     }
 
     // plan bytes of the streams decoded in full for this sub-tile (wave 0): def levels, early string columns
-    if (wave == 0) {
+    if (wave == 0 && count_plan) {
 #pragma unroll
       for (int c = 0; c < NC; c++)
         if ((nullm >> c) & 1u) pbytes += (nsub + 7u) / 8u;
