@@ -47,7 +47,7 @@ clean:
 	rm -rf build $(LIB) $(SYNTH) $(RELIB)
 
 
-.PHONY: all clean asm
+.PHONY: all clean asm exp-depth3
 
 # CPU restatement of the evaluator (oracle: test / bench-baseline infrastructure only, never the product path)
 CPULIB = oracle/liblkcpu.so
@@ -55,3 +55,9 @@ $(CPULIB): oracle/cpu/lkcpu.cpp
 	g++ -O3 -std=c++17 -fPIC -fopenmp -shared -Wall -Wextra -Wno-unused-parameter -o $@ $<
 
 all: $(CPULIB)
+
+# Kernel A/B builds (experiments): the library with another software-pipeline depth, lakeside_amd/exp/ (LK_LIB_PATH).
+exp-depth3:
+	@mkdir -p build/exp/obj lakeside_amd/exp
+	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) '-DLK_DEPTH(n)=3' -c $(SRC)/scan_$$a.hip -o build/exp/obj/scan_$$a.o & done; wait
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_d3.so $(HOST_OBJS) $(OBJDIR)/kernels.o build/exp/obj/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib

@@ -37,6 +37,8 @@ enum {
 /* Flags of lk_eval_pushdown. */
 #define LK_PER_GLOB_ROWS 1u   /* rows of every glob separately (the worker's output, S17) */
 #define LK_MERGED 2u          /* cells merged across globs as query-api does (TimeGroupedSketchAggregator, S19) */
+#define LK_PLAN_BYTES 4u      /* optional, with either: the scan kernel counts the bytes its plan reads
+                                 (lk_result_stats "plan_bytes"; measurement only, costs ~5% of scan time) */
 
 /* options_json: {"device": 0, "rank": 0, "world": 1}; NULL = defaults.
  * Replaces DuckDbConnectionFactory (core/.../utils/DuckDbConnectionFactory.scala:76-114). */

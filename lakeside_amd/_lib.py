@@ -6,7 +6,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "liblakeside_gpu.so")
+# LK_LIB_PATH: an alternative build of the same library (kernel A/B experiments only)
+LIB_PATH = os.environ.get("LK_LIB_PATH") or os.path.join(_HERE, "liblakeside_gpu.so")
 SYNTH_PATH = os.path.join(_HERE, "liblakeside_synth.so")
 
 LK_OK = 0
@@ -17,6 +18,7 @@ LK_ERR_DEVICE = -4
 LK_ERR_MEMORY = -5
 LK_PER_GLOB_ROWS = 1
 LK_MERGED = 2
+LK_PLAN_BYTES = 4
 LK_UNIQUE_ID_BYTES = 128
 
 # (name, restype, argtypes) of every symbol the header declares

@@ -859,7 +859,7 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     nc = hash_mode ? size_t(cap) : size_t(std::max<uint64_t>(ncells, 1));
     zero_table(nc, hash_mode);
     HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));   // flags + the 64-bit plan-bytes counter behind them
-    P.plan_bytes = getenv("LK_NO_PLANBYTES") ? nullptr : reinterpret_cast<unsigned long long*>(P.flags + 2);
+    P.plan_bytes = (flags & LK_PLAN_BYTES) ? reinterpret_cast<unsigned long long*>(P.flags + 2) : nullptr;
     HIP_TRY(hipEventRecord(X->ev_scan0, st));
     const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
     if (getenv("LK_STAMPS") && nstamp) {   // diagnostics only: per-block phase cycle totals

@@ -20,6 +20,8 @@
 //   tile end: LDS cells -> global table with device atomics (count/min/max exact, sums within 1 ulp).
 // Without nullable columns the sub-tile loop has no workgroup barrier: the four waves run independently.
 #pragma once
+#include <type_traits>
+
 #include "device_common.hpp"
 
 namespace lk {
@@ -261,6 +263,21 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
   }
   return bits;
 }
+
+#ifndef LK_DEPTH   // software-pipeline depth per string-column count (ring of pending chunks, see the main loop)
+#define LK_DEPTH(nstr) ((nstr) >= 3 ? 1 : 2)
+#endif
+
+// Listed rows of a wave whose timestamp/value loads are in flight: NS slots of 64 rows (one row per lane per slot).
+template <int NS>
+struct ChunkT {
+  static constexpr int kSlots = NS;
+  v2u ts[NS], v[NS];
+  uint32_t gid[NS];
+  uint32_t vok;    // bit j: value j is non-NULL
+  uint32_t live;   // bit j: slot j holds a row
+  uint32_t n;      // listed rows in the chunk (uniform; 0: none)
+};
 
 template <int AGG, int NSTR, bool TT, bool HASH>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : (NSTR <= 3 ? 3 : 2)))) void scan_tiles(QParams P) {
@@ -516,19 +533,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     for (int q = 0; q < k && m; q++) m &= m - 1;
     late_col[k] = m ? uint32_t(__builtin_ctz(m)) : 0xffu;   // string column index, 0xff: slot unused
   }
-  struct Chunk {
-    v2u ts[PSN], v[PSN];
-    uint32_t gid[PSN];
-    uint32_t vok;    // bit j: value j is non-NULL
-    uint32_t live;   // bit j: slot j holds a row
-    uint32_t n;      // slots in use x 64 (uniform)
-  };
-  auto issue = [&](Chunk& ch, uint32_t cb, uint32_t nlist, uint32_t vb0, uint32_t vb1) {
-    ch.n = min(nlist - cb, uint32_t(PSN * 64));
+  using Chunk = ChunkT<PSN>;
+  auto issue = [&](auto& ch, uint32_t cb, uint32_t nlist, uint32_t vb0, uint32_t vb1) {
+    constexpr int NS = std::remove_reference_t<decltype(ch)>::kSlots;
+    ch.n = min(nlist - cb, uint32_t(NS * 64));
     ch.vok = 0;
     ch.live = 0;
 #pragma unroll
-    for (int j = 0; j < PSN; j++) {
+    for (int j = 0; j < NS; j++) {
       ch.ts[j] = v2u{0u, 0u};
       ch.v[j] = v2u{0u, 0u};
       ch.gid[j] = 0;
@@ -552,10 +564,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     }
   };
   // One row per lane (the late stage's survivors, in place: no compaction), slot 0.
-  auto issue_one = [&](Chunk& ch, bool live, uint32_t gid, uint32_t ey, uint32_t vb0, uint32_t vb1) {
+  auto issue_one = [&](auto& ch, bool live, uint32_t gid, uint32_t ey, uint32_t vb0, uint32_t vb1) {
+    constexpr int NS = std::remove_reference_t<decltype(ch)>::kSlots;
     ch.n = 64;
 #pragma unroll
-    for (int j = 0; j < PSN; j++) {
+    for (int j = 0; j < NS; j++) {
       ch.ts[j] = v2u{0u, 0u};
       ch.v[j] = v2u{0u, 0u};
       ch.gid[j] = 0;
@@ -574,9 +587,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       if (count_plan) pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
     }
   };
-  auto consume = [&](const Chunk& ch) {
+  auto consume = [&](const auto& ch) {
+    constexpr int NS = std::remove_reference_t<decltype(ch)>::kSlots;
 #pragma unroll
-    for (int j = 0; j < PSN; j++) {
+    for (int j = 0; j < NS; j++) {
       if (uint32_t(j * 64) >= ch.n) break;                                     // uniform
       const int64_t ts = (int64_t)(((uint64_t)ch.ts[j].y << 32) | ch.ts[j].x);
       bool ok = ((ch.live >> j) & 1u) && (one_bucket || (ts >= win_lo && ts < win_hi));   // BaseExpr.scala:159-161
@@ -621,8 +635,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       acc_add<AGG>(acc, (ch.vok >> j) & 1u, v);
     }
   };
-  Chunk pend;   // the previous sub-tile's first chunk: consumed after this sub-tile's decode
-  pend.n = 0;
+  // Software pipeline: the first 64 listed rows of sub-tile k are issued into ring slot k % DEPTH and consumed
+  // DEPTH sub-tiles later, after that many decodes have overlapped their timestamp/value (or late-column) loads:
+  // the loop is unrolled DEPTH times so every ring slot keeps its own registers (moving a register a load is still
+  // writing would wait for the load).  Further listed rows of a sub-tile (dense filters) stream at once.
+  constexpr int DEPTH = LK_DEPTH(NSTR);
   const bool stream_on = !(P.ablate & 1);
 
   // Late stage (late_ok tiles), one row per lane: the listed row's late columns' packed words in flight.
@@ -707,7 +724,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   LPend lpend;
   lpend.n = 0;
 
-  for (uint32_t sub = 0; sub < tile_nrows; sub += SUBT) {
+  auto step = [&](auto& ring, uint32_t sub) __attribute__((always_inline)) {
     const uint32_t nsub = min(uint32_t(SUBT), tile_nrows - sub);
     const uint32_t r0 = 8u * tid;   // the thread's first row in the sub-tile
     const uint32_t inb = r0 < nsub ? (nsub - r0 >= 8 ? 0xffu : (1u << (nsub - r0)) - 1u) : 0u;
@@ -912,12 +929,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         //   late-column loads of this sub-tile's first 64 listed rows.
         // Further listed rows (dense early filters) run the late stage and stream at once.
         late_done = true;
-        if (stream_on) consume(pend);
-        pend.n = 0;
+        if (stream_on) consume(ring);
+        ring.n = 0;
         if (lpend.n) {
           uint32_t g;
           const bool pass = late_eval(lpend, g);
-          if (stream_on) issue_one(pend, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
+          if (stream_on) issue_one(ring, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
           lpend.n = 0;
         }
         if (nlist) late_issue(lpend, 0, nlist, sub, vb0, vb1);
@@ -927,20 +944,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
           uint32_t g;
           const bool pass = late_eval(lp, g);
           if (stream_on) {
-            Chunk ch;
+            ChunkT<1> ch;
             issue_one(ch, pass, g, lp.en.y, vb0, vb1);
             consume(ch);
           }
         }
       }
     }
-    // The previous sub-tile's first chunk has had this sub-tile's decode to land; this sub-tile's first chunk
-    // is issued now and consumed after the next decode. Further chunks (dense filters) stream at once.
+    // The ring slot's chunk (issued DEPTH sub-tiles ago) has had DEPTH decodes to land; this sub-tile's first
+    // 64 listed rows take its place.  Further chunks (dense filters) stream at once.
     if (stream_on && !late_done) {
-      consume(pend);
-      pend.n = 0;
-      if (nlist) issue(pend, 0, nlist, vb0, vb1);
-      for (uint32_t cb = PSN * 64; cb < nlist; cb += PSN * 64) {
+      consume(ring);
+      ring.n = 0;
+      if (nlist) issue(ring, 0, nlist, vb0, vb1);
+      for (uint32_t cb = 64; cb < nlist; cb += PSN * 64) {
         Chunk ch;
         issue(ch, cb, nlist, vb0, vb1);
         consume(ch);
@@ -952,16 +969,32 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     LK_STAMP(7)
+  };
+  ChunkT<1> q0, q1, q2;
+  q0.n = q1.n = q2.n = 0;
+  for (uint32_t sub = 0; sub < tile_nrows; sub += DEPTH * SUBT) {
+    step(q0, sub);
+    if constexpr (DEPTH > 1) {
+      if (sub + SUBT < tile_nrows) step(q1, sub + SUBT);
+    }
+    if constexpr (DEPTH > 2) {
+      if (sub + 2 * SUBT < tile_nrows) step(q2, sub + 2 * SUBT);
+    }
   }
-  // drain: the last stream chunk, then the last late chunk's survivors
-  consume(pend);
+  // drain: the ring's chunks still in flight, then the last late chunk's survivors
+  if (stream_on) {
+    consume(q0);
+    if constexpr (DEPTH > 1) consume(q1);
+    if constexpr (DEPTH > 2) consume(q2);
+  }
   if constexpr (NSTR > 1) {
     if (lpend.n) {
       uint32_t g;
       const bool pass = late_eval(lpend, g);
       if (stream_on) {
-        issue_one(pend, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
-        consume(pend);
+        ChunkT<1> ch;
+        issue_one(ch, pass, g, lpend.en.y, lpend.vb0, lpend.vb1);
+        consume(ch);
       }
     }
   }
