@@ -59,5 +59,5 @@ all: $(CPULIB)
 # Kernel A/B builds (experiments): the library with another software-pipeline depth, lakeside_amd/exp/ (LK_LIB_PATH).
 exp-depth3:
 	@mkdir -p build/exp/obj lakeside_amd/exp
-	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) '-DLK_DEPTH(n)=3' -c $(SRC)/scan_$$a.hip -o build/exp/obj/scan_$$a.o & done; wait
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_d3.so $(HOST_OBJS) $(OBJDIR)/kernels.o build/exp/obj/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) '-DLK_DEPTH(n)=2' -c $(SRC)/scan_$$a.hip -o build/exp/obj/scan_$$a.o & done; wait
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_d2.so $(HOST_OBJS) $(OBJDIR)/kernels.o build/exp/obj/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib

@@ -15,6 +15,18 @@ static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
     hipLaunchKernelGGL((scan_tiles<AGG, MAXSTR, false, HASH>), grid, block, 0, st, P);
     return;
   }
+  // lean min / max / count with group dims: the SLIM LDS layout (twice the cells)
+  if constexpr (AGG != AGG_SUM) {
+    if (P.lean && P.nstr >= 2) {
+    switch (P.nstr) {
+      case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2, true, HASH, true>), grid, block, 0, st, P); return;
+      case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true, HASH, true>), grid, block, 0, st, P); return;
+      case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true, HASH, true>), grid, block, 0, st, P); return;
+      case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true, HASH, true>), grid, block, 0, st, P); return;
+      default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH, true>), grid, block, 0, st, P); return;
+    }
+    }
+  }
   switch (P.nstr) {
     case 1: hipLaunchKernelGGL((scan_tiles<AGG, 1, true, HASH>), grid, block, 0, st, P); break;
     case 2: hipLaunchKernelGGL((scan_tiles<AGG, 2, true, HASH>), grid, block, 0, st, P); break;

@@ -47,7 +47,13 @@ template <int NSTR>
 constexpr int hcap_v = NSTR == 1 ? HCAP / 2 : HCAP;
 constexpr int RBLK = TILE_ROWS / 64 + 8;         // run-block table entries per string column
 
-template <int NSTR>
+// LDS aggregation table layout.  FULL: rows, non-NULL count, compensated sum (hi, lo) / ordered extreme.  SLIM
+// (lean tables of min / max / count, LEAN_* in layout.hpp): one 8-B value per cell (the ordered extreme, or the
+// row count), so the same LDS holds twice the cells -- high-cardinality :by queries spill half as often.
+template <int NSTR, bool SLIM>
+constexpr int hslots_v = hcap_v<NSTR> * (SLIM ? 2 : 1);
+
+template <int NSTR, bool SLIM = false>
 struct Lds {
   LRun pool[(2 + 2 * NSTR) * RS];        // run windows (+ sentinel): def runs of column c at c*RS, value runs of
                                          //   string column s at (2 + NSTR + s)*RS
@@ -57,11 +63,13 @@ struct Lds {
   uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
   uint32_t truth_e[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   // late materialization: early / late
   uint32_t truth_l[NSTR > 1 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];   //   conjunct tables
-  unsigned long long hkey[hcap_v<NSTR>];
-  uint32_t hrows[hcap_v<NSTR>];
-  uint32_t hcnt[hcap_v<NSTR>];
-  double hhi[hcap_v<NSTR>];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
-  double hlo[hcap_v<NSTR>];
+  static constexpr int H = hslots_v<NSTR, SLIM>;
+  unsigned long long hkey[H];
+  uint32_t hrows[SLIM ? 1 : H];
+  uint32_t hcnt[SLIM ? 1 : H];
+  double hhi[SLIM ? 1 : H];                      // SUM: hi; MIN/MAX: ordered bits (reinterpreted)
+  double hlo[SLIM ? 1 : H];
+  unsigned long long hval[SLIM ? H : 1];         // SLIM: MIN/MAX ordered extreme, COUNT rows
   uint2 list[WAVES][WROWS];              // per wave: passing rows {group id, ts index | value index << 11 |
                                          //   value valid << 22} (indices relative to the sub-tile's values).
                                          // Its first 2 KB per wave double as the wave's pk slots (thread t:
@@ -76,31 +84,39 @@ struct Lds {
   unsigned long long stamp[LK_NSTAMP];   // diagnostics only
 };
 
-template <int AGG, int NSTR, bool HASH>
-__device__ __forceinline__ void lds_merge(Lds<NSTR>& L, const QParams& P, const Acc& a) {
+template <int AGG, int NSTR, bool HASH, bool SLIM>
+__device__ __forceinline__ void lds_merge(Lds<NSTR, SLIM>& L, const QParams& P, const Acc& a) {
   if (a.rows == 0) return;
-  uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (hcap_v<NSTR> - 1);
+  constexpr int H = hslots_v<NSTR, SLIM>;
+  uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (H - 1);
   for (int probe = 0; probe < HPROBE; probe++) {
     unsigned long long prev = atomicCAS(&L.hkey[h], EMPTY, a.key);
     if (probe == 0 && prev != EMPTY && prev != a.key && L.hfull) break;   // table known full: no more probes
     if (prev == EMPTY || prev == a.key) {
-      atomicAdd(&L.hrows[h], a.rows);
-      if (a.cnt) {
-        atomicAdd(&L.hcnt[h], a.cnt);
-        if (AGG == AGG_SUM) {
-          double old = atomicAdd(&L.hhi[h], a.hi);
-          double s, e;
-          two_sum(old, a.hi, s, e);
-          atomicAdd(&L.hlo[h], a.lo + e);
-        } else if (AGG == AGG_MIN) {
-          atomicMin(reinterpret_cast<unsigned long long*>(&L.hhi[h]), a.ext);
-        } else if (AGG == AGG_MAX) {
-          atomicMax(reinterpret_cast<unsigned long long*>(&L.hhi[h]), a.ext);
+      if constexpr (SLIM) {
+        if (AGG == AGG_MIN) atomicMin(&L.hval[h], a.ext);
+        else if (AGG == AGG_MAX) atomicMax(&L.hval[h], a.ext);
+        else atomicAdd(&L.hval[h], (unsigned long long)a.rows);
+        return;
+      } else {
+        atomicAdd(&L.hrows[h], a.rows);
+        if (a.cnt) {
+          atomicAdd(&L.hcnt[h], a.cnt);
+          if (AGG == AGG_SUM) {
+            double old = atomicAdd(&L.hhi[h], a.hi);
+            double s, e;
+            two_sum(old, a.hi, s, e);
+            atomicAdd(&L.hlo[h], a.lo + e);
+          } else if (AGG == AGG_MIN) {
+            atomicMin(reinterpret_cast<unsigned long long*>(&L.hhi[h]), a.ext);
+          } else if (AGG == AGG_MAX) {
+            atomicMax(reinterpret_cast<unsigned long long*>(&L.hhi[h]), a.ext);
+          }
         }
+        return;
       }
-      return;
     }
-    h = (h + 1) & (hcap_v<NSTR> - 1);
+    h = (h + 1) & (H - 1);
   }
   L.hfull = 1u;                                                     // benign race: any writer stores 1
   global_merge<AGG, HASH>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
@@ -265,7 +281,7 @@ __device__ __forceinline__ uint32_t g8_bits(const G8& g, __amdgpu_buffer_rsrc_t 
 }
 
 #ifndef LK_DEPTH   // software-pipeline depth per string-column count (ring of pending chunks, see the main loop)
-#define LK_DEPTH(nstr) ((nstr) >= 3 ? 1 : 2)
+#define LK_DEPTH(nstr) 1
 #endif
 
 // Listed rows of a wave whose timestamp/value loads are in flight: NS slots of 64 rows (one row per lane per slot).
@@ -279,9 +295,10 @@ struct ChunkT {
   uint32_t n;      // listed rows in the chunk (uniform; 0: none)
 };
 
-template <int AGG, int NSTR, bool TT, bool HASH>
+template <int AGG, int NSTR, bool TT, bool HASH, bool SLIM = false>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1 ? 4 : (NSTR <= 3 ? 3 : 2)))) void scan_tiles(QParams P) {
-  __shared__ Lds<NSTR> L;
+  __shared__ Lds<NSTR, SLIM> L;
+  constexpr int HS = hslots_v<NSTR, SLIM>;
   constexpr int NC = 2 + NSTR;
   auto druns = [&](int c) { return L.pool + c * RS; };                  // def-level runs of column c
   auto vruns = [&](int c) { return L.pool + (NSTR + c) * RS; };         // value runs of string column c >= 2
@@ -383,13 +400,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         L.truth_l[i] = P.truth_late[i];
       }
   }
-  for (int i = tid; i < hcap_v<NSTR>; i += BLOCK) {
+  for (int i = tid; i < HS; i += BLOCK) {
     L.hkey[i] = EMPTY;
-    L.hrows[i] = 0;
-    L.hcnt[i] = 0;
-    L.hlo[i] = 0.0;
-    if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
-    else L.hhi[i] = 0.0;
+    if constexpr (SLIM) {
+      L.hval[i] = AGG == AGG_MIN ? ~0ull : 0ull;
+    } else {
+      L.hrows[i] = 0;
+      L.hcnt[i] = 0;
+      L.hlo[i] = 0.0;
+      if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
+      else L.hhi[i] = 0.0;
+    }
   }
   const bool stamp = P.stamps != nullptr;   // diagnostics only
   if (stamp && tid == 0)
@@ -628,7 +649,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       }
       const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
       if (cell != acc.key) {
-        lds_merge<AGG, NSTR, HASH>(L, P, acc);
+        lds_merge<AGG, NSTR, HASH, SLIM>(L, P, acc);
         acc_reset<AGG>(acc, cell);
       }
       const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
@@ -1005,12 +1026,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     for (int k = 0; k < LK_NSTAMP; k++) o[k] = L.stamp[k] | (k == 0 ? 1ull << 63 : 0ull);   // bit 63: block ran
   }
   if (P.plan_bytes && lane == 0 && pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
-  lds_merge<AGG, NSTR, HASH>(L, P, acc);
+  lds_merge<AGG, NSTR, HASH, SLIM>(L, P, acc);
   __syncthreads();
-  for (int i = tid; i < hcap_v<NSTR>; i += BLOCK) {
+  for (int i = tid; i < HS; i += BLOCK) {
     if (L.hkey[i] == EMPTY) continue;
-    global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
-                      reinterpret_cast<unsigned long long*>(L.hhi)[i]);
+    if constexpr (SLIM) {   // lean table: MIN/MAX existence via the extreme, COUNT rows == non-NULL count
+      const unsigned long long v = L.hval[i];
+      if (AGG == AGG_COUNT) global_merge<AGG, HASH>(P, L.hkey[i], uint32_t(v), uint32_t(v), 0.0, 0.0, 0ull);
+      else global_merge<AGG, HASH>(P, L.hkey[i], 1u, 1u, 0.0, 0.0, v);
+    } else {
+      global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
+                              reinterpret_cast<unsigned long long*>(L.hhi)[i]);
+    }
   }
 }
 

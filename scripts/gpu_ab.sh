@@ -10,6 +10,6 @@ fi
 B="python3 bench.py --steps 10 --warmup 3 --cpu-sample 0"
 for q in ${QUERIES:-c2 c3 c4}; do
   timeout -k 10 300 $B --query $q > gpurun_out/ab/${q}_def.json 2> gpurun_out/ab/${q}_def.log || exit $?
-  LK_LIB_PATH=$PWD/lakeside_amd/exp/liblakeside_gpu_d3.so timeout -k 10 300 $B --query $q > gpurun_out/ab/${q}_d3.json 2> gpurun_out/ab/${q}_d3.log || exit $?
+  LK_LIB_PATH=$PWD/lakeside_amd/exp/liblakeside_gpu_d2.so timeout -k 10 300 $B --query $q > gpurun_out/ab/${q}_d2.json 2> gpurun_out/ab/${q}_d2.log || exit $?
 done
 grep -H "scan kernel" gpurun_out/ab/*.log | sed 's/in the call.*//'
