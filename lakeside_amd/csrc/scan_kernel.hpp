@@ -212,7 +212,7 @@ __device__ __forceinline__ int find_run_blk(const LRun* runs, const uint8_t* blk
 __device__ __forceinline__ G8 g8_issue(__amdgpu_buffer_rsrc_t rs, const LRun* runs, int n, uint32_t v, int bw,
                                        bool wide, const uint8_t* blk = nullptr, uint32_t nb = 0, uint32_t vbase = 0) {
   G8 g;
-  g.ri = blk ? find_run_blk(runs, blk, nb, vbase, v) : find_run(runs, n, v);
+  g.ri = n == 1 ? 0 : (blk ? find_run_blk(runs, blk, nb, vbase, v) : find_run(runs, n, v));   // n: uniform
   const LRun r = runs[g.ri];
   const bool fast = (r.off_lit & 0x80000000u) != 0 && v + 8 <= runs[g.ri + 1].start && bw <= 8;
   const uint32_t byte = (r.off_lit & 0x7fffffffu) + (((v - r.start) * uint32_t(bw)) >> 3);
@@ -480,6 +480,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     }
     emask = __ballot(pass);
   }
+  const bool emask32 = fast && uni(L.hot[2 + ecol].dict_n) <= 32u;   // uniform
+  const uint32_t emask_lo = uint32_t(emask);
 
   // Per column: index (tile-relative) of the sub-tile's first value: its first row for a column without
   // NULLs, the running non-NULL count for a nullable one.
@@ -692,7 +694,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       const LRun* runs = vruns(int(c));
       const uint32_t vb = uni(L.hot[c].vbase);
       const uint32_t v = vb + sub + row;                                    // no NULLs: value index = row
-      const LRun r = runs[find_run_blk(runs, L.rblk[sl], nblk, vb, v)];
+      const LRun r = runs[nr == 1 ? 0 : find_run_blk(runs, L.rblk[sl], nblk, vb, v)];
       const bool lit = (r.off_lit & 0x80000000u) != 0;
       const uint32_t bit = (v - r.start) * uni(L.hot[c].bw);
       const uint32_t byte = (r.off_lit & 0x7fffffffu) + (bit >> 3);
@@ -799,10 +801,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         g8_unpack(gv[s], make_rsrc(L.hot[c].vals, L.hot[c].vals_len + 8), vruns(c),
                   int(uni(L.hot[c].nruns)), uni(L.hot[c].vbase) + vrun[c] + r0, int(uni(L.hot[c].bw)),
                   ctot[c] > r0 ? ctot[c] - r0 : 0u, own, [](uint32_t i) { return i; }, dec);
+        if (emask32) {   // <= 32 codes: one 32-bit shift per row
 #pragma unroll
-        for (int e = 0; e < 8; e++) {
-          gid[e] = dec[e];
-          passf |= uint32_t((emask >> (dec[e] & 63u)) & 1ull) << e;
+          for (int e = 0; e < 8; e++) {
+            gid[e] = dec[e];
+            passf |= ((emask_lo >> (dec[e] & 31u)) & 1u) << e;
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 8; e++) {
+            gid[e] = dec[e];
+            passf |= uint32_t((emask >> (dec[e] & 63u)) & 1ull) << e;
+          }
         }
         continue;
       }
@@ -904,16 +914,32 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     uint32_t nlist;
     {
       uint32_t k = wave_prefix16(__popc(passb), nlist);
-      uint32_t tv = vfirst[0], vv = vfirst[1];
+      if (!(nullm & 3u)) {
+        // no NULL timestamps / values here: value index = row; a loop over the set pass bits (sparse filters
+        // write few entries; the loop runs max-popcount times, not 8)
+        const uint32_t vok_all = (vb[1] != 0u) ? 1u : 0u;   // value column present on this tile
+        uint32_t m = passb;
+        while (m) {
+          const uint32_t e = uint32_t(__builtin_ctz(m));
+          m &= m - 1u;
+          uint32_t g = gid[0];
 #pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const uint32_t vok = (vb[1] >> e) & 1u;
-        if ((passb >> e) & 1u) {
-          wlist[k] = make_uint2(gid[e], tv | (vv << 11) | (vok << 22));
-          k++;
+          for (int q = 1; q < 8; q++) g = (e == uint32_t(q)) ? gid[q] : g;
+          const uint32_t r = r0 + e;
+          wlist[k++] = make_uint2(g, r | (r << 11) | (vok_all << 22));
         }
-        tv += (vb[0] >> e) & 1u;
-        vv += vok;
+      } else {
+        uint32_t tv = vfirst[0], vv = vfirst[1];
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const uint32_t vok = (vb[1] >> e) & 1u;
+          if ((passb >> e) & 1u) {
+            wlist[k] = make_uint2(gid[e], tv | (vv << 11) | (vok << 22));
+            k++;
+          }
+          tv += (vb[0] >> e) & 1u;
+          vv += vok;
+        }
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
