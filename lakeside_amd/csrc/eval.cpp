@@ -219,8 +219,30 @@ bool noisy_tag(const std::string& t) {
 
 }  // namespace
 
+namespace {
+// Metrics timestamps off the step grid: the scan is re-run at millisecond granularity (see below).
+struct MetricsUnaligned {};
+}  // namespace
+
+static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
+                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, bool metrics_raw);
+
+// Metrics: the worker groups by the raw timestamp (`GROUP BY "_cardinalhq.timestamp"`, BaseExpr.scala:376-394); the
+// segment index picks segments whose frequency equals the step (`metric_seg.frequency_ms = ?`,
+// QueryEngineV2.scala:746-752), so timestamps normally sit on the step grid and a bucket per step is exact.  When a
+// row's timestamp is off that grid (the kernel flags it; every rank sees the flag), the evaluation runs again with
+// one bucket per millisecond: the cell key is then the raw timestamp (a sparse key space: the hash table).
 int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
              unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
+  try {
+    return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, false);
+  } catch (const MetricsUnaligned&) {   // thrown before anything is written to *res
+    return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, true);
+  }
+}
+
+static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
+                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, bool metrics_raw) {
   auto t_start = std::chrono::steady_clock::now();
   // Distributed calls issue collectives: one at a time per engine, in the same order on every rank.  Every call
   // runs on its own context (stream, workspaces), so local calls from several threads overlap.
@@ -413,6 +435,8 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
 
   // A tag query's single bucket: ts - ts % 2^62 = 0 for every |ts| < 2^62, so bucket_base = 0 and one bucket.
   if (tagq) step = int64_t(1) << 62;
+  // metrics off the step grid: one bucket per millisecond, i.e. the raw timestamp (see evaluate())
+  if (metrics_raw && R.dataset == "metrics" && !tagq) step = 1;
 
   // ---- group dimensions ----
   const bool merged = !per_glob_rows;
@@ -835,6 +859,9 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
   if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
+  // single string column (filter and group dim on `name` only): NULL-free tiles with a small chunk dictionary go
+  // to scan_lean (lean_kernel.hpp), the rest to scan_tiles
+  P.lean_split = (P.nstr == 1 && P.truth && agg != AGG_ROWS && !getenv("LK_NO_LEAN_SPLIT")) ? 1u : 0u;
 
   // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
   size_t nc = 0;
@@ -945,8 +972,10 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
     }
     break;
   }
-  if (hflags & FLAG_METRICS_UNALIGNED)
-    throw PlanError(LK_ERR_UNSUPPORTED, "metrics timestamps not aligned to the step (round 1 needs frequency == step)");
+  if (hflags & FLAG_METRICS_UNALIGNED) {
+    if (step == 1) throw PlanError(LK_ERR_DEVICE, "internal: metrics timestamp off a 1 ms grid");
+    throw MetricsUnaligned{};
+  }
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
   if (hflags & FLAG_HASH_FULL) throw PlanError(LK_ERR_MEMORY, "aggregation hash table full at its bound");
 

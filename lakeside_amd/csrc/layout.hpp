@@ -152,6 +152,7 @@ struct QParams {
   // table whose slot keys are `hkeys` (EMPTY = ~0); null: dense mode (array index = cell key)
   unsigned long long* hkeys;
   unsigned long long hmask;         // slots - 1 (a power of two)
+  uint32_t lean_split;              // 1: scan_lean takes the lean tiles (lean_tile), scan_tiles skips them
   uint32_t lean;                    // LEAN_* bits: table fields the scan leaves to the fix-up pass (fewer atomics)
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode

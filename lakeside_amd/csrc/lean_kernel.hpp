@@ -1,0 +1,390 @@
+// scan_lean<AGG, HASH>: the single-string-column scan (C2's shape: filter and group dim on `name` only) over the
+// tiles where that column needs no general machinery.  Included by scan_inst.hpp; the general scan_tiles kernel
+// skips these tiles (QParams.lean_split).
+//
+// A tile is "lean" when, over it, the timestamp, value and name columns hold no NULL (value index = row) and
+// the name column's chunk dictionary has at most 64 entries packed in at most 6 bits.  Then the filter outcome is a
+// function of the 6-bit code alone: a 64-bit mask of passing codes (one ballot over the chunk dictionary).
+//
+// Work unit: a 16-value chunk of one hybrid run (bit-packed chunks start on a byte boundary: 16 codes = 2*BW bytes),
+// one chunk per thread per round, chunks of every useful run of the tile flattened into one index space (an RLE
+// run of a failing code contributes no chunk at all).  Per chunk:
+//   one 16-B buffer load of the packed codes -> a pass mask:  SWAR (BW = 1, 2, 4, at most 4 passing codes: per
+//   32-bit word, xor with the code repeated, zero-field detect) or per code (a bit test of the pass mask);
+//   the passing rows (a divergent loop, two rows per trip) gather their value (and timestamp when the tile's zone
+//   map does not pin a single bucket) and accumulate into a per-thread register cell, spilling to an LDS table.
+// No list compaction, no workgroup barrier in the main loop.  VALU per row is a fraction of scan_tiles' (which
+// decodes every column generally, compacts rows through LDS and stages a late stage).
+#pragma once
+#include <type_traits>
+
+#include "device_common.hpp"
+
+namespace lk {
+
+constexpr int LEAN_H = HCAP / 2;                                 // LDS cells (a tile touches few)
+constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a tile, upper bound
+constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
+
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+
+struct LeanRun {            // one run of the name column over the tile (24 B)
+  uint32_t start;           // first value index (page-relative)
+  uint32_t off_lit;         // bit 31: bit-packed; bits 0..30: byte offset in the value stream
+  uint32_t value;           // RLE: the code
+  uint32_t lo, hi;          // value range of the run inside the tile
+  uint32_t cbk;             // chunk index of the run's chunk k = 0 (so k = q - cbk)
+};
+
+struct LeanLds {
+  static constexpr int H = LEAN_H;
+  LeanRun runs[RUN_CAP];
+  uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
+  uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
+  uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
+  unsigned long long hkey[H];
+  uint32_t hrows[H];
+  uint32_t hcnt[H];
+  double hhi[H];
+  double hlo[H];
+  unsigned long long hval[1];
+  uint32_t hfull;
+  uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
+};
+
+// The tile qualifies for scan_lean (uniform: scalar loads).  scan_tiles applies the same test to skip it.
+__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t) {
+  if (!Sp->cols[0].present || !Sp->cols[1].present || !Sp->cols[2].present) return false;
+  const TileCol* a = Sp->cols[0].tcols + t;
+  const TileCol* b = Sp->cols[1].tcols + t;
+  const TileCol* c = Sp->cols[2].tcols + t;
+  return !a->has_nulls && !b->has_nulls && !c->has_nulls && c->kind == PAGE_DICT && c->dict_n <= 64u &&
+         c->nruns > 0u && c->bw >= 1u && c->bw <= 6u;
+}
+
+// Code e (0..15) of a 16-code window of BW-bit fields held in w0..w2 (by value: no address-taken selects).
+template <uint32_t BW>
+__device__ __forceinline__ uint32_t lean_code(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t e) {
+  const uint32_t bit = e * BW, wi = bit >> 5, off = bit & 31u;
+  const uint32_t lo = wi == 0 ? w0 : (wi == 1 ? w1 : w2);
+  const uint32_t hi = wi == 0 ? w1 : (wi == 1 ? w2 : 0u);
+  return __builtin_amdgcn_alignbit(hi, lo, off) & ((1u << BW) - 1u);
+}
+
+template <int AGG, bool HASH>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void scan_lean(QParams P) {
+  __shared__ LeanLds L;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const QSeg* Sp = P.segs + blockIdx.y;
+  const uint32_t t = blockIdx.x;
+  if (t >= Sp->ntiles) return;
+  const TileDesc* tdp = Sp->tiles + t;
+  const int64_t win_lo = Sp->win_lo, win_hi = Sp->win_hi;
+  if (tdp->ts_max < win_lo || tdp->ts_min >= win_hi) return;    // zone map: outside the glob window
+  if (!lean_tile(Sp, t)) return;
+  const TileCol* tc0 = Sp->cols[0].tcols + t;
+  const TileCol* tc1 = Sp->cols[1].tcols + t;
+  const TileCol* tc2 = Sp->cols[2].tcols + t;
+  const uint32_t nrows = tdp->nrows;
+  const uint32_t nr = tc2->nruns, dict_n = tc2->dict_n, bw = tc2->bw;
+  const uint32_t vb2 = tc2->vbase, vend = vb2 + nrows;
+  const bool count_plan = P.plan_bytes != nullptr;
+  uint64_t pbytes = 0;
+
+  // ---- prologue: code lookup values, LDS table ----
+  {
+    const uint32_t* remap = Sp->cols[2].remap + tc2->remap;
+    const uint32_t* tab = P.strp[0].strtab;
+    if (uint32_t(tid) < dict_n) {
+      const uint32_t g = remap[tid];
+      L.lut[tid] = tab ? tab[g] : g;
+    }
+  }
+  for (int i = tid; i < LeanLds::H; i += BLOCK) {
+    L.hkey[i] = EMPTY;
+    L.hrows[i] = 0;
+    L.hcnt[i] = 0;
+    L.hlo[i] = 0.0;
+    if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
+    else L.hhi[i] = 0.0;
+  }
+  if (count_plan)
+    for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) L.lines_t[i] = L.lines_v[i] = 0u;
+  if (tid == 0) L.hfull = 0u;
+  __syncthreads();
+
+  // passing codes: one ballot per wave over the chunk dictionary (Kleene: the leaves' T/F bits of the code)
+  unsigned long long emask;
+  {
+    bool pass = false;
+    if (uint32_t(lane) < dict_n) {
+      const uint32_t lf = Sp->leaf_false;
+      const uint32_t bits = (L.lut[lane] >> 24) << P.strp[0].lbase;
+      const uint32_t lmask = P.strp[0].lmask;
+      const uint32_t T = bits & lmask & ~lf, F = (~bits & lmask) | lf;
+      const uint32_t ix = T | (F << P.nleaves);
+      pass = (P.truth[ix >> 5] >> (ix & 31)) & 1u;
+    }
+    emask = __ballot(pass);
+  }
+  if (!emask) return;   // no row of the tile passes (uniform: every thread leaves; nothing staged to flush)
+
+  // runs of the tile: value range inside the tile, chunk counts (useful runs only)
+  if (uint32_t(tid) < nr) {
+    const RunDesc r = Sp->cols[2].runs[tc2->run_lo + tid];
+    const uint32_t lo = r.start > vb2 ? r.start : vb2;
+    const uint32_t hi = (r.start + r.count) < vend ? (r.start + r.count) : vend;
+    const bool lit = (r.off_lit & 0x80000000u) != 0u;
+    const bool useful = lo < hi && (lit || ((emask >> (r.value & 63u)) & 1ull));
+    const uint32_t k0 = useful ? (lo - r.start) >> 4 : 0u, k1 = useful ? (hi - r.start + 15u) >> 4 : 0u;
+    L.runs[tid] = LeanRun{r.start, r.off_lit, r.value, lo, hi, k0};
+    L.cb[tid] = k1 - k0;
+    if (count_plan && lit && lo < hi) pbytes += (uint64_t(hi - lo) * bw + 7u) / 8u;   // codes decoded in full
+  }
+  __syncthreads();
+  if (tid < 64) {   // exclusive prefix of the chunk counts (<= 128 runs: two per lane)
+    const uint32_t i0 = 2u * uint32_t(lane), i1 = i0 + 1u;
+    const uint32_t n0 = i0 < nr ? L.cb[i0] : 0u, n1 = i1 < nr ? L.cb[i1] : 0u;
+    uint32_t s = n0 + n1, inc = s;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t o = __shfl_up(inc, d, 64);
+      if (lane >= d) inc += o;
+    }
+    const uint32_t ex = inc - s;
+    const uint32_t tot = __shfl(inc, 63, 64);
+    if (i0 < nr) {
+      L.runs[i0].cbk = ex - L.runs[i0].cbk;
+      L.cb[i0] = ex;
+    }
+    if (i1 < nr) {
+      L.runs[i1].cbk = ex + n0 - L.runs[i1].cbk;
+      L.cb[i1] = ex + n0;
+    }
+    if (lane == 0) L.cb[nr] = tot;
+  }
+  __syncthreads();
+  const uint32_t total = L.cb[nr];   // chunks of the tile
+  for (uint32_t q = tid; q < total; q += BLOCK) {   // chunk -> run: last run whose first chunk <= q
+    uint32_t lo = 0;
+#pragma unroll
+    for (uint32_t st = RUN_CAP / 2; st >= 1; st >>= 1) {
+      const uint32_t m = lo + st;
+      lo = (m < nr && L.cb[m] <= q) ? m : lo;
+    }
+    L.ctab[q] = uint8_t(lo);
+  }
+  __syncthreads();
+
+  // ---- per-row state ----
+  const uint32_t vb0 = tc0->vbase, vb1 = tc1->vbase;
+  const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(Sp->base + tc0->vals, tc0->vals_len);
+  const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(Sp->base + tc1->vals, tc1->vals_len);
+  const __amdgpu_buffer_rsrc_t rs2 = make_rsrc(Sp->base + tc2->vals, tc2->vals_len + 16u);
+  const uint32_t line_t0 = (vb0 * 8u) >> 7, line_v0 = (vb1 * 8u) >> 7;
+  const unsigned long long glob_base = (unsigned long long)Sp->glob_slot * P.nbuckets;
+  const uint32_t stride = P.strp[0].dim_stride;
+  const uint32_t npass = uint32_t(__popcll(emask));
+  const uint32_t code0 = uint32_t(__builtin_ctzll(emask));
+  const uint32_t dim_u = (L.lut[code0] & DIM_MASK) * stride;   // the only passing code's group term
+  int64_t tile_b = -1;                                         // zone map: every row in one bucket
+  {
+    const int64_t tmin = tdp->ts_min, tmax = tdp->ts_max;
+    if (tmin >= win_lo && tmax < win_hi) {
+      if (P.metrics) {
+        if (tmin == tmax && (tmin - P.bucket_base) % P.step == 0) tile_b = (tmin - P.bucket_base) / P.step;
+      } else {
+        const int64_t b0 = ((tmin - tmin % P.step) - P.bucket_base) / P.step;
+        const int64_t b1 = ((tmax - tmax % P.step) - P.bucket_base) / P.step;
+        if (b0 == b1) tile_b = b0;
+      }
+      if (tile_b >= int64_t(P.nbuckets)) tile_b = -1;
+    }
+  }
+  const bool one_bucket = tile_b >= 0;
+  const uint32_t step32 = uint32_t(P.step);
+
+  Acc acc;
+  acc_reset<AGG>(acc, EMPTY);
+  // one passing row: bucket (BaseExpr.scala:159-165 window, 163-165 / 376-394 bucket), cell, register cell
+  auto row = [&](int64_t ts, double v, uint32_t dim) __attribute__((always_inline)) {
+    bool ok = true;
+    int64_t b = tile_b;
+    if (!one_bucket) {
+      ok = ts >= win_lo && ts < win_hi;
+      if (P.fast_div) {
+        const uint32_t d = uint32_t(ts - P.bucket_base);
+        uint32_t qd = uint32_t(double(d) * P.inv_step);
+        int64_t rm = int64_t(d) - int64_t(qd) * step32;
+        qd = rm < 0 ? qd - 1 : (rm >= int64_t(step32) ? qd + 1 : qd);
+        rm = int64_t(d) - int64_t(qd) * step32;
+        if (P.metrics && rm != 0 && ok) {
+          atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
+          ok = false;
+        }
+        b = qd;
+      } else if (ok) {
+        if (P.metrics) {
+          const int64_t d = ts - P.bucket_base;
+          b = d / P.step;
+          if (d - b * P.step != 0) {
+            atomicOr(P.flags, FLAG_METRICS_UNALIGNED);
+            ok = false;
+          }
+        } else {
+          b = ((ts - ts % P.step) - P.bucket_base) / P.step;
+        }
+      }
+      if (!ok) return;
+      if (b < 0 || (uint64_t)b >= P.nbuckets) {
+        atomicOr(P.flags, FLAG_CELL_RANGE);
+        return;
+      }
+    }
+    const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + dim;
+    if (cell != acc.key) {
+      lds_merge<AGG, HASH, false>(L, P, acc);
+      acc_reset<AGG>(acc, cell);
+    }
+    acc_add<AGG>(acc, true, v);
+  };
+
+  auto body = [&](auto bwc) __attribute__((always_inline)) {
+    constexpr uint32_t BW = decltype(bwc)::value;
+    constexpr bool POW2 = BW == 1 || BW == 2 || BW == 4;
+    // SWAR filter: BW | 32, at most 4 passing codes (uniform)
+    const bool swar = POW2 && npass <= 4;
+    constexpr uint32_t REP = BW == 1 ? 0xffffffffu : BW == 2 ? 0x55555555u : 0x11111111u;   // 1 per field
+    constexpr uint32_t HI = BW == 1 ? 0xffffffffu : BW == 2 ? 0xaaaaaaaau : 0x88888888u;    // field high bits
+    uint32_t pc[4];
+    {
+      unsigned long long em = emask;
+#pragma unroll
+      for (int j = 0; j < 4; j++) {
+        pc[j] = em ? uint32_t(__builtin_ctzll(em)) : 0xffffffffu;
+        em &= em ? em - 1 : 0ull;
+      }
+    }
+    for (uint32_t q0 = 0; q0 < total; q0 += BLOCK) {   // uniform trip count
+      const uint32_t q = q0 + uint32_t(tid);
+      const bool live = q < total;
+      const LeanRun R = L.runs[live ? L.ctab[q] : 0u];
+      const uint32_t k = q - R.cbk;
+      const uint32_t v0 = R.start + 16u * k;
+      const uint32_t a = (R.lo > v0 ? R.lo : v0) - v0;
+      const uint32_t bnd = ((R.hi < v0 + 16u) ? R.hi : v0 + 16u) - v0;
+      const uint32_t valid = (live && a < bnd) ? (((1u << bnd) - 1u) & ~((1u << a) - 1u)) : 0u;   // bit e
+      const bool lit = (R.off_lit & 0x80000000u) != 0u;
+      const uint32_t rval = R.value & 63u;
+      const uint32_t byte = (R.off_lit & 0x7fffffffu) + 2u * BW * k;
+      const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      const uint32_t sh = (byte & 3u) * 8u;
+      uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
+      uint32_t w1 = __builtin_amdgcn_alignbit(x.z, x.y, sh);
+      uint32_t w2 = __builtin_amdgcn_alignbit(x.w, x.z, sh);
+      if (!lit) {   // RLE run: every field holds the run's code
+        if constexpr (POW2) {
+          w0 = w1 = rval * REP;
+        }
+      }
+      // pass flags: bit e * S + S - 1 (S = BW for SWAR, 1 per code)
+      unsigned long long m = 0;
+      uint32_t shs = 0;
+      if (swar) {
+        if constexpr (POW2) {
+          constexpr uint32_t LO = ~HI;
+          auto zf = [&](uint32_t y) __attribute__((always_inline)) { return ~(((y & LO) + LO) | y | LO); };   // high bit set <=> field == 0
+          uint32_t z0 = 0, z1 = 0;
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            if (pc[j] == 0xffffffffu) break;   // uniform
+            const uint32_t rp = pc[j] * REP;
+            z0 |= zf(w0 ^ rp);
+            if (BW == 4) z1 |= zf(w1 ^ rp);
+          }
+          // valid rows in field-high-bit form
+          unsigned long long vm = 0;
+#pragma unroll
+          for (int e = 0; e < 16; e++) vm |= (unsigned long long)((valid >> e) & 1u) << (e * BW + BW - 1);
+          m = (((unsigned long long)z1 << 32) | z0) & vm;
+          shs = BW == 1 ? 0u : BW == 2 ? 1u : 2u;
+        }
+      } else {
+        uint32_t f = 0;
+#pragma unroll
+        for (int e = 0; e < 16; e++) {
+          const uint32_t c = lit ? lean_code<BW>(w0, w1, w2, uint32_t(e)) : rval;
+          f |= uint32_t((emask >> c) & 1ull) << e;
+        }
+        m = f & valid;
+      }
+      const uint32_t rbase = v0 - vb2;   // tile row of value v0
+      // passing rows: two per trip (their loads in flight together)
+      while (m) {
+        const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
+        m &= m - 1ull;
+        const bool two = m != 0ull;
+        const uint32_t e2 = two ? (uint32_t(__builtin_ctzll(m)) >> shs) : e1;
+        if (two) m &= m - 1ull;
+        const uint32_t r1 = rbase + e1, r2 = rbase + e2;
+        v2u t1 = v2u{0u, 0u}, t2 = v2u{0u, 0u}, x1 = v2u{0u, 0u}, x2 = v2u{0u, 0u};
+        if (!one_bucket) {
+          t1 = __builtin_amdgcn_raw_buffer_load_b64(rs0, (vb0 + r1) * 8u, 0, 0);
+          t2 = __builtin_amdgcn_raw_buffer_load_b64(rs0, two ? (vb0 + r2) * 8u : OOB, 0, 0);
+        }
+        if (AGG != AGG_COUNT) {
+          x1 = __builtin_amdgcn_raw_buffer_load_b64(rs1, (vb1 + r1) * 8u, 0, 0);
+          x2 = __builtin_amdgcn_raw_buffer_load_b64(rs1, two ? (vb1 + r2) * 8u : OOB, 0, 0);
+        }
+        if (count_plan) {
+          auto mark = [&](uint32_t* bm, uint32_t off, uint32_t line0) __attribute__((always_inline)) {
+            const uint32_t l = (off >> 7) - line0;
+            atomicOr(&bm[l >> 5], 1u << (l & 31u));
+          };
+          if (!one_bucket) {
+            mark(L.lines_t, (vb0 + r1) * 8u, line_t0);
+            if (two) mark(L.lines_t, (vb0 + r2) * 8u, line_t0);
+          }
+          if (AGG != AGG_COUNT) {
+            mark(L.lines_v, (vb1 + r1) * 8u, line_v0);
+            if (two) mark(L.lines_v, (vb1 + r2) * 8u, line_v0);
+          }
+        }
+        uint32_t d1 = dim_u, d2 = dim_u;
+        if (npass > 1) {   // uniform: the rows' codes -> group terms
+          d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
+          d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
+        }
+        row((int64_t)(((uint64_t)t1.y << 32) | t1.x), __longlong_as_double((long long)(((uint64_t)x1.y << 32) | x1.x)), d1);
+        if (two)
+          row((int64_t)(((uint64_t)t2.y << 32) | t2.x), __longlong_as_double((long long)(((uint64_t)x2.y << 32) | x2.x)), d2);
+      }
+    }
+  };
+  switch (bw) {   // uniform
+    case 1: body(std::integral_constant<uint32_t, 1>{}); break;
+    case 2: body(std::integral_constant<uint32_t, 2>{}); break;
+    case 3: body(std::integral_constant<uint32_t, 3>{}); break;
+    case 4: body(std::integral_constant<uint32_t, 4>{}); break;
+    case 5: body(std::integral_constant<uint32_t, 5>{}); break;
+    default: body(std::integral_constant<uint32_t, 6>{}); break;
+  }
+
+  lds_merge<AGG, HASH, false>(L, P, acc);
+  __syncthreads();
+  if (count_plan) {
+    if (tid == 0) {
+      pbytes += sizeof(TileDesc) + 3 * sizeof(TileCol) + uint64_t(nr) * sizeof(RunDesc) + uint64_t(dict_n) * 8u;
+    }
+    for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_t[i]) + __popc(L.lines_v[i]));
+    if (pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
+  }
+  for (int i = tid; i < LeanLds::H; i += BLOCK) {
+    if (L.hkey[i] == EMPTY) continue;
+    global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
+                            reinterpret_cast<unsigned long long*>(L.hhi)[i]);
+  }
+}
+
+}  // namespace lk

@@ -84,10 +84,12 @@ struct Lds {
   unsigned long long stamp[LK_NSTAMP];   // diagnostics only
 };
 
-template <int AGG, int NSTR, bool HASH, bool SLIM>
-__device__ __forceinline__ void lds_merge(Lds<NSTR, SLIM>& L, const QParams& P, const Acc& a) {
+// Merge a register cell into the workgroup's LDS table (any LDS layout with hkey/hrows/hcnt/hhi/hlo/hval/hfull and
+// H slots); a full table sends the cell straight to the global table.
+template <int AGG, bool HASH, bool SLIM, class LT>
+__device__ __forceinline__ void lds_merge(LT& L, const QParams& P, const Acc& a) {
   if (a.rows == 0) return;
-  constexpr int H = hslots_v<NSTR, SLIM>;
+  constexpr int H = LT::H;
   uint32_t h = uint32_t(a.key * 0x9E3779B97F4A7C15ull >> 32) & (H - 1);
   for (int probe = 0; probe < HPROBE; probe++) {
     unsigned long long prev = atomicCAS(&L.hkey[h], EMPTY, a.key);
@@ -121,6 +123,12 @@ __device__ __forceinline__ void lds_merge(Lds<NSTR, SLIM>& L, const QParams& P, 
   L.hfull = 1u;                                                     // benign race: any writer stores 1
   global_merge<AGG, HASH>(P, a.key, a.rows, a.cnt, a.hi, a.lo, a.ext);   // LDS table full: straight to HBM
 }
+
+}  // namespace lk
+
+#include "lean_kernel.hpp"   // scan_lean (uses lds_merge); lean_tile for the split
+
+namespace lk {
 
 // Kleene evaluation of the postfix program (filters with more than TT_MAX_LEAVES leaves).
 __device__ __forceinline__ bool interpret(const QParams& P, uint32_t T, uint32_t F) {
@@ -312,6 +320,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   if (t >= Sp->ntiles) return;
   const TileDesc* tdp = Sp->tiles + t;
   if (tdp->ts_max < Sp->win_lo || tdp->ts_min >= Sp->win_hi) return;   // zone map: outside the glob window
+  if (P.lean_split && lean_tile(Sp, t)) return;                         // scan_lean's tile
   const uint32_t tile_nrows = tdp->nrows;
 
   // ---- stage per-tile column state, run windows, lookup values, truth table; clear the LDS table ----
@@ -651,7 +660,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       }
       const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
       if (cell != acc.key) {
-        lds_merge<AGG, NSTR, HASH, SLIM>(L, P, acc);
+        lds_merge<AGG, HASH, SLIM>(L, P, acc);
         acc_reset<AGG>(acc, cell);
       }
       const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
@@ -1052,7 +1061,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     for (int k = 0; k < LK_NSTAMP; k++) o[k] = L.stamp[k] | (k == 0 ? 1ull << 63 : 0ull);   // bit 63: block ran
   }
   if (P.plan_bytes && lane == 0 && pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
-  lds_merge<AGG, NSTR, HASH, SLIM>(L, P, acc);
+  lds_merge<AGG, HASH, SLIM>(L, P, acc);
   __syncthreads();
   for (int i = tid; i < HS; i += BLOCK) {
     if (L.hkey[i] == EMPTY) continue;

@@ -1,0 +1,131 @@
+"""GPU parity of the §8(f) widenings (metrics specifics, other worker query shapes) against the oracle, through
+the C ABI on the MI355X."""
+import json
+
+import numpy as np
+import pytest
+
+from tests.parity import assert_rows_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _metrics_segments(engine, tmp_path, specs):
+    """Metrics segments (rollup_sum / rollup_max value columns) written by pyarrow; specs = [(hour, aligned)]:
+    aligned timestamps sit on the 60 s step grid, unaligned ones on arbitrary milliseconds."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(77)
+    keys, blobs, segs = [], [], []
+    for i, (hour, aligned) in enumerate(specs):
+        n = 150_000
+        t0 = synth.T0 + hour * synth.HOUR
+        ts = t0 + (60_000 * rng.integers(0, 60, n) if aligned else rng.integers(0, synth.HOUR, n))
+        vals = rng.integers(0, 1000, n).astype(np.float64)
+        t = pa.table({
+            dx.TIMESTAMP: pa.array(np.sort(ts), pa.int64()),
+            "rollup_sum": pa.array(vals, pa.float64(), mask=rng.random(n) < 0.03),
+            "rollup_max": pa.array(vals * 2, pa.float64()),
+            synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 4, n)], pa.string()),
+            synth.SERVICE: pa.array([f"svc-{k:03d}" for k in rng.integers(0, 7, n)], pa.string(),
+                                    mask=rng.random(n) < 0.05),
+        })
+        path = str(tmp_path / f"metrics{i}.parquet")
+        strings = [synth.NAME, synth.SERVICE]
+        pq.write_table(t, path, compression="NONE", use_dictionary=strings,
+                       column_encoding={c: "PLAIN" for c in t.column_names if c not in strings},
+                       row_group_size=50_000, data_page_size=65536)
+        engine.load_segment(path)
+        keys.append(path)
+        blobs.append(open(path, "rb").read())
+        segs.append(synth.segment_request(i, hour=hour, dataset="metrics"))
+    return keys, blobs, segs
+
+
+def test_metrics_unaligned_timestamps(engine, tmp_path):
+    """Metrics group by the raw timestamp (BaseExpr.scala:376-394).  Off-grid timestamps (a segment whose
+    frequency is not the step) give one row per distinct timestamp, as the worker's SQL does; the engine re-runs
+    the scan at millisecond granularity (hash table).  On-grid segments alongside keep their rows."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    keys, blobs, segs = _metrics_segments(engine, tmp_path, [(0, True), (1, False), (0, False)])
+    for filt, agg, gbs, rollup in [(synth.leaf(synth.NAME, "eq", "metric_01"), "sum", [synth.SERVICE], None),
+                                   (synth.leaf(synth.NAME, "in", "metric_02", "metric_03"), "max", [], "max")]:
+        req = synth.pushdown(filt, segs, agg, gbs, dataset="metrics")
+        if rollup:
+            req["baseExpr"]["chart"]["rollup"] = rollup
+        req = json.dumps(req)
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 2, keys, sources=blobs)
+        got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS).per_glob(len(cells))
+        assert sum(len(cs) for cs in cells) > 10_000           # raw timestamps: many rows
+        for gi, (g, cs) in enumerate(zip(got, cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"metrics glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, "metrics merged")
+        ts = [r[0] for r in merged.rows()]
+        assert ts == sorted(ts)
+
+
+def test_lean_kernel_shapes(engine, tmp_path):
+    """scan_lean (single string column, NULL-free tiles, chunk dictionaries of <= 64 codes): every code width 1..6,
+    RLE runs (sorted names), SWAR (<= 4 passing codes of a power-of-two width) and per-code filters, multi-bucket
+    tiles (1 s step), a window cutting tiles, every aggregate; GPU == oracle, and == the general kernel
+    (LK_NO_LEAN_SPLIT) bit for bit."""
+    import os
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(5)
+    keys, blobs, segs = [], [], []
+    for i, (card, sort) in enumerate([(2, False), (5, False), (8, False), (16, False), (40, False), (64, False),
+                                      (16, True)]):
+        n = 120_000
+        t0 = synth.T0 + (i % 4) * synth.HOUR
+        codes = rng.integers(0, card, n)
+        if sort:   # long RLE runs
+            codes = np.sort(codes)
+        t = pa.table({
+            dx.TIMESTAMP: pa.array(np.sort(rng.integers(t0, t0 + synth.HOUR, n)), pa.int64()),
+            dx.VALUE: pa.array(rng.lognormal(0.0, 2.0, n), pa.float64()),
+            synth.NAME: pa.array([f"metric_{k:02d}" for k in codes], pa.string()),
+        })
+        path = str(tmp_path / f"lean{i}.parquet")
+        pq.write_table(t, path, compression="NONE", use_dictionary=[synth.NAME],
+                       column_encoding={c: "PLAIN" for c in t.column_names if c != synth.NAME},
+                       row_group_size=60_000, data_page_size=1 << 20)
+        engine.load_segment(path)
+        keys.append(path)
+        blobs.append(open(path, "rb").read())
+        segs.append(synth.segment_request(i, hour=i % 4))
+    filters = [synth.leaf(synth.NAME, "eq", "metric_01"),
+               synth.leaf(synth.NAME, "in", "metric_00", "metric_03", "metric_04"),
+               synth.leaf(synth.NAME, "in", *[f"metric_{k:02d}" for k in range(0, 40, 3)]),
+               synth.leaf(synth.NAME, "!=", "metric_02"),
+               synth.leaf(synth.NAME, "regex", "metric_1[0-5]")]
+    cases = [(f, agg, gbs, step) for f in filters for agg, gbs, step in
+             [("sum", [], 60_000), ("max", [synth.NAME], 1_000), ("count", [], 60_000), ("min", [], 60_000),
+              ("avg", [synth.NAME], 60_000)]]
+    for ci, (filt, agg, gbs, step) in enumerate(cases):
+        segs_s = [dict(s, stepInMillis=step) for s in segs]
+        if ci % 3 == 0:   # a window cutting tiles
+            segs_s = [dict(s, startTs=s["startTs"] + 123_457, endTs=s["endTs"] - 777_001) for s in segs_s]
+        req = json.dumps(synth.pushdown(filt, segs_s, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 3, keys, sources=blobs)
+        got = engine.eval_pushdown(req, keys, 3, LK_PER_GLOB_ROWS)
+        for gi, (g, cs) in enumerate(zip(got.per_glob(len(cells)), cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"lean case {ci} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 3, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, f"lean case {ci} merged")
+        os.environ["LK_NO_LEAN_SPLIT"] = "1"
+        try:
+            general = engine.eval_pushdown(req, keys, 3, LK_MERGED)
+        finally:
+            del os.environ["LK_NO_LEAN_SPLIT"]
+        assert list(general.ts) == list(merged.ts) and general.tags == merged.tags
+        if agg not in ("sum", "avg"):   # compensated sums: each path within 1 ulp of the exact sum (checked above)
+            assert np.array_equal(general.values.view(np.uint64), merged.values.view(np.uint64))
