@@ -71,6 +71,11 @@ const uint32_t* lk_result_globs(const lk_result* r);       /* glob index per row
 size_t lk_result_num_tag_columns(const lk_result* r);
 const char* lk_result_tag_name(const lk_result* r, size_t col);             /* "name", groupBys, queryTags keys */
 const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col); /* NULL => tag absent (S15) */
+/* Percentile aggregations (`p<NN>`, logs/traces): the row's serialized DDSketch (sketches-java DDSketch.serialize
+ * wire format, the `Left(bytes)` of SketchTags, PushDownAggregatorStage.scala:163-167; relative accuracy 0.01); the
+ * row's value is getValueAtQuantile(NN / 100) of that sketch (BaseExpr.scala:59-61).  *len = 0 / NULL for other
+ * aggregations.  Valid until lk_result_free. */
+const uint8_t* lk_result_sketch(const lk_result* r, size_t row, size_t* len);
 /* JSON: {"scan_ms":..,"total_ms":..,"rows_scanned":..,"algorithmic_bytes":..,"tiles":..,"cells":..} */
 const char* lk_result_stats(const lk_result* r);
 void lk_result_free(lk_result* r);

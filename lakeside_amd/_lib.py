@@ -42,6 +42,7 @@ SIGNATURES = [
     ("lk_result_tag_name", _c.c_char_p, [_P, _c.c_size_t]),
     ("lk_result_tag_value", _c.c_char_p, [_P, _c.c_size_t, _c.c_size_t]),
     ("lk_result_stats", _c.c_char_p, [_P]),
+    ("lk_result_sketch", _c.POINTER(_c.c_uint8), [_P, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     ("lk_result_free", None, [_P]),
     ("lk_last_error", _c.c_char_p, []),
     ("lk_comm_unique_id", _c.c_int, [_c.c_void_p]),

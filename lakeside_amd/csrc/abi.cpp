@@ -145,6 +145,12 @@ const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col) {
   return r->tag(row, col);
 }
 const char* lk_result_stats(const lk_result* r) { return r ? r->stats.c_str() : nullptr; }
+const uint8_t* lk_result_sketch(const lk_result* r, size_t row, size_t* len) {
+  if (len) *len = 0;
+  if (!r || row >= r->sketches.size()) return nullptr;
+  if (len) *len = r->sketches[row].size();
+  return reinterpret_cast<const uint8_t*>(r->sketches[row].data());
+}
 void lk_result_free(lk_result* r) { delete r; }
 
 }  // extern "C"

@@ -210,6 +210,7 @@ struct lk_result {
     const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id, or perm[dim id])
     std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
     bool hidden = false;                         // tag name dropped by NoisyTagsDropper (tag queries)
+    const char* null_value = nullptr;            // the tag's value for dim_null (nullptr: tag dropped)
   };
   std::vector<TagCol> tcols;
   // Commons.scala:450-452: a row whose own tags are all absent takes its glob head's queryTags
@@ -219,6 +220,7 @@ struct lk_result {
   std::vector<std::string> count_str;            //   and its per-row value (COUNT(*) as text)
   std::deque<std::string> owned;                 // strings not owned by a dictionary
   std::string stats;
+  std::vector<std::string> sketches;             // percentile rows: the serialized DDSketch of each row
 
   lk_result() = default;
   lk_result(const lk_result&) = delete;
@@ -256,7 +258,7 @@ struct lk_result {
     const TagCol& t = tcols[c];
     if (t.hidden) return nullptr;
     const uint32_t d = uint32_t((gid[row] / t.stride) % t.ndim);
-    if (d == t.dim_null) return nullptr;
+    if (d == t.dim_null) return t.null_value;
     if (!t.local.empty()) return t.local[d];
     const std::string& s = (*t.dict)[t.order ? t.order->perm[d] : d];
     return (s.empty() || s == "null") ? nullptr : s.c_str();

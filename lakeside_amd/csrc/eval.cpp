@@ -25,6 +25,7 @@
 #include "kernels.hpp"
 #include "layout.hpp"
 #include "plan.hpp"
+#include "ddsketch.hpp"
 #include "regex.hpp"
 
 namespace lk {
@@ -275,7 +276,22 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   else if (R.aggregation == "max") agg = AGG_MAX;
   else if (R.aggregation == "count") agg = AGG_COUNT;
   else if (R.aggregation == "avg") agg = AGG_AVG;
+  else if (R.aggregation.size() > 1 && R.aggregation[0] == 'p' && R.dataset != "metrics") agg = AGG_SKETCH;
   else throw PlanError(LK_ERR_UNSUPPORTED, "aggregation " + R.aggregation + " (sketch path) is not on the hot path");
+  // Percentiles (logs / traces): BaseExpr.getChartSql selects the passing rows (BaseExpr.scala:397-399), the
+  // worker's PushDownAggregatorStage builds one DDSketch per (step, group-key tags) (PushDownAggregatorStage.scala:
+  // 69-81, 188-197), query-api merges per (timestamp, tags) and reads getValueAtQuantile(p / 100)
+  // (BaseExpr.scala:59-61).  Here: the scan bins every value on the GPU (COUNT per (cell, DDSketch bin)), the host
+  // assembles the sketches.
+  const bool sketch = agg == AGG_SKETCH;
+  double quantile = 0.0;
+  if (sketch) {
+    char* end = nullptr;
+    const std::string qs = R.aggregation.substr(1);
+    quantile = strtod(qs.c_str(), &end) / 100.0;
+    if (end == qs.c_str() || *end || !(quantile >= 0.0 && quantile <= 1.0))
+      throw PlanError(LK_ERR_ARG, "percentile aggregation " + R.aggregation);
+  }
   // Merged avg: query-api runs AVG as separate SUM and COUNT pushdowns, merges them per (timestamp, tags) into
   // a {sum, count} map and divides (QueryEngineV2.scala:280-283, TimeGroupedSketchAggregator.scala:74-78,
   // BaseExpr.scala:88-91).  The table holds both, so one scan gives Σsum / Σcount (NaN when no value).
@@ -620,6 +636,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::vector<uint32_t> seg_begin;
   uint32_t total_tiles = 0;
   uint64_t rows_scanned = 0, alg_bytes = 0;
+  bool all_lean = true;       // every scanned tile is scan_lean's (the general kernel need not run)
   int local_err = 0;          // distributed: a rank-local failure, agreed on with the other ranks after the scan
   std::string local_msg;
   try {
@@ -657,6 +674,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
       if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
       for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
+      // name page has a small dictionary (lean_tile's test at page granularity)
+      if (all_lean) {
+        const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
+        const int cn = strs.size() == 1 ? S.col_index(strs[0].name) : -1;
+        all_lean = ct >= 0 && cv >= 0 && cn >= 0 && !S.cols[ct].any_nulls && !S.cols[cv].any_nulls &&
+                   !S.cols[cn].any_nulls;
+        if (all_lean)
+          for (const PageDesc& pg : S.cols[cn].pages)
+            if (pg.kind != PAGE_DICT || pg.dict_n > 64 || pg.bw < 1 || pg.bw > 6) { all_lean = false; break; }
+      }
       q.tile_begin = total_tiles;
       seg_begin.push_back(total_tiles);
       total_tiles += q.ntiles;
@@ -741,13 +769,15 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // never exceed the rows scanned.
   const uint64_t dense_max = getenv("LK_DENSE_MAX_CELLS") ? uint64_t(atoll(getenv("LK_DENSE_MAX_CELLS")))
                                                           : (uint64_t(1) << 26);
-  const bool hash_mode = ncells > dense_max;
+  const bool hash_mode = sketch || ncells > dense_max;   // sketch keys: (cell, bin), sparse
+  if (sketch && double(ncells) * double(DD_NBINS) > 9.0e18) throw PlanError(LK_ERR_UNSUPPORTED, "sketch key space beyond 64 bits");
   auto pow2 = [](uint64_t x) {
     uint64_t p = 1;
     while (p < x) p <<= 1;
     return p;
   };
-  const uint64_t hash_bound = std::max<uint64_t>(1, std::min<uint64_t>(ncells, rows_scanned));
+  const double key_space = double(ncells) * (sketch ? double(DD_NBINS) : 1.0);   // distinct keys <= both
+  const uint64_t hash_bound = std::max<uint64_t>(1, key_space < double(rows_scanned) ? uint64_t(key_space) : rows_scanned);
   const uint64_t cap_max = std::max<uint64_t>(pow2(2 * hash_bound), 1 << 16);
   uint64_t cap = hash_mode ? std::min<uint64_t>(cap_max, std::max<uint64_t>(1 << 16, std::min<uint64_t>(pow2(2 * hash_bound), 1 << 25))) : 0;
   if (hash_mode && getenv("LK_HASH_INIT_SLOTS"))   // tests only: a deliberately small first table (regrowth path)
@@ -855,13 +885,19 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   P.truth_late = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_l) : nullptr;
   P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
   const uint32_t* d_maps = reinterpret_cast<const uint32_t*>(dbuf + o_maps);
-  const int kagg = agg == AGG_AVG ? AGG_SUM : (agg == AGG_ROWS ? AGG_COUNT : agg);
+  const int kagg = agg == AGG_AVG ? AGG_SUM : ((agg == AGG_ROWS || agg == AGG_SKETCH) ? AGG_COUNT : agg);
   // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
   if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
   // single string column (filter and group dim on `name` only): NULL-free tiles with a small chunk dictionary go
   // to scan_lean (lean_kernel.hpp), the rest to scan_tiles
-  P.lean_split = (P.nstr == 1 && P.truth && agg != AGG_ROWS && !getenv("LK_NO_LEAN_SPLIT")) ? 1u : 0u;
+  P.lean_split = (P.nstr == 1 && P.truth && agg != AGG_ROWS && !sketch && !getenv("LK_NO_LEAN_SPLIT")) ? (all_lean ? 2u : 1u) : 0u;
+  if (sketch) {
+    P.sketch = 1;
+    P.dd_mult = dd::mapping().multiplier;
+    P.dd_min = dd::mapping().min_indexable;
+    P.dd_max = dd::mapping().max_indexable;
+  }
 
   // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
   size_t nc = 0;
@@ -978,6 +1014,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   }
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
   if (hflags & FLAG_HASH_FULL) throw PlanError(LK_ERR_MEMORY, "aggregation hash table full at its bound");
+  // DDSketch.accept on NaN / a magnitude beyond the mapping's range throws in the worker's stream stage: the
+  // stream fails (Commons.scala:331-335) and query-api sees an empty source
+  if (hflags & FLAG_SKETCH_RANGE) throw PlanError(LK_ERR_ARG, "DDSketch: value outside the trackable range");
 
   // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
   if (dist) {
@@ -999,7 +1038,109 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   uint32_t* d_counts = nullptr;
   void* sws = nullptr;
   unsigned long long nocc = 0;
-  if (!hash_mode) {
+  // Percentiles: one DDSketch per (glob, step, group-key tags) -- the groupBys' values, or {"name": v} without
+  // groupBys (PushDownAggregatorStage.getGroupByKeyTags, 188-197); NULL / "null" / "" values drop out of the tags
+  // (Commons.scala:433).  Merged: per (step, tags), or per step without groupBys (SimpleSketchMerger: one sketch,
+  // tags of one input -- here the smallest name).
+  struct SkRow {
+    int64_t ts;
+    uint32_t glob;
+    unsigned long long gid;
+    dd::Sketch sk;
+    std::string name;   // merged without groupBys: the name of `gid` (the smallest seen)
+  };
+  std::vector<SkRow> sk_rows;
+  if (sketch) {
+    if (emit) {
+      SParams S2{};
+      S2.keys = P.hkeys;
+      S2.rows = P.rows;
+      S2.cnt = P.cnt;
+      S2.hi = P.hi;
+      S2.lo = P.lo;
+      S2.ext = P.ext;
+      S2.cap = cap;
+      const uint32_t nsb = sparse_blocks(cap);
+      uint32_t* occ = static_cast<uint32_t*>(X->workspace("occ_counts", (size_t(nsb) + 2) * 4));
+      HIP_TRY(launch_sparse_count(S2, occ, st));
+      uint32_t n32 = 0;
+      HIP_TRY(hipMemcpyAsync(&n32, occ + nsb, 4, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+      nocc = n32;
+      std::vector<unsigned long long> keys(nocc), cnts(nocc);
+      if (nocc) {
+        auto* recs = static_cast<unsigned long long*>(X->workspace("sketch_recs", size_t(nocc) * 48 + 64));
+        HIP_TRY(launch_table_records(P, cap, occ, recs, nocc, st));
+        HIP_TRY(hipMemcpyAsync(keys.data(), recs, nocc * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(cnts.data(), recs + nocc, nocc * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+      }
+      // group term of each record's key tags
+      std::vector<unsigned long long> kg(nocc, 0);
+      std::vector<unsigned long long> cellv(nocc);
+      for (size_t i = 0; i < nocc; i++) cellv[i] = keys[i] / DD_NBINS;
+      const bool by_name = gbs.empty();
+      const bool name_grouped = std::find(gbs.begin(), gbs.end(), std::string(kName)) != gbs.end();
+      for (size_t si = 0; si < strs.size(); si++) {
+        StrCol& sc = strs[si];
+        if (!sc.is_dim || !sc.stride) continue;
+        const bool drop = si == 0 && !by_name && !name_grouped;   // name is no key tag when groupBys exist
+        GlobalDict& gd = E.dict(sc.name);
+        std::lock_guard<std::mutex> g(gd.mu);
+        std::unordered_map<uint32_t, bool> nl;
+        for (size_t i = 0; i < nocc; i++) {
+          uint32_t d = uint32_t((cellv[i] % ngroups) / sc.stride % sc.ndim);
+          if (drop) d = sc.dim_null;
+          if (d != sc.dim_null) {
+            auto it = nl.find(d);
+            if (it == nl.end()) it = nl.emplace(d, null_like(sc.dim_value(d, gd))).first;
+            if (it->second) d = sc.dim_null;
+          }
+          kg[i] += (unsigned long long)d * sc.stride;
+        }
+      }
+      // merged without groupBys: one sketch per step; its tags: the smallest name ("" for a NULL-like one)
+      std::vector<std::string> name_of;
+      if (!per_glob_rows && by_name) {
+        GlobalDict& gd = E.dict(kName);
+        std::lock_guard<std::mutex> g(gd.mu);
+        name_of.resize(nocc);
+        for (size_t i = 0; i < nocc; i++) {
+          const uint32_t d = uint32_t(kg[i] / strs[0].stride % strs[0].ndim);
+          if (d != strs[0].dim_null) name_of[i] = strs[0].dim_value(d, gd);
+        }
+      }
+      std::map<std::tuple<uint64_t, uint32_t, unsigned long long>, size_t> at;   // (bucket, glob, key) -> row
+      for (size_t i = 0; i < nocc; i++) {
+        const unsigned long long cell = cellv[i];
+        const uint64_t b = (cell / ngroups) % nbuckets;
+        const uint32_t slot = uint32_t(cell / ngroups / nbuckets);
+        const unsigned long long key = (!per_glob_rows && by_name) ? 0ull : kg[i];
+        auto ins = at.emplace(std::make_tuple(b, per_glob_rows ? slot : 0u, key), sk_rows.size());
+        if (ins.second) {
+          sk_rows.push_back(SkRow{bucket_base + int64_t(b) * P.step, per_glob_rows ? slot : 0u, kg[i], dd::Sketch{},
+                                  name_of.empty() ? std::string() : name_of[i]});
+        }
+        SkRow& r = sk_rows[ins.first->second];
+        if (!name_of.empty() && kg[i] != r.gid && name_of[i] < r.name) {   // keep the smallest name's group term
+          r.gid = kg[i];
+          r.name = name_of[i];
+        }
+        r.sk.add_bin(uint32_t(keys[i] % DD_NBINS), double(cnts[i]));
+      }
+      std::vector<size_t> ord(sk_rows.size());
+      for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) {
+        const SkRow &x = sk_rows[a], &y = sk_rows[b];
+        return x.ts != y.ts ? x.ts < y.ts : (x.glob != y.glob ? x.glob < y.glob : x.gid < y.gid);
+      });
+      std::vector<SkRow> sorted;
+      sorted.reserve(ord.size());
+      for (size_t i : ord) sorted.push_back(std::move(sk_rows[i]));
+      sk_rows.swap(sorted);
+      nrows_out = uint32_t(sk_rows.size());
+    }
+  } else if (!hash_mode) {
     // ---- merged min/max with NULL-able values: fold null-like group values per glob-cell SQL value ----
     F.rows = P.rows;
     F.cnt = P.cnt;
@@ -1102,7 +1243,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
   res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
-  if (nrows_out) {
+  if (sketch) {
+    res->sketches.reserve(nrows_out);
+    for (size_t r = 0; r < nrows_out; r++) {
+      const SkRow& k = sk_rows[r];
+      res->ts[r] = k.ts;
+      res->val[r] = k.sk.quantile(quantile);
+      res->gid[r] = k.gid;
+      if (per_glob_rows) res->glob[r] = k.glob;
+      res->sketches.push_back(k.sk.serialize());
+    }
+  } else if (nrows_out) {
     // Rows written by the kernel straight into the mapped pinned result block when it is pinned: no device->host
     // copies (small async D2H copies cost ~1 ms of completion latency each call on this stack, measured in C4).
     const bool direct = res->blk.pinned;
@@ -1140,7 +1291,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::vector<std::string> qt_keys;
   for (auto& g : globs)
     for (auto& kv : g.query_tags)
-      if (!tagq && std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
+      if (!tagq && !sketch && std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
   for (auto& k : qt_keys) res->tag_names.push_back(k);
   // Per tag column: how a row's group id decodes to the tag string (lk_result::tag; nullptr: tag dropped,
   // Commons.scala:433).  Strings local to this call (filter candidates, the distributed union) move into the
@@ -1174,6 +1325,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       m[d] = res->owned.back().c_str();
     }
   }
+  if (sketch && gbs.empty()) res->tcols[0].null_value = "";   // key tags {"name": ""} (getOrElse(NAME, ""))
+  if (sketch && !gbs.empty()) res->tcols[0].hidden = true;     // key tags: the groupBys only
   if (tagq) {
     // Tag-query rows (Commons.toDataPoint, Commons.scala:406-423): every column becomes a tag -- the tag and
     // "count" (COUNT(*) via getString) -- then NoisyTagsDropper.remove (NoisyTagsDropper.scala) drops hidden
@@ -1192,7 +1345,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
   }
   res->qt_of_glob.resize(globs.size());
-  for (size_t gi = 0; gi < globs.size(); gi++)
+  for (size_t gi = 0; gi < globs.size() && !sketch; gi++)
     for (auto& kv : globs[gi].query_tags) {
       size_t c = nreg + size_t(std::find(qt_keys.begin(), qt_keys.end(), kv.first) - qt_keys.begin());
       res->owned.push_back(kv.second);

@@ -152,7 +152,14 @@ struct QParams {
   // table whose slot keys are `hkeys` (EMPTY = ~0); null: dense mode (array index = cell key)
   unsigned long long* hkeys;
   unsigned long long hmask;         // slots - 1 (a power of two)
-  uint32_t lean_split;              // 1: scan_lean takes the lean tiles (lean_tile), scan_tiles skips them
+  // DDSketch mode (percentile aggregations, COUNT instantiation only): the cell key gains the value's DDSketch bin,
+  // key = cell * DD_NBINS + dd_bin(value) (a NULL value reads as 0.0, the JDBC getDouble contract); rows per key
+  uint32_t sketch;
+  double dd_mult;                   // 1 / ln(gamma) of the index mapping
+  double dd_min;                    // smallest indexable magnitude (smaller values go to the zero bin)
+  double dd_max;                    // largest trackable magnitude (beyond: FLAG_SKETCH_RANGE)
+  uint32_t lean_split;              // 1: scan_lean takes the lean tiles (lean_tile), scan_tiles skips them;
+                                    // 2: every tile is lean (scan_tiles is not launched)
   uint32_t lean;                    // LEAN_* bits: table fields the scan leaves to the fix-up pass (fewer atomics)
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
@@ -163,7 +170,13 @@ struct QParams {
   unsigned long long* plan_bytes;
 };
 
-enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u };
+enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u };
+
+// DDSketch bins (sketches-java LogarithmicMapping, relative accuracy 0.01): bin 0 = zero, 1 + DD_BIAS + i = positive
+// index i, 1 + DD_HALF + DD_BIAS + i = negative index i (|i| < DD_BIAS covers every finite double).
+constexpr int32_t DD_BIAS = 40000;
+constexpr uint32_t DD_HALF = 2 * DD_BIAS;
+constexpr uint32_t DD_NBINS = 1 + 2 * DD_HALF;
 constexpr uint32_t HASH_MAX_PROBE = 4096;
 // Lean tables: with no NULL value in the query's value column, a cell's non-NULL count equals its row count
 // (LEAN_NO_CNT: `cnt` is not accumulated), and for min/max a cell exists iff its extreme left the identity

@@ -159,6 +159,21 @@ __device__ __forceinline__ bool interpret(const QParams& P, uint32_t T, uint32_t
   return st & 1;
 }
 
+// DDSketch bin of a value (sketches-java 0.8.2 LogarithmicMapping.index + DDSketch.accept): |v| <= dd_min -> the
+// zero bin; index = (int) (ln|v| * multiplier), minus one when negative (LogLikeIndexMapping.index's floor);
+// NaN / |v| > dd_max is untrackable (accept throws): FLAG_SKETCH_RANGE.
+__device__ __forceinline__ uint32_t dd_bin(const QParams& P, double v) {
+  const double a = fabs(v);
+  if (!(a <= P.dd_max)) {
+    atomicOr(P.flags, FLAG_SKETCH_RANGE);
+    return 0u;
+  }
+  if (a <= P.dd_min) return 0u;
+  const double x = log(a) * P.dd_mult;
+  const int32_t i = x >= 0.0 ? int32_t(x) : int32_t(x) - 1;
+  return uint32_t(1 + DD_BIAS + i) + (v < 0.0 ? DD_HALF : 0u);
+}
+
 // Uniform LDS-staged pointer -> SGPR pair.
 template <class T>
 __device__ __forceinline__ const T* uptr(const T* p) {
@@ -548,6 +563,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
     }
   }
   const bool one_bucket = tile_b >= 0;
+  const bool sketch = AGG == AGG_COUNT && P.sketch != 0u;   // uniform
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
@@ -589,7 +605,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         ch.ts[j] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
         if (count_plan) pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
       }
-      if (AGG != AGG_COUNT) {
+      if (AGG != AGG_COUNT || sketch) {
         ch.v[j] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
         if (count_plan) pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
       }
@@ -614,7 +630,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
       ch.ts[0] = __builtin_amdgcn_raw_buffer_load_b64(rs0, live ? (vb0 + tv) * 8u : OOB, 0, 0);
       if (count_plan) pbytes += 128u * new_lines(live, (vb0 + tv) * 8u, last_ts_line);
     }
-    if (AGG != AGG_COUNT) {
+    if (AGG != AGG_COUNT || sketch) {
       ch.v[0] = __builtin_amdgcn_raw_buffer_load_b64(rs1, vok ? (vb1 + vv) * 8u : OOB, 0, 0);
       if (count_plan) pbytes += 128u * new_lines(vok, (vb1 + vv) * 8u, last_v_line);
     }
@@ -658,13 +674,20 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         atomicOr(P.flags, FLAG_CELL_RANGE);
         continue;
       }
-      const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
+      unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + ch.gid[j];
+      const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
+      bool vvalid = (ch.vok >> j) & 1u;
+      if constexpr (AGG == AGG_COUNT) {
+        if (sketch) {   // DDSketch bin of the value (NULL: 0.0, counted); every passing row counts
+          cell = cell * DD_NBINS + dd_bin(P, vvalid ? v : 0.0);
+          vvalid = true;
+        }
+      }
       if (cell != acc.key) {
         lds_merge<AGG, HASH, SLIM>(L, P, acc);
         acc_reset<AGG>(acc, cell);
       }
-      const double v = __longlong_as_double((long long)(((uint64_t)ch.v[j].y << 32) | ch.v[j].x));
-      acc_add<AGG>(acc, (ch.vok >> j) & 1u, v);
+      acc_add<AGG>(acc, vvalid, v);
     }
   };
   // Software pipeline: the first 64 listed rows of sub-tile k are issued into ring slot k % DEPTH and consumed

@@ -83,6 +83,13 @@ class Result:
             self._tags = out
         return self._tags
 
+    def sketch(self, row: int) -> bytes:
+        """The row's serialized DDSketch (percentile aggregations); b"" otherwise."""
+        L = _lib.lib()
+        n = ctypes.c_size_t()
+        p = L.lk_result_sketch(self._owner.h, row, ctypes.byref(n))
+        return ctypes.string_at(p, n.value) if n.value else b""
+
     def close(self):
         """Drop this object's reference; the library result is freed once no array view remains."""
         self._owner = None

@@ -227,7 +227,9 @@ def check_hot_path(pr: PushDownRequest) -> None:
     if pr.isTagQuery or be.chart is None:
         raise NotImplementedError("tag/exemplar queries are outside the hot path")
     agg = be.chart.aggregation
-    if agg not in (SUM, MIN, MAX, COUNT, AVG):
+    if is_percentile(agg) and be.dataset != METRICS:
+        pass
+    elif agg not in (SUM, MIN, MAX, COUNT, AVG):
         raise NotImplementedError(f"aggregation {agg} (sketch path) is outside the hot path")
     if be.chart.fieldName is not None or be.extract is not None or be.compute is not None:
         raise NotImplementedError("extract/compute/field charts are outside the hot path")
@@ -499,7 +501,8 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
             tags = dict(qtags)                                        # Commons.scala:450-452
         cell.tags = tags
         out.append(cell)
-    out.sort(key=lambda c: (c.ts, sorted(c.tags.items()), c.agg_value(chart.aggregation)))
+    std = chart.aggregation in (SUM, MIN, MAX, COUNT, AVG)
+    out.sort(key=lambda c: (c.ts, sorted(c.tags.items()), c.agg_value(chart.aggregation) if std else 0.0))
     return out
 
 
@@ -774,3 +777,60 @@ def final_eval(base_expr: dict, merged_rows, step_ms: int, now_ms: int) -> List[
             out.append({"id": base_expr.get("id", "_"), "type": "timeseries",
                         "message": {"timestamp": ts, "tags": tags, "value": transform(v), "label": lab}})
     return out
+
+
+# ----------------------------------------------------------------------------------------------
+# Percentiles: DDSketch per (step, group-key tags)
+# ----------------------------------------------------------------------------------------------
+def is_percentile(agg: Optional[str]) -> bool:
+    return agg is not None and len(agg) > 1 and agg[0] == "p"
+
+
+def _key_tags(pr: PushDownRequest, tags: Dict[str, str]) -> Dict[str, str]:
+    """PushDownAggregatorStage.getGroupByKeyTags (PushDownAggregatorStage.scala:188-197) over the DataPoint's tags
+    (Commons.toDataPoint: NULL / "null" / "" dropped, Commons.scala:433)."""
+    gbs = pr.baseExpr.chart.groupBys
+    if not gbs:
+        return {"name": tags.get("name", "")}
+    return {g: tags[g] for g in gbs if g in tags}
+
+
+def evaluate_percentile_per_glob(pr: PushDownRequest, glob_size: int, paths: Sequence[str], sources=None):
+    """Per glob: [(ts, key tags, Sketch)] ascending in ts (ties: sorted tags).  The worker's SQL returns the passing
+    rows (BaseExpr.scala:397-399); each row's value (NULL -> 0.0, JDBC getDouble) goes into the sketch of its
+    (ts - ts % step, key tags) (PushDownAggregatorStage.scala:56-60, 69-81)."""
+    from oracle import ddsketch
+    check_hot_path(pr)
+    out = []
+    for g in globs_of(pr, glob_size):
+        cells = evaluate_glob(pr, g, [paths[i] for i in g], None if sources is None else [sources[i] for i in g])
+        acc: Dict[Tuple, Tuple[Dict[str, str], Any]] = {}
+        for c in cells:
+            kt = _key_tags(pr, c.tags)
+            vals = np.concatenate([c.values, np.zeros(c.rows - c.count)])
+            sk = ddsketch.Sketch().accept_all(vals)
+            key = (c.ts, tuple(sorted(kt.items())))
+            if key in acc:
+                acc[key][1].merge(sk)
+            else:
+                acc[key] = (kt, sk)
+        out.append([(k[0], acc[k][0], acc[k][1]) for k in sorted(acc)])
+    return out
+
+
+def merge_percentile(pr: PushDownRequest, per_glob) -> List[Tuple[int, Dict[str, str], Any]]:
+    """query-api merge of DD sketches (TimeGroupedSketchAggregator.scala:34-37, 101-114): per (timestamp, tags) with
+    groupBys, else one sketch per timestamp whose tags are one input's (here: the smallest name)."""
+    from oracle import ddsketch
+    gbs = pr.baseExpr.chart.groupBys
+    acc: Dict[Tuple, Tuple[Dict[str, str], Any]] = {}
+    for rows in per_glob:
+        for ts, kt, sk in rows:
+            key = (ts, tuple(sorted(kt.items()))) if gbs else (ts,)
+            if key not in acc:
+                acc[key] = (dict(kt), ddsketch.Sketch().merge(sk))
+            else:
+                if not gbs and kt.get("name", "") < acc[key][0].get("name", ""):
+                    acc[key] = (dict(kt), acc[key][1])
+                acc[key][1].merge(sk)
+    return [(k[0], acc[k][0], acc[k][1]) for k in sorted(acc)]

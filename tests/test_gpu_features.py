@@ -129,3 +129,68 @@ def test_lean_kernel_shapes(engine, tmp_path):
         assert list(general.ts) == list(merged.ts) and general.tags == merged.tags
         if agg not in ("sum", "avg"):   # compensated sums: each path within 1 ulp of the exact sum (checked above)
             assert np.array_equal(general.values.view(np.uint64), merged.values.view(np.uint64))
+
+
+def _pct_rows_equal(got_rows, want_rows, q, label):
+    """Percentile rows: (ts, tags) in ascending time (ties compared as sorted tag lists), DDSketch bins identical,
+    value == the oracle sketch's getValueAtQuantile(q) bit for bit."""
+    from oracle import ddsketch
+    key = lambda r: (r[0], sorted(r[1].items()))
+    got_rows = sorted(got_rows, key=key)
+    want_rows = sorted(want_rows, key=key)
+    assert [key(r) for r in got_rows] == [key(r) for r in want_rows], label
+    for (ts, tags, val, blob), (_, _, sk) in zip(got_rows, want_rows):
+        gs = ddsketch.decode(blob)
+        assert gs.bins() == sk.bins(), (label, ts, tags)
+        assert val == sk.quantile(q), (label, ts, tags, val, sk.quantile(q))
+
+
+def test_percentile_sketches(engine, tmp_path):
+    """`p<NN>` aggregations (logs): per-glob DDSketches per (step, key tags) and query-api's merged quantiles equal
+    the oracle's restatement of sketches-java (bins exact, quantile values bit for bit); NULL values count as 0.0;
+    negative values and zeros; key tags = groupBys, or {"name": v} without groupBys."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(9)
+    keys, blobs, segs = [], [], []
+    for i in range(5):
+        n = 80_000
+        t0 = synth.T0 + (i % 2) * synth.HOUR
+        v = rng.lognormal(0.0, 2.0, n) * np.where(rng.random(n) < 0.2, -1.0, 1.0)
+        v[rng.random(n) < 0.02] = 0.0
+        t = pa.table({
+            dx.TIMESTAMP: pa.array(np.sort(rng.integers(t0, t0 + synth.HOUR, n)), pa.int64()),
+            dx.VALUE: pa.array(v, pa.float64(), mask=rng.random(n) < 0.05),
+            synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 4, n)], pa.string(),
+                                 mask=rng.random(n) < 0.03),
+            synth.SERVICE: pa.array([["svc-a", "svc-b", "null", ""][k] for k in rng.integers(0, 4, n)], pa.string(),
+                                    mask=rng.random(n) < 0.05),
+        })
+        path = str(tmp_path / f"pct{i}.parquet")
+        pq.write_table(t, path, compression="NONE", use_dictionary=[synth.NAME, synth.SERVICE],
+                       column_encoding={dx.TIMESTAMP: "PLAIN", dx.VALUE: "PLAIN"}, row_group_size=40_000)
+        engine.load_segment(path)
+        keys.append(path)
+        blobs.append(open(path, "rb").read())
+        segs.append(synth.segment_request(i, hour=i % 2, step=300_000))
+    for filt, agg, gbs in [(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "p95", []),
+                           (synth.leaf(synth.NAME, "!=", "metric_03"), "p50", [synth.SERVICE]),
+                           ({"op": "or", "q1": synth.leaf(synth.NAME, "eq", "metric_00"),
+                             "q2": synth.leaf(synth.SERVICE, "eq", "svc-a")}, "p99.9", [synth.SERVICE, synth.NAME])]:
+        q = float(agg[1:]) / 100.0
+        req_d = synth.pushdown(filt, segs, agg, gbs)
+        req_d["baseExpr"]["chart"]["rollup"] = agg
+        req = json.dumps(req_d)
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_percentile_per_glob(pr, 2, keys, sources=blobs)
+        res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        assert list(res.ts) == sorted(res.ts)
+        for gi in range(len(want)):
+            got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
+                   for r in range(len(res)) if int(res.globs[r]) == gi]
+            _pct_rows_equal(got, want[gi], q, f"{agg} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        got = [(int(merged.ts[r]), merged.tags[r], float(merged.values[r]), merged.sketch(r)) for r in range(len(merged))]
+        _pct_rows_equal(got, dx.merge_percentile(pr, want), q, f"{agg} merged")
