@@ -26,6 +26,7 @@
 #include "layout.hpp"
 #include "plan.hpp"
 #include "ddsketch.hpp"
+#include "hll.hpp"
 #include "regex.hpp"
 
 namespace lk {
@@ -271,6 +272,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     throw PlanError(LK_ERR_ARG, "Invalid dataset: " + R.dataset);
   int agg;
   if (tagq) agg = AGG_ROWS;
+  // Cardinality (`ces` in the chart's rollup, PushDownAggregatorStage.scala:44,82-94; computeCardinality sets it,
+  // QueryEngineV2.scala:616-617): per step one HLL over the rows' group-key strings, whatever the SQL aggregate.
+  else if ((R.aggregation == "ces" || R.rollup.find("ces") != std::string::npos) && R.dataset != "metrics") agg = AGG_CES;
   else if (R.aggregation == "sum") agg = AGG_SUM;
   else if (R.aggregation == "min") agg = AGG_MIN;
   else if (R.aggregation == "max") agg = AGG_MAX;
@@ -284,6 +288,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // (BaseExpr.scala:59-61).  Here: the scan bins every value on the GPU (COUNT per (cell, DDSketch bin)), the host
   // assembles the sketches.
   const bool sketch = agg == AGG_SKETCH;
+  const bool ces = agg == AGG_CES;
   double quantile = 0.0;
   if (sketch) {
     char* end = nullptr;
@@ -769,7 +774,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // never exceed the rows scanned.
   const uint64_t dense_max = getenv("LK_DENSE_MAX_CELLS") ? uint64_t(atoll(getenv("LK_DENSE_MAX_CELLS")))
                                                           : (uint64_t(1) << 26);
-  const bool hash_mode = sketch || ncells > dense_max;   // sketch keys: (cell, bin), sparse
+  const bool hash_mode = sketch || ces || ncells > dense_max;   // sketch keys: (cell, bin), sparse
   if (sketch && double(ncells) * double(DD_NBINS) > 9.0e18) throw PlanError(LK_ERR_UNSUPPORTED, "sketch key space beyond 64 bits");
   auto pow2 = [](uint64_t x) {
     uint64_t p = 1;
@@ -885,7 +890,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   P.truth_late = late_mask ? reinterpret_cast<const uint32_t*>(dbuf + o_truth_l) : nullptr;
   P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
   const uint32_t* d_maps = reinterpret_cast<const uint32_t*>(dbuf + o_maps);
-  const int kagg = agg == AGG_AVG ? AGG_SUM : ((agg == AGG_ROWS || agg == AGG_SKETCH) ? AGG_COUNT : agg);
+  const int kagg = agg == AGG_AVG ? AGG_SUM : ((agg == AGG_ROWS || agg == AGG_SKETCH || agg == AGG_CES) ? AGG_COUNT : agg);
   // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
   if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
@@ -1050,7 +1055,68 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     std::string name;   // merged without groupBys: the name of `gid` (the smallest seen)
   };
   std::vector<SkRow> sk_rows;
-  if (sketch) {
+  struct CesRow {
+    int64_t ts;
+    uint32_t glob;
+    hll::Sketch h;
+  };
+  std::vector<CesRow> ces_rows;
+  if (ces && emit) {
+    // occupied cells -> (glob, step) -> the set of group-key strings, one HLL each
+    SParams S2{};
+    S2.keys = P.hkeys;
+    S2.rows = P.rows;
+    S2.cnt = P.cnt;
+    S2.hi = P.hi;
+    S2.lo = P.lo;
+    S2.ext = P.ext;
+    S2.cap = cap;
+    const uint32_t nsb = sparse_blocks(cap);
+    uint32_t* occ = static_cast<uint32_t*>(X->workspace("occ_counts", (size_t(nsb) + 2) * 4));
+    HIP_TRY(launch_sparse_count(S2, occ, st));
+    uint32_t n32 = 0;
+    HIP_TRY(hipMemcpyAsync(&n32, occ + nsb, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    nocc = n32;
+    std::vector<unsigned long long> keys(nocc);
+    if (nocc) {
+      auto* recs = static_cast<unsigned long long*>(X->workspace("ces_recs", size_t(nocc) * 48 + 64));
+      HIP_TRY(launch_table_records(P, cap, occ, recs, nocc, st));
+      HIP_TRY(hipMemcpyAsync(keys.data(), recs, nocc * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipStreamSynchronize(st));
+    }
+    // key string of each cell: groupBys.map(g => tags.getOrElse(g, "")).mkString(":") (Aggregator.scala:53-56)
+    std::vector<std::string> kstr(nocc);
+    for (size_t gi2 = 0; gi2 < R.group_bys.size(); gi2++) {
+      StrCol& sc = strs[size_t(str_index(R.group_bys[gi2]))];
+      GlobalDict& gd = E.dict(sc.name);
+      std::lock_guard<std::mutex> g(gd.mu);
+      for (size_t i = 0; i < nocc; i++) {
+        const uint32_t d = uint32_t((keys[i] % ngroups) / (sc.stride ? sc.stride : 1) % sc.ndim);
+        if (gi2) kstr[i] += ':';
+        if (d != sc.dim_null && sc.stride) {
+          const std::string& v = sc.dim_value(d, gd);
+          if (!null_like(v)) kstr[i] += v;
+        }
+      }
+    }
+    std::map<std::pair<uint64_t, uint32_t>, size_t> at;   // (step, glob) -> row
+    for (size_t i = 0; i < nocc; i++) {
+      const unsigned long long cell = keys[i];
+      const uint64_t b = (cell / ngroups) % nbuckets;
+      const uint32_t slot = per_glob_rows ? uint32_t(cell / ngroups / nbuckets) : 0u;
+      auto ins = at.emplace(std::make_pair(b, slot), ces_rows.size());
+      if (ins.second) ces_rows.push_back(CesRow{bucket_base + int64_t(b) * P.step, slot, hll::Sketch{}});
+      ces_rows[ins.first->second].h.update(kstr[i]);
+    }
+    std::vector<CesRow> sorted;   // std::map order: (step, glob) ascending
+    sorted.reserve(ces_rows.size());
+    for (auto& kv : at) sorted.push_back(std::move(ces_rows[kv.second]));
+    ces_rows.swap(sorted);
+    nrows_out = uint32_t(ces_rows.size());
+  }
+  if (ces) {
+  } else if (sketch) {
     if (emit) {
       SParams S2{};
       S2.keys = P.hkeys;
@@ -1243,7 +1309,14 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
   res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
-  if (sketch) {
+  if (ces) {
+    for (size_t r = 0; r < nrows_out; r++) {
+      res->ts[r] = ces_rows[r].ts;
+      res->val[r] = ces_rows[r].h.estimate();
+      res->gid[r] = 0;
+      if (per_glob_rows) res->glob[r] = ces_rows[r].glob;
+    }
+  } else if (sketch) {
     res->sketches.reserve(nrows_out);
     for (size_t r = 0; r < nrows_out; r++) {
       const SkRow& k = sk_rows[r];
@@ -1291,7 +1364,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::vector<std::string> qt_keys;
   for (auto& g : globs)
     for (auto& kv : g.query_tags)
-      if (!tagq && !sketch && std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
+      if (!tagq && !sketch && !ces && std::find(qt_keys.begin(), qt_keys.end(), kv.first) == qt_keys.end()) qt_keys.push_back(kv.first);
   for (auto& k : qt_keys) res->tag_names.push_back(k);
   // Per tag column: how a row's group id decodes to the tag string (lk_result::tag; nullptr: tag dropped,
   // Commons.scala:433).  Strings local to this call (filter candidates, the distributed union) move into the
@@ -1327,6 +1400,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   }
   if (sketch && gbs.empty()) res->tcols[0].null_value = "";   // key tags {"name": ""} (getOrElse(NAME, ""))
   if (sketch && !gbs.empty()) res->tcols[0].hidden = true;     // key tags: the groupBys only
+  if (ces)   // the HLL SketchInput carries no tags (Aggregator.scala:58)
+    for (auto& tc : res->tcols) tc.hidden = true;
   if (tagq) {
     // Tag-query rows (Commons.toDataPoint, Commons.scala:406-423): every column becomes a tag -- the tag and
     // "count" (COUNT(*) via getString) -- then NoisyTagsDropper.remove (NoisyTagsDropper.scala) drops hidden
@@ -1345,7 +1420,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
   }
   res->qt_of_glob.resize(globs.size());
-  for (size_t gi = 0; gi < globs.size() && !sketch; gi++)
+  for (size_t gi = 0; gi < globs.size() && !sketch && !ces; gi++)
     for (auto& kv : globs[gi].query_tags) {
       size_t c = nreg + size_t(std::find(qt_keys.begin(), qt_keys.end(), kv.first) - qt_keys.begin());
       res->owned.push_back(kv.second);

@@ -30,6 +30,7 @@ struct FParams {
 constexpr int AGG_AVG = 4;
 constexpr int AGG_ROWS = 5;        // COUNT(*): passing rows, NULL values included (tag queries)
 constexpr int AGG_SKETCH = 6;      // percentiles: COUNT per (cell, DDSketch bin) (P.sketch), sketches on the host
+constexpr int AGG_CES = 7;         // cardinality estimates: distinct (cell) set, HLL per step on the host
 
 struct RParams {                   // rekey_minmax: per-glob uncollapsed table -> merged collapsed table
   const unsigned long long* in_rows;

@@ -227,7 +227,7 @@ def check_hot_path(pr: PushDownRequest) -> None:
     if pr.isTagQuery or be.chart is None:
         raise NotImplementedError("tag/exemplar queries are outside the hot path")
     agg = be.chart.aggregation
-    if is_percentile(agg) and be.dataset != METRICS:
+    if (is_percentile(agg) or is_ces(be)) and be.dataset != METRICS:
         pass
     elif agg not in (SUM, MIN, MAX, COUNT, AVG):
         raise NotImplementedError(f"aggregation {agg} (sketch path) is outside the hot path")
@@ -501,7 +501,7 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
             tags = dict(qtags)                                        # Commons.scala:450-452
         cell.tags = tags
         out.append(cell)
-    std = chart.aggregation in (SUM, MIN, MAX, COUNT, AVG)
+    std = chart.aggregation in (SUM, MIN, MAX, COUNT, AVG) and not is_ces(be)
     out.sort(key=lambda c: (c.ts, sorted(c.tags.items()), c.agg_value(chart.aggregation) if std else 0.0))
     return out
 
@@ -834,3 +834,35 @@ def merge_percentile(pr: PushDownRequest, per_glob) -> List[Tuple[int, Dict[str,
                     acc[key] = (dict(kt), acc[key][1])
                 acc[key][1].merge(sk)
     return [(k[0], acc[k][0], acc[k][1]) for k in sorted(acc)]
+
+
+# ----------------------------------------------------------------------------------------------
+# Cardinality estimates (`ces`): one HLL per step over the group-key strings
+# ----------------------------------------------------------------------------------------------
+def is_ces(be: BaseExpr) -> bool:
+    c = be.chart
+    return c is not None and (c.aggregation == "ces" or "ces" in (c.rollup or ""))
+
+
+def evaluate_ces_per_glob(pr: PushDownRequest, glob_size: int, paths: Sequence[str], sources=None):
+    """Per glob: [(ts, key set)] ascending in ts.  Each passing row feeds its step's HLL the string
+    groupBys.map(g => tags.getOrElse(g, "")).mkString(":") (Aggregator.scala:53-56; tags after toDataPoint's
+    NULL / "null" / "" drop, Commons.scala:433).  The set of strings determines the HLL state."""
+    gbs = pr.baseExpr.chart.groupBys
+    out = []
+    for g in globs_of(pr, glob_size):
+        cells = evaluate_glob(pr, g, [paths[i] for i in g], None if sources is None else [sources[i] for i in g])
+        acc: Dict[int, set] = {}
+        for c in cells:
+            acc.setdefault(c.ts, set()).add(":".join(c.tags.get(x, "") for x in gbs))
+        out.append([(ts, acc[ts]) for ts in sorted(acc)])
+    return out
+
+
+def merge_ces(per_glob) -> List[Tuple[int, set]]:
+    """query-api: HLL union per timestamp (TimeGroupedSketchAggregator.scala:38-43) = the union of the key sets."""
+    acc: Dict[int, set] = {}
+    for rows in per_glob:
+        for ts, ks in rows:
+            acc.setdefault(ts, set()).update(ks)
+    return [(ts, acc[ts]) for ts in sorted(acc)]

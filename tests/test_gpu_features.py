@@ -194,3 +194,38 @@ def test_percentile_sketches(engine, tmp_path):
         merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
         got = [(int(merged.ts[r]), merged.tags[r], float(merged.values[r]), merged.sketch(r)) for r in range(len(merged))]
         _pct_rows_equal(got, dx.merge_percentile(pr, want), q, f"{agg} merged")
+
+
+def test_cardinality_estimates(engine):
+    """`ces` (cardinality, HLL per step): per-glob and merged (union) estimates equal the oracle's HLL over the
+    distinct group-key strings per step -- exact key counts below 384 coupons, the HLL estimate above (a 10K-value
+    container key); NULL group values join as ""; no groupBys: every key is "" (ignored) -> 0."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx, hll
+    keys, blobs, segs = [], [], []
+    for i in range(4):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 19, null_frac=0.05, highcard_n=10_000,
+                                                  rg_rows=1 << 18, page_rows=1 << 15))
+        key = f"ces/{i}"
+        engine.put_segment_ptr(key, s.ptr, s.size)
+        blobs.append(s.bytes())
+        s.free()
+        keys.append(key)
+        segs.append(synth.segment_request(i, step=600_000))
+    for filt, gbs, agg, rollup in [(synth.leaf(synth.NAME, "eq", "metric_03"), [synth.SERVICE, synth.NAMESPACE], "count", "ces"),
+                                   (synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), [synth.CONTAINER], "ces", None),
+                                   (synth.leaf(synth.SERVICE, "regex", "svc-00[0-4]"), [], "ces", None)]:
+        req_d = synth.pushdown(filt, segs, agg, gbs)
+        if rollup:
+            req_d["baseExpr"]["chart"]["rollup"] = rollup
+        req = json.dumps(req_d)
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_ces_per_glob(pr, 2, keys, sources=blobs)
+        res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        got = [[(int(res.ts[r]), float(res.values[r])) for r in range(len(res)) if int(res.globs[r]) == gi]
+               for gi in range(len(want))]
+        assert got == [[(ts, hll.estimate(ks)) for ts, ks in w] for w in want], (gbs, agg)
+        assert all(t == {} for t in res.tags)
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert [(int(t), float(v)) for t, v in zip(merged.ts, merged.values)] == \
+            [(ts, hll.estimate(ks)) for ts, ks in dx.merge_ces(want)], (gbs, agg)
