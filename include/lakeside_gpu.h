@@ -40,7 +40,10 @@ enum {
 #define LK_PLAN_BYTES 4u      /* optional, with either: the scan kernel counts the bytes its plan reads
                                  (lk_result_stats "plan_bytes"; measurement only, costs ~5% of scan time) */
 
-/* options_json: {"device": 0, "rank": 0, "world": 1}; NULL = defaults.
+/* options_json: {"device": 0, "hbm_budget_bytes": N, "max_calls": 4}; NULL = defaults.
+ * hbm_budget_bytes: weight bound of the HBM segment cache (the worker's Caffeine cache weight,
+ * query-worker/.../WorkerApi.scala:53-64): inserting past it evicts least-recently-used segments; 0 (default) = no
+ * bound, eviction only when HBM runs out.  max_calls: evaluations in flight (one stream each).
  * Replaces DuckDbConnectionFactory (core/.../utils/DuckDbConnectionFactory.scala:76-114). */
 int lk_engine_create(const char* options_json, lk_engine** out);
 void lk_engine_destroy(lk_engine* e);

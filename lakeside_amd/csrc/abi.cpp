@@ -60,6 +60,11 @@ int lk_engine_create(const char* options_json, lk_engine** out) {
     auto* e = new lk_engine();
     try {
       e->e = std::make_unique<lk::Engine>(dev);
+      if (options_json && *options_json) {
+        lk::Json o = lk::Json::parse(options_json);
+        if (const lk::Json* b = o.get("hbm_budget_bytes")) e->e->hbm_budget = size_t(b->as_i64());
+        if (const lk::Json* c = o.get("max_calls")) e->e->max_calls = size_t(std::max<int64_t>(1, c->as_i64()));
+      }
     } catch (...) {
       delete e;
       throw;

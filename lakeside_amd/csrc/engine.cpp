@@ -645,13 +645,42 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
   return S;
 }
 
+size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep) {
+  size_t freed = 0;
+  while (cache_bytes > target_bytes) {
+    auto victim = cache.end();
+    for (auto it = cache.begin(); it != cache.end(); ++it)
+      if (it->first != keep && (victim == cache.end() || it->second->last_use < victim->second->last_use)) victim = it;
+    if (victim == cache.end()) break;
+    const size_t b = victim->second->data_bytes + victim->second->meta_bytes;
+    cache_bytes -= b;
+    freed += b;
+    evictions++;
+    cache.erase(victim);
+  }
+  return freed;
+}
+
 int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size) {
-  auto S = build_segment(key, data, size);
+  std::shared_ptr<Segment> S;
+  try {
+    S = build_segment(key, data, size);
+  } catch (const DeviceError&) {
+    // HBM exhausted: make room by evicting least recently used segments (about twice the file), then retry once
+    {
+      std::lock_guard<std::mutex> g(cache_mu);
+      const size_t want = 2 * size + (64u << 20);
+      if (evict_lru_locked(cache_bytes > want ? cache_bytes - want : 0, key) == 0) throw;
+    }
+    S = build_segment(key, data, size);
+  }
+  S->last_use = ++use_clock;
   std::lock_guard<std::mutex> g(cache_mu);
   auto it = cache.find(key);
   if (it != cache.end()) cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
   cache_bytes += S->data_bytes + S->meta_bytes;
   cache[key] = S;
+  if (hbm_budget) evict_lru_locked(hbm_budget, key);
   return LK_OK;
 }
 
@@ -659,7 +688,10 @@ std::shared_ptr<Segment> Engine::get_segment(const std::string& key, bool load_o
   {
     std::lock_guard<std::mutex> g(cache_mu);
     auto it = cache.find(key);
-    if (it != cache.end()) return it->second;
+    if (it != cache.end()) {
+      it->second->last_use = ++use_clock;
+      return it->second;
+    }
   }
   if (!load_on_miss) return nullptr;
   std::ifstream f(key, std::ios::binary);

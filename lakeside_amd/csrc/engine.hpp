@@ -1,5 +1,6 @@
 // Engine state shared by engine.cpp (segment cache), eval.cpp (query evaluation), comm.cpp (RCCL).
 #pragma once
+#include <atomic>
 #include <hip/hip_runtime.h>
 
 #include <condition_variable>
@@ -82,6 +83,7 @@ struct Segment {
   size_t data_bytes = 0;
   void* d_meta = nullptr;
   size_t meta_bytes = 0;
+  std::atomic<uint64_t> last_use{0};             // LRU clock value of the last lookup (cache eviction)
   int col_index(const std::string& name) const;
   ~Segment();
 };
@@ -152,6 +154,14 @@ struct Engine {
   std::mutex cache_mu;
   std::unordered_map<std::string, std::shared_ptr<Segment>> cache;
   size_t cache_bytes = 0;
+  // HBM budget of the segment cache (lk_engine_create {"hbm_budget_bytes": N}; 0 = none): inserting past it evicts
+  // the least recently used segments, as the worker's weighted Caffeine cache does (WorkerApi.scala:53-64).  A
+  // segment an evaluation still holds is freed when that evaluation drops it.
+  size_t hbm_budget = 0;
+  std::atomic<uint64_t> use_clock{0};
+  size_t evictions = 0;
+  // evict LRU segments (never `keep`) until cache_bytes + extra <= budget; caller holds cache_mu
+  size_t evict_lru_locked(size_t target_bytes, const std::string& keep);
   std::mutex dict_mu;
   std::unordered_map<std::string, std::unique_ptr<GlobalDict>> dicts;
   std::mutex leaf_mu;

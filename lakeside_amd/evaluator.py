@@ -110,10 +110,11 @@ class Result:
 class Engine:
     """One per process per GPU: HIP device, stream, HBM segment cache, optional RCCL communicator."""
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, hbm_budget_bytes: int = 0, max_calls: int = 4):
         L = _lib.lib()
         h = ctypes.c_void_p()
-        check(L.lk_engine_create(json.dumps({"device": device}).encode(), ctypes.byref(h)))
+        opts = {"device": device, "hbm_budget_bytes": int(hbm_budget_bytes), "max_calls": int(max_calls)}
+        check(L.lk_engine_create(json.dumps(opts).encode(), ctypes.byref(h)))
         self._h = h
         self.device = device
 

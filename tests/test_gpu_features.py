@@ -229,3 +229,37 @@ def test_cardinality_estimates(engine):
         merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
         assert [(int(t), float(v)) for t, v in zip(merged.ts, merged.values)] == \
             [(ts, hll.estimate(ks)) for ts, ks in dx.merge_ces(want)], (gbs, agg)
+
+
+def test_hbm_budget_lru_eviction():
+    """HBM segment cache with a weight bound (lk_engine_create hbm_budget_bytes; the worker's weighted Caffeine
+    cache, WorkerApi.scala:53-64): inserts past the budget evict the least recently used segments; a segment used
+    by a query is recent; an evicted key is re-loaded on demand (here: put again) and answers identically."""
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd.evaluator import Engine
+    blobs = []
+    for i in range(4):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 18, rg_rows=1 << 17, page_rows=1 << 15))
+        blobs.append(s.bytes())
+        s.free()
+    probe = Engine(0)
+    probe.put_segment("p", blobs[0])
+    one = probe.segment_bytes()
+    probe.close()
+    e = Engine(0, hbm_budget_bytes=int(2.5 * one))
+    try:
+        req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), [synth.segment_request(0)]))
+        e.put_segment("s0", blobs[0])
+        e.put_segment("s1", blobs[1])
+        want = e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows()   # s0 becomes the most recent
+        e.put_segment("s2", blobs[2])                              # over budget: s1 (LRU) goes
+        assert e.segment_count() == 2 and e.segment_bytes() <= int(2.5 * one)
+        assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
+        with pytest.raises(Exception):
+            e.eval_pushdown(req, ["s1"], 10, LK_MERGED)             # evicted, and not a file path
+        e.put_segment("s3", blobs[3])                              # s2 is now the LRU
+        assert e.segment_count() == 2
+        e.put_segment("s0", blobs[0])
+        assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
+    finally:
+        e.close()
