@@ -683,9 +683,16 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       // name page has a small dictionary (lean_tile's test at page granularity)
       if (all_lean) {
         const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
-        const int cn = strs.size() == 1 ? S.col_index(strs[0].name) : -1;
+        const int cn = strs.size() <= 3 ? S.col_index(strs[0].name) : -1;
         all_lean = ct >= 0 && cv >= 0 && cn >= 0 && !S.cols[ct].any_nulls && !S.cols[cv].any_nulls &&
                    !S.cols[cn].any_nulls;
+        for (size_t s2 = 1; s2 < strs.size() && all_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
+          const int cl = S.col_index(strs[s2].name);
+          if (cl < 0) continue;
+          if (S.cols[cl].any_nulls) all_lean = false;
+          for (const PageDesc& pg : S.cols[cl].pages)
+            if (pg.kind != PAGE_DICT || pg.bw > 32) { all_lean = false; break; }
+        }
         if (all_lean)
           for (const PageDesc& pg : S.cols[cn].pages)
             if (pg.kind != PAGE_DICT || pg.dict_n > 64 || pg.bw < 1 || pg.bw > 6) { all_lean = false; break; }
@@ -896,7 +903,11 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
   // single string column (filter and group dim on `name` only): NULL-free tiles with a small chunk dictionary go
   // to scan_lean (lean_kernel.hpp), the rest to scan_tiles
-  P.lean_split = (P.nstr == 1 && P.truth && agg != AGG_ROWS && !sketch && !getenv("LK_NO_LEAN_SPLIT")) ? (all_lean ? 2u : 1u) : 0u;
+  // single string column (filter and group dim on `name` only), or name early with every other string column late
+  // (<= 2 of them): NULL-free tiles with a small name dictionary go to scan_lean (lean_kernel.hpp), the rest to
+  // scan_tiles
+  const bool lean_shape = P.nstr == 1 || (P.nstr <= 3 && P.late_mask == ((1u << P.nstr) - 2u));
+  P.lean_split = (lean_shape && P.truth && agg != AGG_ROWS && !sketch && !getenv("LK_NO_LEAN_SPLIT")) ? (all_lean ? 2u : 1u) : 0u;
   if (sketch) {
     P.sketch = 1;
     P.dd_mult = dd::mapping().multiplier;

@@ -25,6 +25,7 @@ namespace lk {
 constexpr int LEAN_H = HCAP / 2;                                 // LDS cells (a tile touches few)
 constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a tile, upper bound
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
+constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -36,8 +37,10 @@ struct LeanRun {            // one run of the name column over the tile (24 B)
   uint32_t cbk;             // chunk index of the run's chunk k = 0 (so k = q - cbk)
 };
 
+template <int NL>
 struct LeanLds {
   static constexpr int H = LEAN_H;
+  static constexpr int NLA = NL > 0 ? NL : 1;
   LeanRun runs[RUN_CAP];
   uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
   uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
@@ -50,16 +53,45 @@ struct LeanLds {
   unsigned long long hval[1];
   uint32_t hfull;
   uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
+  // late columns (NL > 0): value runs (+ sentinel), run-block tables, lookup values, the late conjuncts' table
+  LRun lruns[NLA][NL > 0 ? RUN_CAP + 1 : 1];
+  uint8_t lrblk[NLA][NL > 0 ? TILE_ROWS / 64 + 8 : 1];
+  uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
+  uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
+  uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
 };
 
-// The tile qualifies for scan_lean (uniform: scalar loads).  scan_tiles applies the same test to skip it.
-__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t) {
+// The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
+// same test to skip it.  Late columns (query columns 3 .. 2 + nl) must hold no NULL over the tile (value index =
+// row) or be absent from the segment.
+__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t, uint32_t nl) {
   if (!Sp->cols[0].present || !Sp->cols[1].present || !Sp->cols[2].present) return false;
   const TileCol* a = Sp->cols[0].tcols + t;
   const TileCol* b = Sp->cols[1].tcols + t;
   const TileCol* c = Sp->cols[2].tcols + t;
-  return !a->has_nulls && !b->has_nulls && !c->has_nulls && c->kind == PAGE_DICT && c->dict_n <= 64u &&
-         c->nruns > 0u && c->bw >= 1u && c->bw <= 6u;
+  if (a->has_nulls || b->has_nulls || c->has_nulls || c->kind != PAGE_DICT || c->dict_n > 64u || c->nruns == 0u ||
+      c->bw < 1u || c->bw > 6u)
+    return false;
+  for (uint32_t k = 0; k < nl; k++) {
+    if (!Sp->cols[3 + k].present) continue;
+    const TileCol* l = Sp->cols[3 + k].tcols + t;
+    if (l->has_nulls || l->kind != PAGE_DICT || l->nruns == 0u || l->bw > 32u) return false;
+  }
+  return true;
+}
+
+// Run of value v among `n` staged runs (+ sentinel) through a 64-value-block table (blk[b]: run holding vbase + 64b).
+__device__ __forceinline__ int lean_find_run(const LRun* runs, const uint8_t* blk, uint32_t nb, uint32_t vbase,
+                                             uint32_t v) {
+  uint32_t b = (v - vbase) >> 6;
+  b = b < nb ? b : nb - 1u;
+  int lo = blk[b], hi = blk[b + 1];
+  while (lo < hi) {
+    const int m = (lo + hi + 1) >> 1;
+    if (runs[m].start <= v) lo = m;
+    else hi = m - 1;
+  }
+  return lo;
 }
 
 // Code e (0..15) of a 16-code window of BW-bit fields held in w0..w2 (by value: no address-taken selects).
@@ -71,9 +103,10 @@ __device__ __forceinline__ uint32_t lean_code(uint32_t w0, uint32_t w1, uint32_t
   return __builtin_amdgcn_alignbit(hi, lo, off) & ((1u << BW) - 1u);
 }
 
-template <int AGG, bool HASH>
+template <int AGG, bool HASH, int NL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void scan_lean(QParams P) {
-  __shared__ LeanLds L;
+  using LT = LeanLds<NL>;
+  __shared__ LT L;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const QSeg* Sp = P.segs + blockIdx.y;
@@ -82,7 +115,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   const TileDesc* tdp = Sp->tiles + t;
   const int64_t win_lo = Sp->win_lo, win_hi = Sp->win_hi;
   if (tdp->ts_max < win_lo || tdp->ts_min >= win_hi) return;    // zone map: outside the glob window
-  if (!lean_tile(Sp, t)) return;
+  if (!lean_tile(Sp, t, NL)) return;
   const TileCol* tc0 = Sp->cols[0].tcols + t;
   const TileCol* tc1 = Sp->cols[1].tcols + t;
   const TileCol* tc2 = Sp->cols[2].tcols + t;
@@ -101,7 +134,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       L.lut[tid] = tab ? tab[g] : g;
     }
   }
-  for (int i = tid; i < LeanLds::H; i += BLOCK) {
+  for (int i = tid; i < LT::H; i += BLOCK) {
     L.hkey[i] = EMPTY;
     L.hrows[i] = 0;
     L.hcnt[i] = 0;
@@ -109,8 +142,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
     else L.hhi[i] = 0.0;
   }
-  if (count_plan)
+  if (count_plan) {
     for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) L.lines_t[i] = L.lines_v[i] = 0u;
+#pragma unroll
+    for (int k = 0; k < NL; k++)
+      for (uint32_t i = tid; i < LEAN_LLINES; i += BLOCK) L.lines_l[k][i] = 0u;
+  }
   if (tid == 0) L.hfull = 0u;
   __syncthreads();
 
@@ -124,11 +161,53 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       const uint32_t lmask = P.strp[0].lmask;
       const uint32_t T = bits & lmask & ~lf, F = (~bits & lmask) | lf;
       const uint32_t ix = T | (F << P.nleaves);
-      pass = (P.truth[ix >> 5] >> (ix & 31)) & 1u;
+      pass = ((NL > 0 ? P.truth_early : P.truth)[ix >> 5] >> (ix & 31)) & 1u;
     }
     emask = __ballot(pass);
   }
   if (!emask) return;   // no row of the tile passes (uniform: every thread leaves; nothing staged to flush)
+
+  // late columns: runs, lookup values, the late conjuncts' truth table (run-block tables after the next barrier)
+  const uint32_t nblk = (nrows + 63u) / 64u;
+  uint32_t lpres = 0, llut_on = 0;          // bit k: late column k present / its lookup values in LDS
+  uint32_t lnr[LT::NLA], lvb[LT::NLA], lbw[LT::NLA];
+  __amdgpu_buffer_rsrc_t lrs[LT::NLA];
+  const uint32_t* lremap[LT::NLA];
+#pragma unroll
+  for (int k = 0; k < NL; k++) {
+    lnr[k] = lvb[k] = lbw[k] = 0;
+    lremap[k] = nullptr;
+    lrs[k] = make_rsrc(Sp->base, 0u);
+    if (!Sp->cols[3 + k].present) continue;
+    const TileCol* tl = Sp->cols[3 + k].tcols + t;
+    lpres |= 1u << k;
+    lnr[k] = tl->nruns;
+    lvb[k] = tl->vbase;
+    lbw[k] = tl->bw;
+    lrs[k] = make_rsrc(Sp->base + tl->vals, tl->vals_len + 8u);
+    lremap[k] = Sp->cols[3 + k].remap + tl->remap;
+    const RunDesc* rr = Sp->cols[3 + k].runs + tl->run_lo;
+    for (uint32_t i = tid; i < lnr[k]; i += BLOCK) {
+      const RunDesc r = rr[i];
+      L.lruns[k][i] = LRun{r.start, r.off_lit, r.value};
+      if (i == lnr[k] - 1) L.lruns[k][lnr[k]] = LRun{r.start + r.count, 0u, 0u};
+    }
+    const uint32_t dn = tl->dict_n;
+    if (dn <= LUT_CAP) {
+      llut_on |= 1u << k;
+      const uint32_t* tab = P.strp[1 + k].strtab;
+      for (uint32_t i = tid; i < dn; i += BLOCK) {
+        const uint32_t g = lremap[k][i];
+        L.llut[k][i] = tab ? tab[g] : g;
+      }
+    }
+    if (count_plan && tid == 0)
+      pbytes += sizeof(TileCol) + uint64_t(lnr[k]) * sizeof(RunDesc) + ((llut_on >> k) & 1u ? uint64_t(dn) * 8u : 0u);
+  }
+  if (NL > 0) {
+    const uint32_t words = ((1u << (2 * P.nleaves)) + 31) / 32;
+    for (uint32_t i = tid; i < words; i += BLOCK) L.ltruth[i] = P.truth_late[i];
+  }
 
   // runs of the tile: value range inside the tile, chunk counts (useful runs only)
   if (uint32_t(tid) < nr) {
@@ -143,6 +222,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     if (count_plan && lit && lo < hi) pbytes += (uint64_t(hi - lo) * bw + 7u) / 8u;   // codes decoded in full
   }
   __syncthreads();
+#pragma unroll
+  for (int k = 0; k < NL; k++)   // run-block tables of the late columns (runs staged above)
+    if ((lpres >> k) & 1u)
+      for (uint32_t b = tid; b <= nblk; b += BLOCK) {
+        uint32_t lo = 0;
+        const uint32_t v = lvb[k] + 64u * b;
+#pragma unroll
+        for (uint32_t st = RUN_CAP / 2; st >= 1; st >>= 1) {
+          const uint32_t m = lo + st;
+          lo = (m < lnr[k] && L.lruns[k][m].start <= v) ? m : lo;
+        }
+        L.lrblk[k][b] = uint8_t(lo);
+      }
   if (tid < 64) {   // exclusive prefix of the chunk counts (<= 128 runs: two per lane)
     const uint32_t i0 = 2u * uint32_t(lane), i1 = i0 + 1u;
     const uint32_t n0 = i0 < nr ? L.cb[i0] : 0u, n1 = i1 < nr ? L.cb[i1] : 0u;
@@ -204,6 +296,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   }
   const bool one_bucket = tile_b >= 0;
   const uint32_t step32 = uint32_t(P.step);
+  bool late_trivial = true;   // no filter leaf on a late column: the late stage only adds group terms (uniform)
+#pragma unroll
+  for (int k = 0; k < NL; k++) late_trivial = late_trivial && P.strp[1 + k].lmask == 0u;
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
@@ -328,14 +423,91 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         const uint32_t e2 = two ? (uint32_t(__builtin_ctzll(m)) >> shs) : e1;
         if (two) m &= m - 1ull;
         const uint32_t r1 = rbase + e1, r2 = rbase + e2;
-        v2u t1 = v2u{0u, 0u}, t2 = v2u{0u, 0u}, x1 = v2u{0u, 0u}, x2 = v2u{0u, 0u};
-        if (!one_bucket) {
-          t1 = __builtin_amdgcn_raw_buffer_load_b64(rs0, (vb0 + r1) * 8u, 0, 0);
-          t2 = __builtin_amdgcn_raw_buffer_load_b64(rs0, two ? (vb0 + r2) * 8u : OOB, 0, 0);
+        uint32_t d1 = dim_u, d2 = dim_u;
+        if (npass > 1) {   // uniform: the rows' codes -> group terms
+          d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
+          d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
         }
-        if (AGG != AGG_COUNT) {
-          x1 = __builtin_amdgcn_raw_buffer_load_b64(rs1, (vb1 + r1) * 8u, 0, 0);
-          x2 = __builtin_amdgcn_raw_buffer_load_b64(rs1, two ? (vb1 + r2) * 8u : OOB, 0, 0);
+        bool p1 = true, p2 = two;
+        v2u t1 = v2u{0u, 0u}, t2 = v2u{0u, 0u}, x1 = v2u{0u, 0u}, x2 = v2u{0u, 0u};
+        auto gather = [&]() __attribute__((always_inline)) {   // timestamps / values of the passing rows
+          if (!one_bucket) {
+            t1 = __builtin_amdgcn_raw_buffer_load_b64(rs0, p1 ? (vb0 + r1) * 8u : OOB, 0, 0);
+            t2 = __builtin_amdgcn_raw_buffer_load_b64(rs0, p2 ? (vb0 + r2) * 8u : OOB, 0, 0);
+          }
+          if (AGG != AGG_COUNT) {
+            x1 = __builtin_amdgcn_raw_buffer_load_b64(rs1, p1 ? (vb1 + r1) * 8u : OOB, 0, 0);
+            x2 = __builtin_amdgcn_raw_buffer_load_b64(rs1, p2 ? (vb1 + r2) * 8u : OOB, 0, 0);
+          }
+        };
+        if constexpr (NL > 0) {
+          // late columns of both rows: run lookup + packed-word load (in flight together); with no late filter
+          // leaf every row passes, so the timestamp / value loads go out with them
+          v2u lw1[LT::NLA], lw2[LT::NLA];
+          uint32_t lm1[LT::NLA], lm2[LT::NLA];
+#pragma unroll
+          for (int k = 0; k < NL; k++) {
+            lw1[k] = lw2[k] = v2u{0u, 0u};
+            lm1[k] = lm2[k] = 0u;
+            if (!((lpres >> k) & 1u)) continue;   // uniform
+            auto issue = [&](uint32_t r, bool live, v2u& w, uint32_t& meta) __attribute__((always_inline)) {
+              const uint32_t v = lvb[k] + r;
+              const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
+              const LRun rr = L.lruns[k][ri];
+              const bool lt = (rr.off_lit & 0x80000000u) != 0u;
+              const uint32_t bit = (v - rr.start) * lbw[k];
+              const uint32_t byte = (rr.off_lit & 0x7fffffffu) + (bit >> 3);
+              w = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], (live && lt) ? (byte & ~3u) : OOB, 0, 0);
+              meta = lt ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : rr.value;
+              if (count_plan && live && lt) {   // distinct 128-B lines of the late stream gathered
+                const uint32_t l = ((byte & ~3u) >> 7) - ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
+                if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
+              }
+            };
+            issue(r1, true, lw1[k], lm1[k]);
+            issue(r2, two, lw2[k], lm2[k]);
+          }
+          if (late_trivial) gather();
+          uint32_t T1 = 0, F1 = 0, T2 = 0, F2 = 0;
+#pragma unroll
+          for (int k = 0; k < NL; k++) {
+            const StrParam sp = P.strp[1 + k];
+            if (!((lpres >> k) & 1u)) {   // absent column: NULL in every row
+              d1 += sp.dim_null * sp.dim_stride;
+              d2 += sp.dim_null * sp.dim_stride;
+              F1 |= sp.hmask;
+              F2 |= sp.hmask;
+              continue;
+            }
+            const uint32_t bwk = lbw[k];
+            const uint32_t msk = bwk >= 32u ? ~0u : ((1u << bwk) - 1u);
+            auto look = [&](v2u w, uint32_t meta, uint32_t& d, uint32_t& T, uint32_t& F) __attribute__((always_inline)) {
+              const uint64_t x = ((uint64_t)w.y << 32) | w.x;
+              const uint32_t idx = (meta >> 31) ? uint32_t(x >> (meta & 63u)) & msk : meta;
+              uint32_t packed;
+              if ((llut_on >> k) & 1u) {
+                packed = L.llut[k][idx < LUT_CAP ? idx : 0u];
+              } else {
+                const uint32_t g = lremap[k][idx];
+                packed = sp.strtab ? sp.strtab[g] : g;
+              }
+              const uint32_t bits = (packed >> 24) << sp.lbase;
+              d += (packed & DIM_MASK) * sp.dim_stride;
+              T |= bits & sp.lmask;
+              F |= ~bits & sp.lmask;
+            };
+            look(lw1[k], lm1[k], d1, T1, F1);
+            look(lw2[k], lm2[k], d2, T2, F2);
+          }
+          if (!late_trivial) {
+            const uint32_t lf = Sp->leaf_false;
+            const uint32_t ix1 = (T1 & ~lf) | ((F1 | lf) << P.nleaves), ix2 = (T2 & ~lf) | ((F2 | lf) << P.nleaves);
+            p1 = (L.ltruth[ix1 >> 5] >> (ix1 & 31)) & 1u;
+            p2 = two && ((L.ltruth[ix2 >> 5] >> (ix2 & 31)) & 1u);
+            gather();
+          }
+        } else {
+          gather();
         }
         if (count_plan) {
           auto mark = [&](uint32_t* bm, uint32_t off, uint32_t line0) __attribute__((always_inline)) {
@@ -343,21 +515,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             atomicOr(&bm[l >> 5], 1u << (l & 31u));
           };
           if (!one_bucket) {
-            mark(L.lines_t, (vb0 + r1) * 8u, line_t0);
-            if (two) mark(L.lines_t, (vb0 + r2) * 8u, line_t0);
+            if (p1) mark(L.lines_t, (vb0 + r1) * 8u, line_t0);
+            if (p2) mark(L.lines_t, (vb0 + r2) * 8u, line_t0);
           }
           if (AGG != AGG_COUNT) {
-            mark(L.lines_v, (vb1 + r1) * 8u, line_v0);
-            if (two) mark(L.lines_v, (vb1 + r2) * 8u, line_v0);
+            if (p1) mark(L.lines_v, (vb1 + r1) * 8u, line_v0);
+            if (p2) mark(L.lines_v, (vb1 + r2) * 8u, line_v0);
           }
         }
-        uint32_t d1 = dim_u, d2 = dim_u;
-        if (npass > 1) {   // uniform: the rows' codes -> group terms
-          d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
-          d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
-        }
-        row((int64_t)(((uint64_t)t1.y << 32) | t1.x), __longlong_as_double((long long)(((uint64_t)x1.y << 32) | x1.x)), d1);
-        if (two)
+        if (p1)
+          row((int64_t)(((uint64_t)t1.y << 32) | t1.x), __longlong_as_double((long long)(((uint64_t)x1.y << 32) | x1.x)), d1);
+        if (p2)
           row((int64_t)(((uint64_t)t2.y << 32) | t2.x), __longlong_as_double((long long)(((uint64_t)x2.y << 32) | x2.x)), d2);
       }
     }
@@ -378,9 +546,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       pbytes += sizeof(TileDesc) + 3 * sizeof(TileCol) + uint64_t(nr) * sizeof(RunDesc) + uint64_t(dict_n) * 8u;
     }
     for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_t[i]) + __popc(L.lines_v[i]));
+#pragma unroll
+    for (int k = 0; k < NL; k++)
+      for (uint32_t i = tid; i < LEAN_LLINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_l[k][i]));
     if (pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
   }
-  for (int i = tid; i < LeanLds::H; i += BLOCK) {
+  for (int i = tid; i < LT::H; i += BLOCK) {
     if (L.hkey[i] == EMPTY) continue;
     global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
                             reinterpret_cast<unsigned long long*>(L.hhi)[i]);

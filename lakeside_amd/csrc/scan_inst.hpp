@@ -11,7 +11,13 @@ namespace lk {
 template <int AGG, bool HASH>
 static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
   const dim3 block(BLOCK);
-  if (P.lean_split) hipLaunchKernelGGL((scan_lean<AGG, HASH>), grid, block, 0, st, P);   // lean tiles first
+  if (P.lean_split) {   // lean tiles first (lean_kernel.hpp), by late string columns
+    switch (P.nstr) {
+      case 1: hipLaunchKernelGGL((scan_lean<AGG, HASH, 0>), grid, block, 0, st, P); break;
+      case 2: hipLaunchKernelGGL((scan_lean<AGG, HASH, 1>), grid, block, 0, st, P); break;
+      default: hipLaunchKernelGGL((scan_lean<AGG, HASH, 2>), grid, block, 0, st, P); break;
+    }
+  }
   if (P.lean_split == 2) return;                                   // no other tile: scan_tiles need not run
   if (!P.truth) {   // > TT_MAX_LEAVES leaves: one generic instantiation interprets the Kleene program per row
     hipLaunchKernelGGL((scan_tiles<AGG, MAXSTR, false, HASH>), grid, block, 0, st, P);

@@ -244,7 +244,7 @@ def test_hbm_budget_lru_eviction():
         s.free()
     probe = Engine(0)
     probe.put_segment("p", blobs[0])
-    one = probe.segment_bytes()
+    one = probe.segment_bytes
     probe.close()
     e = Engine(0, hbm_budget_bytes=int(2.5 * one))
     try:
@@ -253,13 +253,57 @@ def test_hbm_budget_lru_eviction():
         e.put_segment("s1", blobs[1])
         want = e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows()   # s0 becomes the most recent
         e.put_segment("s2", blobs[2])                              # over budget: s1 (LRU) goes
-        assert e.segment_count() == 2 and e.segment_bytes() <= int(2.5 * one)
+        assert e.segment_count == 2 and e.segment_bytes <= int(2.5 * one)
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
         with pytest.raises(Exception):
             e.eval_pushdown(req, ["s1"], 10, LK_MERGED)             # evicted, and not a file path
         e.put_segment("s3", blobs[3])                              # s2 is now the LRU
-        assert e.segment_count() == 2
+        assert e.segment_count == 2
         e.put_segment("s0", blobs[0])
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
     finally:
         e.close()
+
+
+def test_lean_kernel_late_columns(engine):
+    """scan_lean with late string columns (name early; the others decoded per listed row): a group dim only
+    (every listed row passes, loads issued together), a late regex filter + 2 group dims, a high-cardinality late
+    column (lookup values outside LDS), a late column absent from one segment; GPU == oracle, and == scan_tiles
+    (LK_NO_LEAN_SPLIT)."""
+    import os
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    keys, blobs, segs = [], [], []
+    for i in range(5):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 19, null_frac=0.0, highcard_n=5000 if i != 2 else 0,
+                                                  rg_rows=1 << 18, page_rows=1 << 15, value_mode=1))
+        key = f"late/{i}"
+        engine.put_segment_ptr(key, s.ptr, s.size)
+        blobs.append(s.bytes())
+        s.free()
+        keys.append(key)
+        segs.append(synth.segment_request(i))
+    re_f = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"),
+            "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
+    for filt, agg, gbs in [(synth.leaf(synth.NAME, "eq", "metric_07"), "sum", [synth.SERVICE]),
+                           (re_f, "max", [synth.SERVICE, synth.NAMESPACE]),
+                           (synth.leaf(synth.NAME, "in", "metric_01", "metric_09"), "count", [synth.CONTAINER]),
+                           ({"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_03"),
+                             "q2": synth.leaf(synth.CONTAINER, "in", "c0000001", "c0000007", "c0004999")},
+                            "min", [synth.NAMESPACE])]:
+        req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 2, keys, sources=blobs)
+        got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        for gi, (g, cs) in enumerate(zip(got.per_glob(len(cells)), cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"late {gbs} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, f"late {gbs} merged")
+        os.environ["LK_NO_LEAN_SPLIT"] = "1"
+        try:
+            general = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        finally:
+            del os.environ["LK_NO_LEAN_SPLIT"]
+        assert list(general.ts) == list(merged.ts) and general.tags == merged.tags
+        if agg not in ("sum", "avg"):
+            assert np.array_equal(general.values.view(np.uint64), merged.values.view(np.uint64))
