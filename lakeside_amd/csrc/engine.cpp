@@ -254,6 +254,10 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
   uint32_t remap_off = uint32_t(col.remap.size());
   uint32_t dict_n = 0;
   bool have_dict = false;
+  // numeric columns: fixed width of a PLAIN value (BOOLEAN: bit-packed) and the chunk's dictionary, if any (its
+  // pages are materialized to PLAIN at load, so the kernels only ever see PLAIN numeric pages)
+  const size_t width = col.ptype == pq::INT64 || col.ptype == pq::DOUBLE ? 8 : (col.ptype == pq::BOOLEAN ? 0 : 4);
+  std::vector<uint8_t> ndict;
   uint32_t first_row = 0;
   while (seen < m.num_values) {
     if (pos >= B.size) throw PlanError(LK_ERR_IO, "parquet: page walk ran past the file");
@@ -278,8 +282,16 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
         n = out.size();
       }
     }
+    if (h.type == pq::DICTIONARY_PAGE && !col.is_string) {
+      if (width == 0) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: dictionary-encoded BOOLEAN column " + col.name);
+      if (h.dict_num_values < 0 || size_t(h.dict_num_values) * width > n)
+        throw PlanError(LK_ERR_IO, "parquet: truncated dictionary page in " + col.name);
+      ndict.assign(data, data + size_t(h.dict_num_values) * width);
+      dict_n = uint32_t(h.dict_num_values);
+      have_dict = true;
+      continue;
+    }
     if (h.type == pq::DICTIONARY_PAGE) {
-      if (!col.is_string) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: dictionary-encoded non-string column " + col.name);
       GlobalDict& gd = B.E.dict(col.name);
       std::lock_guard<std::mutex> g(gd.mu);
       size_t p = 0;
@@ -405,11 +417,32 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       d.vals = B.put(stream, slen);
       d.vals_len = uint32_t(slen);
     } else {
-      if (st.encoding != pq::PLAIN) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: non-PLAIN numeric page in " + col.name);
-      if (st.vals_len < size_t(nvals) * 8) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN page in " + col.name);
-      d.kind = PAGE_PLAIN64;
-      d.vals = B.put(st.vals, size_t(nvals) * 8);
-      d.vals_len = nvals * 8;
+      if ((st.encoding == pq::RLE_DICTIONARY || st.encoding == pq::PLAIN_DICTIONARY) && width) {
+        // dictionary-encoded numeric page (e.g. a writer's default dictionary for every column): materialized to
+        // PLAIN values here
+        if (!have_dict) throw PlanError(LK_ERR_IO, "parquet: dictionary page missing for " + col.name);
+        if (st.vals_len < 1 && nvals) throw PlanError(LK_ERR_IO, "parquet: empty dictionary-index page");
+        const int bw = st.vals_len ? st.vals[0] : 0;
+        if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
+        std::vector<uint32_t> idx(nvals);
+        pq::hybrid_decode(st.vals_len ? st.vals + 1 : st.vals, st.vals_len ? st.vals_len - 1 : 0, bw, nvals, idx.data());
+        B.plain.emplace_back(size_t(nvals) * width);
+        std::vector<uint8_t>& out = B.plain.back();
+        for (uint32_t i = 0; i < nvals; i++) {
+          if (idx[i] >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
+          memcpy(out.data() + size_t(i) * width, ndict.data() + size_t(idx[i]) * width, width);
+        }
+        st.vals = out.data();
+        st.vals_len = out.size();
+      } else if (st.encoding != pq::PLAIN) {
+        throw PlanError(LK_ERR_UNSUPPORTED, "parquet: numeric page encoding " + std::to_string(st.encoding) + " in " + col.name);
+      }
+      // PLAIN: 8-B (INT64 / DOUBLE) or 4-B (INT32 / FLOAT) values; BOOLEAN bit-packed, LSB first
+      const size_t bytes = width ? size_t(nvals) * width : (size_t(nvals) + 7) / 8;
+      if (st.vals_len < bytes) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN page in " + col.name);
+      d.kind = width == 8 ? PAGE_PLAIN64 : (width == 4 ? PAGE_PLAIN32 : PAGE_BOOL);
+      d.vals = B.put(st.vals, bytes);
+      d.vals_len = uint32_t(bytes);
       hp.host_vals = st.vals;
     }
     B.pages[ci].push_back(std::move(hp));
@@ -544,6 +577,13 @@ Segment::~Segment() {
   if (d_meta) (void)hipFree(d_meta);
 }
 
+// Physical types the engine loads: BYTE_ARRAY strings, INT64 / DOUBLE (the scan's timestamp and value columns), and
+// INT32 / FLOAT / BOOLEAN (read by exemplar rows).  INT96 / FIXED_LEN_BYTE_ARRAY stay unloaded ("absent" for queries).
+static bool loadable_type(const HostCol& c) {
+  return c.is_string || c.ptype == pq::INT64 || c.ptype == pq::DOUBLE || c.ptype == pq::INT32 || c.ptype == pq::FLOAT ||
+         c.ptype == pq::BOOLEAN;
+}
+
 std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uint8_t* F, size_t size) {
   auto S = std::make_shared<Segment>();
   S->key = key;
@@ -554,6 +594,7 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     if (e.num_children > 0 || e.type < 0) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: nested schema");
     if (e.repetition == pq::REPEATED) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: repeated column " + e.name);
     S->all_columns.insert(e.name);
+    S->schema.emplace_back(e.name, e.type);
     HostCol c;
     c.name = e.name;
     c.ptype = e.type;
@@ -574,15 +615,14 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     for (size_t ci = 0; ci < S->cols.size(); ci++) {
       HostCol& col = S->cols[ci];
       // only the physical types the kernels decode are loaded; others stay "absent" for queries
-      bool supported = col.is_string || col.ptype == pq::INT64 || col.ptype == pq::DOUBLE;
-      if (!supported) continue;
+      if (!loadable_type(col)) continue;
       load_column_chunk(B, int(ci), rg, fm.row_groups[rg].columns[ci]);
     }
   }
   // drop columns of unsupported types from the index
   for (size_t ci = 0; ci < S->cols.size(); ci++) {
     HostCol& col = S->cols[ci];
-    if (!(col.is_string || col.ptype == pq::INT64 || col.ptype == pq::DOUBLE)) col.unsupported = true;
+    if (!loadable_type(col)) col.unsupported = true;
   }
   // unsupported columns still need page lists for tile building: give them none and skip in build_tiles
   {

@@ -76,6 +76,7 @@ struct Segment {
   std::vector<int64_t> rg_rows;
   std::vector<HostCol> cols;                     // loadable columns
   std::set<std::string> all_columns;             // every column of the file (DESCRIBE, Commons.scala:214-221)
+  std::vector<std::pair<std::string, int>> schema;   // (name, Parquet physical type) in file order (SELECT *)
   std::unordered_map<std::string, int> by_name;
   std::vector<TileDesc> tiles;
   TileDesc* d_tiles = nullptr;
@@ -254,7 +255,12 @@ struct lk_result {
   }
   std::shared_ptr<void> zeros;                   // glob column of merged rows (see alloc_rows)
 
+  // exemplar rows: every row's tag strings, materialized ([row][tag column]; nullptr: tag absent)
+  bool exemplar = false;
+  std::vector<const char*> ex_tags;
+
   const char* tag(size_t row, size_t col) const {
+    if (exemplar) return ex_tags[row * tag_names.size() + col];
     if (int(col) == count_col) return count_str[row].c_str();
     if (col < tcols.size()) return own_tag(row, col);
     for (size_t c = 0; c < tcols.size(); c++)

@@ -28,6 +28,7 @@
 #include "ddsketch.hpp"
 #include "hll.hpp"
 #include "regex.hpp"
+#include "evalutil.hpp"
 
 namespace lk {
 
@@ -38,14 +39,9 @@ namespace lk {
       throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
   } while (0)
 
+// (the helpers below up to noisy_tag are shared with exemplar.cpp through evalutil.hpp)
+
 namespace {
-
-struct LeafInfo {
-  const FilterNode* node;
-  int str;      // string column index
-  int index;    // global leaf index
-};
-
 struct StrCol {
   std::string name;
   std::vector<const FilterNode*> leaves;
@@ -103,6 +99,7 @@ struct GlobInfo {
   int64_t step = 0;
   std::vector<std::pair<std::string, std::string>> query_tags;   // glob head's queryTags
 };
+}  // namespace
 
 // One leaf on one dictionary value (BaseExpr.scala:470-501).  `re`: the compiled RE2-semantics matcher of a
 // regex / contains leaf; `set`: the value list of a large in / not_in.
@@ -219,8 +216,6 @@ bool noisy_tag(const std::string& t) {
   return t.rfind("rollup_", 0) == 0;
 }
 
-}  // namespace
-
 namespace {
 // Metrics timestamps off the step grid: the scan is re-run at millisecond granularity (see below).
 struct MetricsUnaligned {};
@@ -256,6 +251,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
   if (glob_size <= 0) glob_size = 10;
   if (n_paths != R.segments.size()) throw PlanError(LK_ERR_ARG, "paths must match segmentRequests");
+  // Exemplar query (no chart, not a tag query): raw rows, ORDER BY timestamp LIMIT n (BaseExpr.scala:234-239)
+  if (!R.is_tag_query && !R.has_chart) return evaluate_exemplar(E, *X, R, paths, n_paths, glob_size, flags, dist, res);
 
   // ---- shape gate ----
   // Tag query (isTagQuery with a tagDataType): BaseExpr.generateSql (BaseExpr.scala:127-143) emits
@@ -264,8 +261,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const bool tagq = R.is_tag_query && !R.tag_name.empty();
   if (tagq && R.tag_data_type != "string")
     throw PlanError(LK_ERR_UNSUPPORTED, "tag query over a " + R.tag_data_type + " tag");
-  if (!tagq && (R.is_tag_query || !R.has_chart))
-    throw PlanError(LK_ERR_UNSUPPORTED, "exemplar queries are not on the hot path");
+  if (!tagq && R.is_tag_query)   // isTagQuery without a tagDataType: SELECT * ... WHERE <filter> (BaseExpr.scala:231-232)
+    throw PlanError(LK_ERR_UNSUPPORTED, "tag queries without a tagDataType");
   if (R.field_chart || R.has_extract || R.has_compute)
     throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute / field charts are not on the hot path");
   if (R.dataset != "logs" && R.dataset != "traces" && R.dataset != "metrics")

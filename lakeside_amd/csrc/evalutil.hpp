@@ -1,0 +1,40 @@
+// Plan helpers shared by the aggregate evaluator (eval.cpp) and the exemplar path (exemplar.cpp).
+#pragma once
+#include <chrono>
+#include <cstdint>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "engine.hpp"
+#include "plan.hpp"
+#include "regex.hpp"
+
+namespace lk {
+
+struct LeafInfo {
+  const FilterNode* node;
+  int str;      // string column index
+  int index;    // global leaf index
+};
+
+// One leaf on one dictionary value (BaseExpr.scala:470-501).
+bool leaf_eval(const FilterNode& f, const std::string& s, re::Regex* re, const std::unordered_set<std::string>* set);
+// regexp_matches(label, p, 'i') / contains' '.*p.*' as an RE2-semantics matcher (PlanError on a bad pattern).
+re::Regex compile_leaf_regex(const FilterNode& l);
+// Postfix Kleene program of the filter over numbered leaves.
+void postfix(const FilterNode* n, const std::vector<LeafInfo>& leaves, std::vector<uint8_t>& prog);
+void collect_leaves(const FilterNode* n, std::vector<const FilterNode*>& out);
+// Truth table of a postfix program over L leaves: bit (T | F << L) = TRUE.
+std::vector<uint32_t> truth_table(const std::vector<uint8_t>& prog, uint32_t L);
+bool null_like(const std::string& s);
+double ms_since(std::chrono::steady_clock::time_point t0);
+
+// Exemplar queries (no chart): exemplar.cpp.
+int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
+                      int glob_size, unsigned flags, bool dist, lk_result* res);
+// Java Double.toString / Float.toString text.
+template <class F>
+std::string java_float_text(F d);
+
+}  // namespace lk

@@ -1,0 +1,346 @@
+// Exemplar scans (raw rows, no chart): per glob the worker runs
+//   SELECT <projection>, * FROM (SELECT * FROM {table} WHERE <window>) WHERE <filter>
+//   ORDER BY "_cardinalhq.timestamp" <DESC|ASC> LIMIT <n>
+// (BaseExpr.getBaseQuery, core/src/main/scala/com/cardinal/utils/ast/BaseExpr.scala:234-239).  Top-n by time is a
+// selection problem, solved here without sorting the glob:
+//   ex_scan (HIST): every tile whose zone map meets a glob's open range decodes its filter columns row by row,
+//     evaluates the filter (Kleene truth table / program) and counts passing rows per time bin of that range
+//     (LDS histogram, one device atomic per non-empty bin per tile);
+//   host: per glob, the bins from the ordered end until n rows are covered give a narrower range (refined again
+//     while its candidates exceed the emit capacity);
+//   ex_scan (EMIT): the same decode over the tiles meeting the narrowed ranges; passing rows inside them are
+//     appended as (timestamp, segment | tile | row) records (wave-aggregated atomics);
+//   host: sort the few candidates, keep n per glob;
+//   ex_gather: one thread per (selected row, output column) decodes that row's value of every column of the
+//     glob's union (def-level prefix over the tile's def runs, then PLAIN / bit-packed / dictionary value) -> raw
+//     payload + valid flag; the host formats the tag strings (Commons.toDataPoint, Commons.scala:428-459).
+// HBM traffic is the filter columns of the tiles in the window (HIST) plus the tiles near the ordered end (EMIT);
+// the gather is a few KB.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_common.hpp"
+#include "kernels.hpp"
+#include "layout.hpp"
+
+namespace lk {
+
+namespace {
+
+constexpr int XNC = 1 + MAXSTR;   // column 0 = timestamp, 1.. = string columns (QSeg cols 2..)
+
+struct XHot {
+  const uint8_t* vals;
+  const uint8_t* defs;
+  const uint32_t* remap;
+  const uint32_t* tab;
+  uint32_t vals_len, defs_len, vbase, rip, nruns, ndruns, bw, kind, nulls, present;
+};
+
+__device__ __forceinline__ bool x_interpret(const XParams& X, uint32_t T, uint32_t F) {
+  uint64_t st = 0, sf = 0;
+  for (uint32_t i = 0; i < X.nprog; i++) {
+    const uint8_t op = X.prog[i];
+    if (op < 0x80) {
+      st = (st << 1) | ((T >> op) & 1u);
+      sf = (sf << 1) | ((F >> op) & 1u);
+    } else if (op == OP_NOT) {
+      const uint64_t t1 = st & 1, f1 = sf & 1;
+      st = (st & ~1ull) | f1;
+      sf = (sf & ~1ull) | t1;
+    } else if (op == OP_TRUE) {
+      st = (st << 1) | 1;
+      sf = sf << 1;
+    } else {
+      const uint64_t t2 = st & 1, f2 = sf & 1;
+      st >>= 1;
+      sf >>= 1;
+      const uint64_t t1 = st & 1, f1 = sf & 1;
+      st = (st & ~1ull) | ((op == OP_AND) ? (t1 & t2) : (t1 | t2));
+      sf = (sf & ~1ull) | ((op == OP_AND) ? (f1 | f2) : (f1 & f2));
+    }
+  }
+  return st & 1;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
+  return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
+  __shared__ XHot H[XNC];
+  __shared__ LRun vr[XNC][RUN_CAP];
+  __shared__ LRun dr[XNC][RUN_CAP];
+  __shared__ uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
+  __shared__ uint32_t wsum[XNC][BLOCK / 64];
+  __shared__ uint32_t hist[XBINS];
+
+  const QSeg* Sp = X.segs + blockIdx.y;
+  const uint32_t t = blockIdx.x;
+  if (t >= Sp->ntiles) return;
+  const uint32_t g = Sp->glob_slot;
+  const int64_t lo = X.rlo[g], hi = X.rhi[g];
+  const TileDesc* tdp = Sp->tiles + t;
+  if (lo >= hi || tdp->ts_max < lo || tdp->ts_min >= hi) return;   // zone map outside the glob's open range
+  const uint32_t nrows = tdp->nrows;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nc = 1 + int(X.nstr);
+
+  if (tid < nc) {
+    const int qc = tid == 0 ? 0 : tid + 1;
+    XHot h{};
+    h.present = Sp->cols[qc].present;
+    if (h.present) {
+      const TileCol tc = Sp->cols[qc].tcols[t];
+      h.vals = Sp->base + tc.vals;
+      h.defs = Sp->base + tc.defs;
+      h.remap = Sp->cols[qc].remap + tc.remap;
+      h.tab = tid ? X.strp[tid - 1].strtab : nullptr;
+      h.vals_len = tc.vals_len;
+      h.defs_len = tc.defs_len;
+      h.vbase = tc.vbase;
+      h.rip = tc.row_in_page;
+      h.nruns = tc.kind == PAGE_DICT ? tc.nruns : 0u;
+      h.ndruns = tc.has_nulls ? tc.ndruns : 0u;
+      h.bw = tc.bw;
+      h.kind = tc.kind;
+      h.nulls = tc.has_nulls;
+    }
+    H[tid] = h;
+  }
+  if (X.truth)
+    for (uint32_t i = tid; i < ((1u << (2 * X.nleaves)) + 31) / 32; i += BLOCK) truth[i] = X.truth[i];
+  if (X.mode == XMODE_HIST)
+    for (uint32_t i = tid; i < X.nbins; i += BLOCK) hist[i] = 0;
+  __syncthreads();
+  for (int k = 0; k < nc; k++) {
+    if (!H[k].present) continue;
+    const int qc = k == 0 ? 0 : k + 1;
+    const TileCol* tc = Sp->cols[qc].tcols + t;
+    const RunDesc* runs = Sp->cols[qc].runs;
+    for (uint32_t i = tid; i < H[k].nruns; i += BLOCK) {
+      const RunDesc r = runs[tc->run_lo + i];
+      vr[k][i] = LRun{r.start, r.off_lit, r.value};
+    }
+    for (uint32_t i = tid; i < H[k].ndruns; i += BLOCK) {
+      const RunDesc r = runs[tc->drun_lo + i];
+      dr[k][i] = LRun{r.start, r.off_lit, r.value};
+    }
+  }
+  __syncthreads();
+
+  const uint32_t leaf_false = Sp->leaf_false;
+  const int64_t hbase = X.mode == XMODE_HIST ? X.hbase[g] : 0;
+  const int64_t hwidth = X.mode == XMODE_HIST ? X.hwidth[g] : 1;
+  uint32_t carry[XNC];
+#pragma unroll
+  for (int k = 0; k < XNC; k++) carry[k] = 0;
+
+  for (uint32_t c0 = 0; c0 < nrows; c0 += BLOCK) {
+    const uint32_t r = c0 + uint32_t(tid);
+    const bool inb = r < nrows;
+    uint32_t T = 0, F = 0;
+    bool ts_ok = false;
+    int64_t ts = 0;
+#pragma unroll
+    for (int k = 0; k < XNC; k++) {
+      if (k >= nc) break;
+      const XHot& h = H[k];
+      bool ok = inb && h.present;
+      uint32_t vi = h.vbase + r;
+      if (h.present && h.nulls) {   // block-uniform
+        const __amdgpu_buffer_rsrc_t drs = make_rsrc(h.defs, h.defs_len + 8);
+        const uint32_t row = h.rip + r;
+        const int ri = find_run(dr[k], int(h.ndruns), row);
+        const bool bit = inb && (hybrid_get_buf(drs, dr[k][ri], row, 1) & 1u);
+        const unsigned long long m = __ballot(bit);
+        const uint32_t below = lanes_below(m);
+        if (lane == 0) wsum[k][wave] = uint32_t(__popcll(m));
+        __syncthreads();
+        uint32_t before = 0, all = 0;
+#pragma unroll
+        for (int w = 0; w < BLOCK / 64; w++) {
+          before += w < wave ? wsum[k][w] : 0u;
+          all += wsum[k][w];
+        }
+        __syncthreads();
+        vi = h.vbase + carry[k] + before + below;
+        carry[k] += all;
+        ok = bit;
+      }
+      if (k == 0) {
+        if (h.kind != PAGE_PLAIN64) ok = false;
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len);
+        const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? vi * 8u : OOB, 0, 0);
+        ts = int64_t((uint64_t(w.y) << 32) | w.x);
+        ts_ok = ok;
+        continue;
+      }
+      const StrParam& sp = X.strp[k - 1];
+      if (!h.present || h.nruns == 0u) ok = false;   // absent / no value in this tile: NULL
+      if (ok) {
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len + 8);
+        const int ri = find_run(vr[k], int(h.nruns), vi);
+        const uint32_t idx = hybrid_get_buf(rs, vr[k][ri], vi, int(h.bw));
+        const uint32_t gid = h.remap[idx];
+        const uint32_t packed = h.tab ? h.tab[gid] : 0u;
+        const uint32_t bits = (packed >> 24) << sp.lbase;
+        T |= bits & sp.lmask;
+        F |= ~bits & sp.lmask;
+      } else {
+        F |= sp.hmask;   // IS NOT NULL on NULL: FALSE; other leaves NULL
+      }
+    }
+    T &= ~leaf_false;
+    F |= leaf_false;
+    bool pass;
+    if (X.truth) {
+      const uint32_t ix = T | (F << X.nleaves);
+      pass = (truth[ix >> 5] >> (ix & 31)) & 1u;
+    } else {
+      pass = x_interpret(X, T, F);
+    }
+    pass = pass && ts_ok && ts >= lo && ts < hi;
+    if (X.mode == XMODE_HIST) {
+      if (pass) {
+        int64_t b = (ts - hbase) / hwidth;
+        b = b < 0 ? 0 : (b >= int64_t(X.nbins) ? int64_t(X.nbins) - 1 : b);
+        atomicAdd(&hist[b], 1u);
+      }
+    } else {
+      const unsigned long long m = __ballot(pass);
+      if (m) {
+        uint32_t base = 0;
+        if (lane == 0) base = atomicAdd(X.out_n, uint32_t(__popcll(m)));
+        base = __shfl(base, 0) + lanes_below(m);
+        if (pass && base < X.cap) {
+          X.out[2 * size_t(base)] = (unsigned long long)ts;
+          X.out[2 * size_t(base) + 1] = ((unsigned long long)blockIdx.y << 48) | ((unsigned long long)t << 16) | r;
+        }
+      }
+    }
+  }
+  if (X.mode == XMODE_HIST) {
+    __syncthreads();
+    for (uint32_t i = tid; i < X.nbins; i += BLOCK)
+      if (hist[i]) atomicAdd(&X.hist[size_t(g) * X.nbins + i], hist[i]);
+  }
+}
+
+namespace {
+
+// Bits [a, b) of a little-endian bit stream: how many are set.
+__device__ uint32_t popcount_range(const uint8_t* p, uint32_t a, uint32_t b) {
+  uint32_t n = 0;
+  while (a < b && (a & 7u)) {
+    n += (p[a >> 3] >> (a & 7u)) & 1u;
+    a++;
+  }
+  while (a + 8 <= b) {
+    n += __popc(p[a >> 3]);
+    a += 8;
+  }
+  while (a < b) {
+    n += (p[a >> 3] >> (a & 7u)) & 1u;
+    a++;
+  }
+  return n;
+}
+
+// `bw` bits at bit offset `bit` of a little-endian bit-packed stream of `len` bytes.
+__device__ uint32_t packed_get(const uint8_t* p, uint32_t len, uint64_t bit, uint32_t bw) {
+  uint64_t x = 0;
+  const uint64_t byte = bit >> 3;
+  for (uint32_t i = 0; i < 5; i++)
+    if (byte + i < len) x |= uint64_t(p[byte + i]) << (8 * i);
+  x >>= (bit & 7u);
+  return bw >= 32 ? uint32_t(x) : uint32_t(x) & ((1u << bw) - 1u);
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(256) void ex_gather(GParams G) {
+  const uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= uint64_t(G.nsel) * G.ncols) return;
+  const uint32_t j = uint32_t(i / G.ncols), k = uint32_t(i % G.ncols);
+  const unsigned long long ref = G.sel[j];
+  const uint32_t seg = uint32_t(ref >> 48), tile = uint32_t((ref >> 16) & 0xffffffffu), r = uint32_t(ref & 0xffffu);
+  const GCol& C = G.cols[size_t(seg) * G.ncols + k];
+  G.ok[i] = 0;
+  G.val[i] = 0;
+  if (!C.present) return;
+  const TileCol tc = C.tcols[tile];
+  const uint32_t row = tc.row_in_page + r;   // page-relative
+  uint32_t vi = tc.vbase + r;
+  if (tc.has_nulls) {
+    const uint8_t* defs = C.base + tc.defs;
+    uint32_t cnt = 0;
+    bool bit = false;
+    for (uint32_t q = 0; q < tc.ndruns; q++) {
+      const RunDesc rd = C.runs[tc.drun_lo + q];
+      const uint32_t s = rd.start, e = rd.start + rd.count;
+      const uint32_t a = s > tc.row_in_page ? s : tc.row_in_page, b = e < row ? e : row;
+      const bool lit = (rd.off_lit & 0x80000000u) != 0;
+      const uint32_t off = rd.off_lit & 0x7fffffffu;
+      if (a < b) cnt += lit ? popcount_range(defs + off, a - s, b - s) : (rd.value ? b - a : 0u);
+      if (row >= s && row < e) bit = lit ? ((defs[off + ((row - s) >> 3)] >> ((row - s) & 7u)) & 1u) : rd.value != 0;
+    }
+    if (!bit) return;
+    vi = tc.vbase + cnt;
+  }
+  const uint8_t* vals = C.base + tc.vals;
+  unsigned long long v = 0;
+  switch (tc.kind) {
+    case PAGE_PLAIN64:
+      if (uint64_t(vi) * 8 + 8 > tc.vals_len) return;
+      for (int b = 0; b < 8; b++) v |= (unsigned long long)vals[size_t(vi) * 8 + b] << (8 * b);
+      break;
+    case PAGE_PLAIN32:
+      if (uint64_t(vi) * 4 + 4 > tc.vals_len) return;
+      for (int b = 0; b < 4; b++) v |= (unsigned long long)vals[size_t(vi) * 4 + b] << (8 * b);
+      break;
+    case PAGE_BOOL:
+      if ((vi >> 3) >= tc.vals_len) return;
+      v = (vals[vi >> 3] >> (vi & 7u)) & 1u;
+      break;
+    case PAGE_DICT: {
+      if (tc.nruns == 0) return;
+      uint32_t a = tc.run_lo, b = tc.run_lo + tc.nruns - 1;   // last run whose start <= vi
+      while (a < b) {
+        const uint32_t m = (a + b + 1) / 2;
+        if (C.runs[m].start <= vi) a = m;
+        else b = m - 1;
+      }
+      const RunDesc rd = C.runs[a];
+      const uint32_t idx = (rd.off_lit & 0x80000000u)
+                               ? packed_get(vals + (rd.off_lit & 0x7fffffffu), tc.vals_len - (rd.off_lit & 0x7fffffffu),
+                                            uint64_t(vi - rd.start) * tc.bw, tc.bw)
+                               : rd.value;
+      if (idx >= tc.dict_n) return;
+      v = C.remap[tc.remap + idx];
+      break;
+    }
+    default:
+      return;
+  }
+  G.val[i] = v;
+  G.ok[i] = 1;
+}
+
+hipError_t launch_ex_scan(const XParams& X, hipStream_t stream) {
+  if (!X.nsegs || !X.max_tiles) return hipSuccess;
+  hipLaunchKernelGGL(ex_scan, dim3(X.max_tiles, X.nsegs), dim3(BLOCK), 0, stream, X);
+  return hipGetLastError();
+}
+
+hipError_t launch_ex_gather(const GParams& G, hipStream_t stream) {
+  const uint64_t n = uint64_t(G.nsel) * G.ncols;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(ex_gather, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, stream, G);
+  return hipGetLastError();
+}
+
+}  // namespace lk

@@ -1,0 +1,677 @@
+// Exemplar queries: a PushDownRequest whose baseExpr has no chart (and no tag query) -- raw rows.
+//
+// Reference (per glob of `glob_size` segments, Commons.scala:361-389):
+//   SELECT "_cardinalhq.timestamp", "_cardinalhq.value", "_cardinalhq.name", "_cardinalhq.message", *     (logs)
+//          "_cardinalhq.timestamp", "_cardinalhq.value", "span.name", "span.kind", *                      (traces)
+//   FROM (SELECT * FROM read_parquet([...], union_by_name=True) WHERE <window>) WHERE <filter>
+//   ORDER BY "_cardinalhq.timestamp" <order, default DESC> LIMIT <limit, default 1000>
+// (BaseExpr.getBaseQuery, BaseExpr.scala:206-239; projections 41-45; defaults ASTUtils.scala:360-361).
+// Each row becomes DataPoint(timestamp = col 1, value = getDouble(col 2), tags = every later column whose value is
+// non-NULL, not "null" and not empty, keyed by column name, values as JDBC getString text) (Commons.toDataPoint,
+// Commons.scala:428-459); PushDownAggregatorStage passes exemplar rows through (PushDownAggregatorStage.scala:42,
+// 66-68); the globs' streams are folded with Akka mergeSorted under pushDownResponseOrdering (timestamp, reversed
+// when reverseSort; Commons.scala:116-132, 391-392).
+//
+// Here: ex_scan HIST passes narrow each glob's window to the rows that can be in its top `limit`, one ex_scan EMIT
+// pass lists them, the host sorts those few candidates, and ex_gather decodes every column of the selected rows
+// (ex_kernels.hip).  Documented choices where the reference is unspecified: rows tied on the timestamp keep file
+// order (segment position in the glob, then row), which DuckDB's ORDER BY leaves open; metrics exemplars (value =
+// getDouble of the name column) fail like the reference's stream does (-> empty).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <charconv>
+#include <chrono>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <unordered_set>
+#include <vector>
+
+#include "../../include/lakeside_gpu.h"
+#include "engine.hpp"
+#include "evalutil.hpp"
+#include "kernels.hpp"
+#include "layout.hpp"
+#include "parquet.hpp"
+
+namespace lk {
+
+#define XHIP_TRY(x)                                                                             \
+  do {                                                                                          \
+    hipError_t _e = (x);                                                                        \
+    if (_e != hipSuccess)                                                                       \
+      throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+// Java Double.toString / Float.toString text (what DuckDB's JDBC getString returns for DOUBLE / FLOAT): the shortest
+// round-trip digits, laid out plain for 1e-3 <= |x| < 1e7 ("100.0", "0.001") and as d.dddE<exp> otherwise
+// ("1.0E7", "1.5E-4").  (JDK >= 19 prints the shortest digits; JDK 17's FloatingDecimal differs in rare cases.)
+template <class F>
+std::string java_float_text(F d) {
+  if (std::isnan(d)) return "NaN";
+  if (std::isinf(d)) return d > 0 ? "Infinity" : "-Infinity";
+  if (d == F(0)) return std::signbit(d) ? "-0.0" : "0.0";
+  char buf[64];
+  const auto r = std::to_chars(buf, buf + sizeof buf, d, std::chars_format::scientific);
+  std::string sci(buf, r.ptr);
+  const bool neg = sci[0] == '-';
+  if (neg) sci.erase(0, 1);
+  const size_t e = sci.find('e');
+  int exp = std::stoi(sci.substr(e + 1));
+  std::string digits;
+  for (size_t i = 0; i < e; i++)
+    if (sci[i] != '.') digits += sci[i];
+  if (digits.size() == 1) {
+    // Java prints at least two significant digits: the 2-digit decimal closest to the exact value (4.9E-324)
+    const auto r2 = std::to_chars(buf, buf + sizeof buf, std::fabs(d), std::chars_format::scientific, 1);
+    const std::string s2(buf, r2.ptr);
+    const size_t e2 = s2.find('e');
+    exp = std::stoi(s2.substr(e2 + 1));
+    digits = std::string(1, s2[0]) + s2[2];
+    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
+  }
+  std::string out = neg ? "-" : "";
+  const double a = std::fabs(double(d));
+  if (a >= 1e-3 && a < 1e7) {
+    if (exp >= 0) {
+      std::string ip = digits.substr(0, std::min(digits.size(), size_t(exp) + 1));
+      while (ip.size() < size_t(exp) + 1) ip += '0';
+      std::string fp = digits.size() > size_t(exp) + 1 ? digits.substr(size_t(exp) + 1) : "0";
+      out += ip + "." + fp;
+    } else {
+      out += "0." + std::string(size_t(-exp - 1), '0') + digits;
+    }
+  } else {
+    out += digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(exp);
+  }
+  return out;
+}
+template std::string java_float_text<double>(double);
+template std::string java_float_text<float>(float);
+
+namespace {
+
+const char* const kMessage = "_cardinalhq.message";   // Commons.scala:59
+const char* const kSpanName = "span.name";            // Commons.scala:71
+const char* const kSpanKind = "span.kind";            // Commons.scala:72
+
+// union_by_name type of a column over a glob's files (DuckDB's common supertype for the physical types a segment
+// writer produces): equal types stay; INT32/INT64 -> BIGINT; integers with FLOAT -> FLOAT; with DOUBLE -> DOUBLE.
+// Anything else (strings mixed with numbers, BOOLEAN with numbers, INT96 / FIXED_LEN) is not decoded here.
+int union_type(int a, int b) {
+  if (a < 0) return b;
+  if (a == b) return a;
+  auto rank = [](int t) {
+    switch (t) {
+      case pq::INT32: return 1;
+      case pq::INT64: return 2;
+      case pq::FLOAT: return 3;
+      case pq::DOUBLE: return 4;
+      default: return 0;
+    }
+  };
+  const int ra = rank(a), rb = rank(b);
+  if (!ra || !rb) throw PlanError(LK_ERR_UNSUPPORTED, "union_by_name over incompatible column types");
+  if ((ra <= 2 && rb <= 2)) return pq::INT64;
+  if (ra == 4 || rb == 4) return pq::DOUBLE;
+  return pq::FLOAT;
+}
+
+// JDBC getString text of a raw value of physical type `pt` read as union type `ut`.
+std::string value_text(unsigned long long raw, int pt, int ut) {
+  int64_t iv = 0;
+  double dv = 0.0;
+  float fv = 0.0f;
+  switch (pt) {
+    case pq::INT64: iv = int64_t(raw); dv = double(iv); fv = float(iv); break;
+    case pq::INT32: iv = int32_t(uint32_t(raw)); dv = double(iv); fv = float(iv); break;
+    case pq::DOUBLE: memcpy(&dv, &raw, 8); break;
+    case pq::FLOAT: {
+      const uint32_t u = uint32_t(raw);
+      memcpy(&fv, &u, 4);
+      dv = double(fv);
+      break;
+    }
+    case pq::BOOLEAN: return raw ? "true" : "false";
+    default: throw PlanError(LK_ERR_UNSUPPORTED, "exemplar column of an undecoded type");
+  }
+  switch (ut) {
+    case pq::INT64:
+    case pq::INT32: return std::to_string(iv);
+    case pq::FLOAT: return java_float_text(fv);
+    default: return java_float_text(dv);
+  }
+}
+
+double value_double(unsigned long long raw, int pt) {
+  switch (pt) {
+    case pq::DOUBLE: {
+      double d;
+      memcpy(&d, &raw, 8);
+      return d;
+    }
+    case pq::INT64: return double(int64_t(raw));
+    case pq::INT32: return double(int32_t(uint32_t(raw)));
+    case pq::FLOAT: {
+      float f;
+      const uint32_t u = uint32_t(raw);
+      memcpy(&f, &u, 4);
+      return double(f);
+    }
+    default: throw PlanError(LK_ERR_UNSUPPORTED, "exemplar value column of a non-numeric type");
+  }
+}
+
+struct XGlob {
+  std::vector<int> segs;
+  bool skip = false;
+  uint32_t leaf_false = 0;
+  int64_t win_lo = 0, win_hi = 0;
+  std::vector<std::string> cols;          // output columns: projection, then the union (file order)
+  std::map<std::string, int> types;       // union type per column
+  // selection state
+  bool open = false;
+  int64_t hlo = 0, hhi = 0;               // range still being narrowed
+  uint64_t need = 0, above = 0;           // rows still wanted from [hlo, hhi); rows certainly in beyond it
+  int64_t elo = 0, ehi = 0;               // final emit range
+  uint64_t count = 0;                     // rows in the emit range
+};
+
+struct Cand {
+  int64_t ts;
+  uint32_t qseg;
+  uint32_t pos;       // segment position in the glob
+  uint64_t row;       // row in the file
+  unsigned long long ref;
+};
+
+}  // namespace
+
+int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
+                      int glob_size, unsigned flags, bool dist, lk_result* res) {
+  const auto t_start = std::chrono::steady_clock::now();
+  if (dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed exemplar queries (each worker streams its own rows)");
+  if (R.has_extract || R.has_compute)
+    throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute exemplar queries are not on the hot path");
+  const bool logs = R.dataset == "logs";
+  if (!logs && R.dataset != "traces") {
+    // metrics: the projection's second column is "_cardinalhq.name" (BaseExpr.scala:41); getDouble of a metric
+    // name fails the stream, which query-api turns into an empty source (QueryEngineV2.scala:141-145)
+    if (R.dataset == "metrics") throw PlanError(LK_ERR_ARG, "metrics exemplar: getDouble of \"_cardinalhq.name\"");
+    throw PlanError(LK_ERR_ARG, "Invalid dataset: " + R.dataset);
+  }
+  std::string order = R.order;
+  for (auto& c : order) c = char(toupper(static_cast<unsigned char>(c)));
+  if (order != "DESC" && order != "ASC") throw PlanError(LK_ERR_ARG, "ORDER BY direction '" + R.order + "'");
+  if (R.limit < 0) throw PlanError(LK_ERR_ARG, "negative LIMIT");
+  const bool desc = order == "DESC";
+  const uint64_t limit = uint64_t(R.limit);
+  const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
+
+  std::vector<const FilterNode*> all_leaves;
+  collect_leaves(R.filter.get(), all_leaves);
+  for (auto* l : all_leaves) {
+    if (l->extracted || l->computed) throw PlanError(LK_ERR_UNSUPPORTED, "extracted/computed filter fields");
+    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
+    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; })) {
+      if (l->op == "gt" || l->op == "ge" || l->op == "lt" || l->op == "le")
+        throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves are not on the hot path yet");
+      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
+    }
+  }
+  res->exemplar = true;
+  res->per_glob = true;
+  if (R.segments.empty()) {   // Commons.scala:393-396: the sentinel DataPoint(-1, -1, {})
+    if (per_glob_rows) {
+      res->alloc_rows(1);
+      res->ts[0] = -1;
+      res->val[0] = -1.0;
+      res->glob[0] = 0;
+      res->gid[0] = 0;
+    }
+    res->stats = "{\"scan_ms\":0,\"total_ms\":0,\"rows_scanned\":0,\"candidates\":0}";
+    return LK_OK;
+  }
+
+  // ---- filter columns (string dictionaries) and the Kleene program ----
+  struct XStr {
+    std::string name;
+    std::vector<const FilterNode*> leaves;
+    uint32_t lbase = 0, lmask = 0, hmask = 0, dict_n = 0;
+  };
+  std::vector<XStr> strs;
+  for (auto* l : all_leaves) {
+    auto it = std::find_if(strs.begin(), strs.end(), [&](const XStr& s) { return s.name == l->k; });
+    if (it == strs.end()) {
+      strs.push_back(XStr{});
+      strs.back().name = l->k;
+      it = strs.end() - 1;
+    }
+    it->leaves.push_back(l);
+  }
+  if (strs.size() > size_t(MAXSTR)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter columns in one query");
+  if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
+  std::vector<LeafInfo> leaves;
+  for (size_t s = 0; s < strs.size(); s++) {
+    XStr& sc = strs[s];
+    if (sc.leaves.size() > size_t(LEAF_BITS)) throw PlanError(LK_ERR_UNSUPPORTED, "too many leaves on one column");
+    sc.lbase = uint32_t(leaves.size());
+    for (const FilterNode* l : sc.leaves) {
+      const uint32_t idx = uint32_t(leaves.size());
+      leaves.push_back(LeafInfo{l, int(s), int(idx)});
+      sc.lmask |= 1u << idx;
+      if (l->op == "has" || l->op == "exists") sc.hmask |= 1u << idx;
+    }
+  }
+  std::vector<uint8_t> prog;
+  postfix(R.filter.get(), leaves, prog);
+  if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
+
+  // ---- segments and globs ----
+  std::vector<std::shared_ptr<Segment>> segs(n_paths);
+  for (size_t i = 0; i < n_paths; i++) segs[i] = E.get_segment(paths[i], true);
+  if (glob_size <= 0) glob_size = 10;
+  const std::vector<std::string> proj = logs ? std::vector<std::string>{kTimestamp, kValue, kName, kMessage}
+                                             : std::vector<std::string>{kTimestamp, kValue, kSpanName, kSpanKind};
+  const std::set<std::string> fset = field_set(R);
+  std::vector<XGlob> globs;
+  for (size_t i = 0; i < n_paths; i += size_t(glob_size)) {
+    XGlob g;
+    for (size_t j = i; j < std::min(n_paths, i + size_t(glob_size)); j++) g.segs.push_back(int(j));
+    g.win_lo = INT64_MAX;
+    g.win_hi = INT64_MIN;
+    std::vector<std::string> uni;
+    for (int si : g.segs) {
+      g.win_lo = std::min(g.win_lo, R.segments[si].start_ts);
+      g.win_hi = std::max(g.win_hi, R.segments[si].end_ts);
+      for (auto& [name, pt] : segs[si]->schema) {
+        if (!g.types.count(name)) uni.push_back(name);
+        g.types[name] = union_type(g.types.count(name) ? g.types[name] : -1, pt);
+      }
+    }
+    for (auto& l : leaves)   // nonExistentFields -> literal false (Commons.scala:224, BaseExpr.scala:462-464)
+      if (fset.count(l.node->k) && !g.types.count(l.node->k)) g.leaf_false |= 1u << l.index;
+    for (auto& p : proj)      // Binder Error -> empty glob (Commons.scala:249-253)
+      if (!g.types.count(p)) g.skip = true;
+    for (auto& l : leaves)
+      if (!(g.leaf_false >> l.index & 1u) && !g.types.count(l.node->k)) g.skip = true;
+    g.cols = proj;
+    for (auto& u : uni)
+      if (std::find(g.cols.begin(), g.cols.end(), u) == g.cols.end()) g.cols.push_back(u);
+    globs.push_back(std::move(g));
+  }
+
+  // ---- per filter column: dictionary value -> leaf bits (cached per (column, leaves) like the aggregate path) ----
+  std::vector<std::vector<uint32_t>> tabs(strs.size());
+  for (size_t s = 0; s < strs.size(); s++) {
+    XStr& sc = strs[s];
+    GlobalDict& gd = E.dict(sc.name);
+    std::lock_guard<std::mutex> dg(gd.mu);
+    sc.dict_n = uint32_t(gd.vals.size());
+    std::string key = sc.name;
+    for (const FilterNode* l : sc.leaves) {
+      key += '\x1f';
+      key += l->op;
+      for (auto& v : l->v) {
+        key += '\x1e';
+        key += v;
+      }
+    }
+    std::vector<std::unique_ptr<re::Regex>> rxs(sc.leaves.size());
+    std::vector<std::unique_ptr<std::unordered_set<std::string>>> sets(sc.leaves.size());
+    for (size_t j = 0; j < sc.leaves.size(); j++) {
+      const FilterNode* l = sc.leaves[j];
+      if (l->op == "regex" || l->op == "contains") rxs[j] = std::make_unique<re::Regex>(compile_leaf_regex(*l));
+      if ((l->op == "in" || l->op == "not_in") && l->v.size() > 8)
+        sets[j] = std::make_unique<std::unordered_set<std::string>>(l->v.begin(), l->v.end());
+    }
+    auto lb = E.leaf_bits(key);
+    std::lock_guard<std::mutex> lg(lb->mu);
+    for (uint32_t gid = uint32_t(lb->hit.size()); gid < sc.dict_n; gid++) {
+      uint8_t bits = 0;
+      for (size_t j = 0; j < sc.leaves.size(); j++)
+        if (leaf_eval(*sc.leaves[j], gd.vals[gid], rxs[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
+      lb->hit.push_back(bits);
+    }
+    tabs[s].resize(std::max<uint32_t>(sc.dict_n, 1));
+    for (uint32_t gid = 0; gid < sc.dict_n; gid++) tabs[s][gid] = uint32_t(lb->hit[gid]) << 24;
+  }
+
+  // ---- per-segment descriptors ----
+  std::vector<QSeg> qsegs;
+  std::vector<const Segment*> qseg_seg;
+  std::vector<uint32_t> qseg_pos, qseg_glob;
+  uint64_t rows_scanned = 0;
+  uint32_t max_tiles = 0;
+  for (size_t gi = 0; gi < globs.size(); gi++) {
+    XGlob& g = globs[gi];
+    if (g.skip || g.win_lo >= g.win_hi || limit == 0) continue;
+    g.open = true;
+    for (size_t p = 0; p < g.segs.size(); p++) {
+      const Segment& S = *segs[g.segs[p]];
+      QSeg q{};
+      q.base = S.d_data;
+      q.tiles = S.d_tiles;
+      q.ntiles = uint32_t(S.tiles.size());
+      q.glob_slot = uint32_t(gi);
+      q.leaf_false = g.leaf_false;
+      q.win_lo = g.win_lo;
+      q.win_hi = g.win_hi;
+      auto bind = [&](int qc, const std::string& name, bool want_string) {
+        const int c = S.col_index(name);
+        if (c < 0) return;
+        const HostCol& hc = S.cols[c];
+        if (want_string != hc.is_string)
+          throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
+        if (qc == 0 && hc.ptype != pq::INT64) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
+      };
+      bind(0, kTimestamp, false);
+      if (!q.cols[0].present) continue;
+      for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      rows_scanned += uint64_t(S.num_rows);
+      max_tiles = std::max(max_tiles, q.ntiles);
+      qsegs.push_back(q);
+      qseg_seg.push_back(&S);
+      qseg_pos.push_back(uint32_t(p));
+      qseg_glob.push_back(uint32_t(gi));
+    }
+  }
+  if (qsegs.size() > 65535) throw PlanError(LK_ERR_UNSUPPORTED, "more than 65535 segments in one evaluation");
+
+  // ---- device staging ----
+  XHIP_TRY(hipSetDevice(E.device));
+  hipStream_t st = X.stream;
+  std::vector<uint32_t> truth;
+  if (leaves.size() <= size_t(TT_MAX_LEAVES)) truth = truth_table(prog, uint32_t(leaves.size()));
+  std::vector<StrParam> strp(strs.size());
+  const size_t ng = globs.size();
+  size_t off = 0;
+  auto reserve = [&](size_t n) { size_t o = (off + 255) / 256 * 256; off = o + n; return o; };
+  const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
+  const size_t o_truth = reserve(truth.size() * 4);
+  std::vector<size_t> o_tab(strs.size());
+  for (size_t s = 0; s < strs.size(); s++) o_tab[s] = reserve(tabs[s].size() * 4);
+  const size_t o_strp = reserve(strp.size() * sizeof(StrParam));
+  const size_t o_rng = reserve(ng * 8 * 4);          // rlo, rhi, hbase, hwidth
+  const size_t o_n = reserve(8);
+  const size_t stage_bytes = off;
+  const size_t o_hist = reserve(ng * XBINS * 4);   // host side only: the histogram read back each pass
+  uint8_t* hbuf = static_cast<uint8_t*>(X.pinned_buf(off));
+  uint8_t* dbuf = static_cast<uint8_t*>(X.workspace("xquery", stage_bytes));
+  uint32_t* d_hist = static_cast<uint32_t*>(X.workspace("xhist", std::max<size_t>(ng * XBINS * 4, 4)));
+  memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
+  if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
+  for (size_t s = 0; s < strs.size(); s++) {
+    memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
+    strp[s].strtab = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
+    strp[s].lbase = strs[s].lbase;
+    strp[s].lmask = strs[s].lmask;
+    strp[s].hmask = strs[s].hmask;
+  }
+  memcpy(hbuf + o_strp, strp.data(), strp.size() * sizeof(StrParam));
+  int64_t* hr = reinterpret_cast<int64_t*>(hbuf + o_rng);
+  XParams P{};
+  P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
+  P.nsegs = uint32_t(qsegs.size());
+  P.max_tiles = max_tiles;
+  P.strp = reinterpret_cast<const StrParam*>(dbuf + o_strp);
+  P.nstr = uint32_t(strs.size());
+  P.nleaves = uint32_t(leaves.size());
+  P.nprog = uint32_t(prog.size());
+  memcpy(P.prog, prog.data(), prog.size());
+  P.truth = truth.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_truth);
+  int64_t* d_rng = reinterpret_cast<int64_t*>(dbuf + o_rng);
+  P.rlo = d_rng;
+  P.rhi = d_rng + ng;
+  P.hbase = d_rng + 2 * ng;
+  P.hwidth = d_rng + 3 * ng;
+  P.out_n = reinterpret_cast<uint32_t*>(dbuf + o_n);
+
+  // ---- HIST passes: narrow every glob to the rows that can make its top `limit` ----
+  // rows listed beyond each glob's `limit` at most, unless tied on one millisecond (tests shrink it with
+  // LK_EX_CAND_CAP to exercise the refinement)
+  const uint64_t kCandCap = getenv("LK_EX_CAND_CAP") ? std::max<uint64_t>(1, strtoull(getenv("LK_EX_CAND_CAP"), nullptr, 10))
+                                                     : (uint64_t(1) << 24);
+  hipEvent_t e0 = X.ev_scan0, e1 = X.ev_scan1;
+  float scan_ms = 0.f;
+  int passes = 0;
+  for (auto& g : globs) {
+    g.hlo = g.win_lo;
+    g.hhi = g.win_hi;
+    g.need = limit;
+    g.elo = g.win_lo;
+    g.ehi = g.win_hi;
+  }
+  bool first_upload = true;
+  while (std::any_of(globs.begin(), globs.end(), [](const XGlob& g) { return g.open; })) {
+    std::vector<uint32_t> nb(ng, 0);
+    for (size_t gi = 0; gi < ng; gi++) {
+      XGlob& g = globs[gi];
+      const int64_t span = g.open ? g.hhi - g.hlo : 0;
+      const int64_t w = span > 0 ? (span + XBINS - 1) / XBINS : 1;
+      hr[gi] = g.open ? g.hlo : 0;
+      hr[ng + gi] = g.open ? g.hhi : 0;
+      hr[2 * ng + gi] = g.hlo;
+      hr[3 * ng + gi] = w;
+      nb[gi] = span > 0 ? uint32_t((span + w - 1) / w) : 0u;
+    }
+    XHIP_TRY(hipMemcpyAsync(first_upload ? dbuf : dbuf + o_rng, first_upload ? hbuf : hbuf + o_rng,
+                            first_upload ? stage_bytes : ng * 32, hipMemcpyHostToDevice, st));
+    first_upload = false;
+    XHIP_TRY(hipMemsetAsync(d_hist, 0, ng * XBINS * 4, st));
+    P.mode = XMODE_HIST;
+    P.nbins = XBINS;
+    P.hist = d_hist;
+    XHIP_TRY(hipEventRecord(e0, st));
+    XHIP_TRY(launch_ex_scan(P, st));
+    XHIP_TRY(hipEventRecord(e1, st));
+    uint32_t* hh = reinterpret_cast<uint32_t*>(hbuf + o_hist);
+    XHIP_TRY(hipMemcpyAsync(hh, d_hist, ng * XBINS * 4, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    XHIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    scan_ms += ms;
+    passes++;
+    for (size_t gi = 0; gi < ng; gi++) {
+      XGlob& g = globs[gi];
+      if (!g.open) continue;
+      const uint32_t* h = hh + gi * XBINS;
+      const int64_t w = hr[3 * ng + gi];
+      uint64_t cum = 0;
+      int64_t split = -1;
+      for (uint32_t k = 0; k < nb[gi]; k++) {
+        const uint32_t b = desc ? nb[gi] - 1 - k : k;
+        if (cum + h[b] >= g.need) {
+          split = int64_t(b);
+          break;
+        }
+        cum += h[b];
+      }
+      if (split < 0) {   // fewer rows than wanted: every row of the range
+        g.count = g.above + cum;
+        if (desc) g.elo = g.hlo;
+        else g.ehi = g.hhi;
+        g.open = false;
+        continue;
+      }
+      const int64_t blo = g.hlo + split * w, bhi = std::min(g.hhi, blo + w);
+      // the split bin is taken whole when the rows it adds beyond the `need` still wanted stay under the cap (or it
+      // is one millisecond wide: those rows are tied and all listed)
+      const uint64_t with_bin = g.above + cum + h[split];
+      if (cum + h[split] - g.need <= kCandCap || w == 1) {
+        g.count = with_bin;
+        if (desc) g.elo = blo;
+        else g.ehi = bhi;
+        g.open = false;
+      } else {
+        g.above += cum;
+        g.need -= cum;
+        g.hlo = blo;
+        g.hhi = bhi;
+      }
+    }
+  }
+
+  // ---- EMIT: the candidates of every glob's final range ----
+  uint64_t total = 0;
+  for (auto& g : globs) total += g.count;
+  if (total > (uint64_t(1) << 28)) throw PlanError(LK_ERR_UNSUPPORTED, "too many exemplar candidates");
+  std::vector<Cand> cands;
+  if (total) {
+    for (size_t gi = 0; gi < ng; gi++) {
+      const XGlob& g = globs[gi];
+      const bool live = g.count > 0;
+      hr[gi] = live ? g.elo : 0;
+      hr[ng + gi] = live ? g.ehi : 0;
+    }
+    unsigned long long* d_out = static_cast<unsigned long long*>(X.workspace("xcand", total * 16));
+    XHIP_TRY(hipMemcpyAsync(dbuf + o_rng, hbuf + o_rng, ng * 16, hipMemcpyHostToDevice, st));
+    XHIP_TRY(hipMemsetAsync(dbuf + o_n, 0, 8, st));
+    P.mode = XMODE_EMIT;
+    P.out = d_out;
+    P.cap = uint32_t(total);
+    XHIP_TRY(hipEventRecord(e0, st));
+    XHIP_TRY(launch_ex_scan(P, st));
+    XHIP_TRY(hipEventRecord(e1, st));
+    std::vector<unsigned long long> h_out(total * 2);
+    uint32_t got = 0;
+    XHIP_TRY(hipMemcpyAsync(h_out.data(), d_out, total * 16, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipMemcpyAsync(&got, dbuf + o_n, 4, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipStreamSynchronize(st));
+    float ms = 0.f;
+    XHIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    scan_ms += ms;
+    if (got != total) throw PlanError(LK_ERR_DEVICE, "internal: exemplar candidate count disagrees with the histogram");
+    cands.resize(total);
+    for (uint64_t i = 0; i < total; i++) {
+      const unsigned long long ref = h_out[2 * i + 1];
+      const uint32_t qs = uint32_t(ref >> 48), tile = uint32_t((ref >> 16) & 0xffffffffu), r = uint32_t(ref & 0xffffu);
+      const Segment& S = *qseg_seg[qs];
+      const TileDesc& td = S.tiles[tile];
+      uint64_t row = uint64_t(td.row0) + r;
+      for (uint32_t k = 0; k < td.rg; k++) row += uint64_t(S.rg_rows[k]);
+      cands[i] = Cand{int64_t(h_out[2 * i]), qs, qseg_pos[qs], row, ref};
+    }
+  }
+
+  // ---- per glob: the top `limit` in ORDER BY order (ties: file order) ----
+  std::vector<std::vector<const Cand*>> per(ng);
+  for (auto& c : cands) per[qseg_glob[c.qseg]].push_back(&c);
+  for (auto& v : per) {
+    std::sort(v.begin(), v.end(), [&](const Cand* a, const Cand* b) {
+      if (a->ts != b->ts) return desc ? a->ts > b->ts : a->ts < b->ts;
+      if (a->pos != b->pos) return a->pos < b->pos;
+      return a->row < b->row;
+    });
+    if (v.size() > limit) v.resize(size_t(limit));
+  }
+  // Akka mergeSorted fold over the globs' streams (Commons.scala:391-392): merge(merge(merge([], g0), g1), g2)...,
+  // each merge emitting the left head when it is strictly less under the ordering, the right head otherwise.
+  const bool rev = R.reverse_sort;   // rollupAgg is empty for exemplars (Commons.scala:125-129)
+  auto less = [&](const Cand* a, const Cand* b) { return rev ? a->ts > b->ts : a->ts < b->ts; };
+  std::vector<const Cand*> stream;
+  for (auto& v : per) {
+    std::vector<const Cand*> m;
+    m.reserve(stream.size() + v.size());
+    size_t i = 0, j = 0;
+    while (i < stream.size() && j < v.size()) {
+      if (less(stream[i], v[j])) m.push_back(stream[i++]);
+      else m.push_back(v[j++]);
+    }
+    while (i < stream.size()) m.push_back(stream[i++]);
+    while (j < v.size()) m.push_back(v[j++]);
+    stream.swap(m);
+  }
+
+  // ---- gather every output column of the selected rows ----
+  std::vector<std::string> out_cols;
+  for (auto& g : globs) {
+    if (g.skip) continue;
+    for (auto& c : g.cols)
+      if (std::find(out_cols.begin(), out_cols.end(), c) == out_cols.end()) out_cols.push_back(c);
+  }
+  const size_t nsel = stream.size(), ncols = out_cols.size();
+  std::vector<unsigned long long> gval(nsel * ncols);
+  std::vector<uint8_t> gok(nsel * ncols);
+  if (nsel && ncols) {
+    std::vector<GCol> gcols(qsegs.size() * ncols);
+    for (size_t q = 0; q < qsegs.size(); q++) {
+      const Segment& S = *qseg_seg[q];
+      for (size_t k = 0; k < ncols; k++) {
+        GCol& gc = gcols[q * ncols + k];
+        const int c = S.col_index(out_cols[k]);
+        if (c < 0) {
+          if (S.all_columns.count(out_cols[k]))
+            throw PlanError(LK_ERR_UNSUPPORTED, "column " + out_cols[k] + " has a physical type the engine does not load");
+          continue;
+        }
+        const HostCol& hc = S.cols[c];
+        gc = GCol{S.d_data, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
+      }
+    }
+    std::vector<unsigned long long> sel(nsel);
+    for (size_t i = 0; i < nsel; i++) sel[i] = stream[i]->ref;
+    const size_t gb = gcols.size() * sizeof(GCol), sb = nsel * 8, vb = nsel * ncols * 8, ob = nsel * ncols;
+    uint8_t* dg = static_cast<uint8_t*>(X.workspace("xgather", gb + sb + vb + ob + 1024));
+    XHIP_TRY(hipMemcpyAsync(dg, gcols.data(), gb, hipMemcpyHostToDevice, st));
+    XHIP_TRY(hipMemcpyAsync(dg + gb, sel.data(), sb, hipMemcpyHostToDevice, st));
+    GParams G{};
+    G.cols = reinterpret_cast<const GCol*>(dg);
+    G.sel = reinterpret_cast<const unsigned long long*>(dg + gb);
+    G.nsel = uint32_t(nsel);
+    G.ncols = uint32_t(ncols);
+    G.val = reinterpret_cast<unsigned long long*>(dg + gb + sb);
+    G.ok = dg + gb + sb + vb;
+    XHIP_TRY(launch_ex_gather(G, st));
+    XHIP_TRY(hipMemcpyAsync(gval.data(), G.val, vb, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipMemcpyAsync(gok.data(), G.ok, ob, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipStreamSynchronize(st));
+  }
+
+  // ---- rows: timestamp, getDouble(value) (SQL NULL -> 0.0), tags as JDBC getString text ----
+  res->alloc_rows(nsel);
+  res->tag_names = out_cols;
+  res->ex_tags.assign(nsel * ncols, nullptr);
+  const size_t vcol = size_t(std::find(out_cols.begin(), out_cols.end(), std::string(kValue)) - out_cols.begin());
+  for (size_t i = 0; i < nsel; i++) {
+    const Cand& c = *stream[i];
+    const XGlob& g = globs[qseg_glob[c.qseg]];
+    const Segment& S = *qseg_seg[c.qseg];
+    res->ts[i] = c.ts;
+    res->glob[i] = qseg_glob[c.qseg];
+    res->gid[i] = i;
+    res->val[i] = 0.0;
+    for (size_t k = 0; k < ncols; k++) {
+      if (!gok[i * ncols + k]) continue;
+      const std::string& name = out_cols[k];
+      const int ci = S.col_index(name);
+      const HostCol& hc = S.cols[ci];
+      const unsigned long long raw = gval[i * ncols + k];
+      const auto ut = g.types.find(name);
+      const int utype = ut == g.types.end() ? hc.ptype : ut->second;
+      if (k == vcol) res->val[i] = value_double(raw, hc.ptype);
+      if (hc.is_string) {
+        if (utype != pq::BYTE_ARRAY) throw PlanError(LK_ERR_UNSUPPORTED, "union_by_name over string and numeric " + name);
+        GlobalDict& gd = E.dict(name);
+        std::lock_guard<std::mutex> dg(gd.mu);
+        const std::string& s = gd.vals[size_t(raw)];
+        if (!null_like(s)) res->ex_tags[i * ncols + k] = s.c_str();   // Commons.scala:433
+      } else {
+        res->owned.push_back(value_text(raw, hc.ptype, utype));
+        res->ex_tags[i * ncols + k] = res->owned.back().c_str();
+      }
+    }
+  }
+  char buf[256];
+  snprintf(buf, sizeof buf,
+           "{\"scan_ms\":%.4f,\"total_ms\":%.4f,\"rows_scanned\":%llu,\"candidates\":%llu,\"hist_passes\":%d}",
+           double(scan_ms), ms_since(t_start), (unsigned long long)rows_scanned, (unsigned long long)total, passes);
+  res->stats = buf;
+  return LK_OK;
+}
+
+}  // namespace lk

@@ -103,6 +103,52 @@ hipError_t launch_sparse_sort(const SParams& S, const uint32_t* d_counts, unsign
 hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws, int64_t* ts, double* val,
                                unsigned long long* gid, uint32_t* glob, hipStream_t stream);
 
+// Exemplar scans (ex_kernels.hip).  ex_scan decodes the filter columns (QSeg cols 0 = timestamp, 2.. = strings) of
+// every tile meeting its glob's open range [rlo, rhi) and either counts passing rows per time bin (HIST) or appends
+// them as (timestamp, segment << 48 | tile << 16 | row) records (EMIT).
+constexpr uint32_t XBINS = 2048;
+enum XMode : uint32_t { XMODE_HIST = 0, XMODE_EMIT = 1 };
+struct XParams {
+  const QSeg* segs;
+  uint32_t nsegs;
+  uint32_t max_tiles;
+  const StrParam* strp;            // [nstr]: strtab = global id -> leaf bits << 24
+  uint32_t nstr;
+  uint32_t nleaves;
+  uint32_t nprog;
+  uint8_t prog[MAXPROG];
+  const uint32_t* truth;           // null: interpret prog
+  const int64_t* rlo;              // per glob slot: the open range
+  const int64_t* rhi;
+  uint32_t mode;
+  uint32_t nbins;                  // HIST: bins per glob (<= XBINS)
+  uint32_t* hist;                  // HIST: [glob][nbins] passing rows
+  const int64_t* hbase;            // HIST: per glob: bin b covers [hbase + b*hwidth, + hwidth)
+  const int64_t* hwidth;
+  unsigned long long* out;         // EMIT: 2 words per record
+  uint32_t* out_n;                 // EMIT: records appended (may exceed cap: only the first cap are written)
+  uint32_t cap;
+};
+hipError_t launch_ex_scan(const XParams& X, hipStream_t stream);
+
+struct GCol {                      // one (segment, output column) of an exemplar gather
+  const uint8_t* base;             // segment streams
+  const RunDesc* runs;
+  const TileCol* tcols;
+  const uint32_t* remap;
+  uint32_t present;
+  uint32_t pad;
+};
+struct GParams {
+  const unsigned long long* sel;   // selected rows: segment << 48 | tile << 16 | row
+  uint32_t nsel;
+  uint32_t ncols;
+  const GCol* cols;                // [segment][ncols]
+  unsigned long long* val;         // [nsel][ncols]: raw value (8/4-B PLAIN, BOOLEAN bit, or string global id)
+  uint8_t* ok;                     // [nsel][ncols]: 1 = non-NULL
+};
+hipError_t launch_ex_gather(const GParams& G, hipStream_t stream);
+
 hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* parts, int world, size_t nc, int agg,
                                hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);

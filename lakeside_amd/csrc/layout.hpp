@@ -25,7 +25,7 @@ constexpr uint32_t DIM_MASK = 0x00ffffffu;   // group-dim id bits of the packed 
 constexpr uint32_t TILE_ROWS = 65536;        // max rows per tile
 constexpr uint32_t RUN_CAP = 128;            // max runs of one stream of one column inside a tile
 
-enum PageKind : uint8_t { PAGE_PLAIN64 = 1, PAGE_DICT = 2 };
+enum PageKind : uint8_t { PAGE_PLAIN64 = 1, PAGE_DICT = 2, PAGE_PLAIN32 = 3, PAGE_BOOL = 4 };   // PLAIN32: INT32 / FLOAT
 
 struct PageDesc {           // 48 B
   uint64_t vals;            // byte offset (from segment base) of the value stream: PLAIN data, or dictionary

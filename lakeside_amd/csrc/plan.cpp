@@ -91,6 +91,10 @@ Request parse_request(const std::string& text) {
   }
   if (const Json* x = be->get("extract"); x && !x->is_null()) r.has_extract = true;
   if (const Json* x = be->get("compute"); x && !x->is_null()) r.has_compute = true;
+  // ASTUtils.scala:360-361: Option(node.get("order")).map(_.textValue), Option(node.get("limit")).map(_.intValue)
+  if (const Json* o = be->get("order"); o && o->is_str()) r.order = o->str;
+  if (const Json* l = be->get("limit"))
+    r.limit = l->kind == Json::Number ? l->as_i64() : 0;   // JSON null: NullNode.intValue = 0
   const Json* f = be->get("filter");
   if (!f || f->is_null()) throw PlanError(LK_ERR_ARG, "No filter provided!");
   r.filter = handle_filter(*f);

@@ -49,6 +49,10 @@ struct Request {
   std::string chart_type = "count";
   std::string rollup;            // empty = none
   bool field_chart = false, has_extract = false, has_compute = false;
+  // exemplar queries (no chart): ORDER BY "_cardinalhq.timestamp" <order> LIMIT <limit> (BaseExpr.scala:234-239;
+  // defaults ASTUtils.scala:360-361)
+  int64_t limit = 1000;
+  std::string order = "DESC";
   bool is_tag_query = false, reverse_sort = false;
   std::string tag_name, tag_data_type = "string";   // PushDownRequest.tagDataType (SegmentRequest.scala:55-58)
   std::vector<SegmentReq> segments;

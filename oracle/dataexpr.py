@@ -79,6 +79,8 @@ class BaseExpr:
     chart: Optional[ChartOptions]
     extract: Any = None
     compute: Any = None
+    limit: int = 1000          # exemplar queries (ASTUtils.scala:360-361)
+    order: str = "DESC"
 
 
 @dataclass
@@ -160,7 +162,9 @@ def to_base_expr(node: dict, id_: Optional[str] = None) -> BaseExpr:
         raise ValueError("No filter provided!")
     return BaseExpr(id=id_ if id_ is not None else node.get("id", "_"),
                     dataset=node.get("dataset", METRICS), filter=handle_filter(node["filter"]),
-                    chart=chart, extract=node.get("extract"), compute=node.get("compute"))
+                    chart=chart, extract=node.get("extract"), compute=node.get("compute"),
+                    limit=(node["limit"] if isinstance(node.get("limit"), int) else 0) if "limit" in node else 1000,
+                    order=node["order"] if isinstance(node.get("order"), str) else "DESC")
 
 
 def parse_pushdown(text: str) -> PushDownRequest:
