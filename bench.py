@@ -209,6 +209,19 @@ def main():
     for sgm in kept.values():
         sgm.free()
 
+    # HBM traffic of the scan kernel(s) per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same bench
+    # command (scripts/gpu_bench_prof.sh -> scripts/pmc_traffic.py; separate runs, as counters must be collected
+    # alone), committed under profiles/ -- read here only when it profiled this query at this size.
+    traffic, traffic_src = None, None
+    pmc_file = os.path.join(ROOT, "profiles", f"r02_pmc_{args.query}.json")
+    if os.path.exists(pmc_file):
+        pmc = json.load(open(pmc_file))
+        if pmc.get("query") == args.query and pmc.get("algorithmic_bytes_per_launch") == alg_bytes:
+            traffic = pmc["hbm_bytes_per_launch"]
+            traffic_src = (f"profiles/r02_pmc_{args.query}.json: rocprofv3 --pmc FETCH_SIZE (x{pmc['fetch_correction']} "
+                           f"gfx950 correction, calibrated in profiles/r02_gather_fetchsize.json) + WRITE_SIZE passes "
+                           f"over this bench command; scan kernel {pmc.get('scan_kernel_ms')} ms in that run")
+
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "rows/s", "n_gpus": world, "steps": args.steps,
@@ -222,14 +235,14 @@ def main():
             "rows_scanned": rows_total, "output_rows": out_rows,
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "definition": "achieved = plan bytes per launch (counted by the scan kernel: streams "
                                        "decoded in full + distinct 128-B lines of every per-row gather + tile "
                                        "metadata) / scan-kernel time (HIP events on the call's stream)",
                          "plan_bytes_per_launch": pbytes,
                          "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_gbs": alg_gbs,
-                         "traffic_note": "PMC HBM bytes come from separate rocprofv3 --pmc passes "
-                                         "(profiles/r02_pmc_*.json); not measurable inside this run",
+                         "traffic_source": traffic_src,
+                         "traffic_gbs": traffic / (scan_avg / 1e3) / 1e9 if traffic else None,
                          "stream_copy_gbs": copy_gbs},
             "validated": validated,
             "cpu_baseline": cpu,

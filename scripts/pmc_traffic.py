@@ -2,7 +2,8 @@
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB per dispatch (median over the run's dispatches). Correction per
 MI355X_MICROARCH.md (HBM section): on gfx950 FETCH_SIZE tallies 128-B requests at 64 B, i.e. half the bytes of
-a wide coalesced read, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for the atomics/stores used here.
+a wide coalesced read, so read bytes = 2 x FETCH_SIZE (calibrated for this kernel's 8-B per-lane gathers too:
+profiles/r02_gather_fetchsize.json, tools/gather_bench.hip); WRITE_SIZE is exact for the atomics/stores used here.
 The dense query (every row passes) is reported beside it as a sanity check: its corrected reads must come close
 to the bytes it actually touches (every value, the name column, and the timestamps of tiles not bucketed by
 the zone map) and stay below its algorithmic bytes.
@@ -14,12 +15,18 @@ FETCH_CORR = 2.0
 
 
 def counter(d, name):
-    vals = []
+    """Per-eval bytes of the scan kernels: the median dispatch of each scan kernel (scan_tiles / scan_lean
+    instantiations; an eval launches each at most once), summed over kernels."""
+    per = {}
     for f in glob.glob(os.path.join(root, d, "**", "*counter_collection.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
-            if "scan_tiles" in row["Kernel_Name"] and row["Counter_Name"] == name:
-                vals.append(float(row["Counter_Value"]) * 1024.0)
-    return vals
+            k = row["Kernel_Name"]
+            if ("scan_tiles" in k or "scan_lean" in k) and row["Counter_Name"] == name:
+                per.setdefault(k, []).append(float(row["Counter_Value"]) * 1024.0)
+    if not per:
+        return []
+    n = min(len(v) for v in per.values())
+    return [sum(statistics.median(v) for v in per.values())] * n
 
 
 def bench_line(name):
@@ -42,6 +49,8 @@ out = {
     "hbm_bytes_per_launch": read + write,
     "algorithmic_bytes_per_launch": q_alg,
     "traffic_over_algorithmic": (read + write) / q_alg,
+    "plan_bytes_per_launch": bench_line("bench_fetch.json")["roofline"].get("plan_bytes_per_launch"),
+    "scan_kernel_ms": bench_line("bench_fetch.json").get("scan_kernel_ms"),
 }
 d_fetch = counter("dense_fetch", "FETCH_SIZE")
 if d_fetch:
