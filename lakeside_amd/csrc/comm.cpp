@@ -54,6 +54,8 @@ struct Comm {
   // untouched), ordered on X.stream
   virtual void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
                               const std::vector<size_t>& off) = 0;
+  // pieces to / from other ranks (comm_exchange)
+  virtual void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) = 0;
 };
 
 namespace {
@@ -103,6 +105,15 @@ struct RcclComm final : Comm {
     }
     NCCL_TRY(ncclGroupEnd());
   }
+
+  void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) override {
+    NCCL_TRY(ncclGroupStart());
+    for (const Piece& p : sends)
+      if (p.peer != rank && p.bytes) NCCL_TRY(ncclSend(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
+    for (const Piece& p : recvs)
+      if (p.peer != rank && p.bytes) NCCL_TRY(ncclRecv(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
+    NCCL_TRY(ncclGroupEnd());
+  }
 };
 
 struct HostComm final : Comm {
@@ -147,6 +158,42 @@ struct HostComm final : Comm {
           HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * mx,
                                   bytes[size_t(r)], hipMemcpyHostToDevice, X.stream));
       HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed on return
+    }
+  }
+
+  void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) override {
+    HIP_TRY2(hipSetDevice(E.device));
+    // one all-gather round per destination d: every rank contributes its pieces for d, concatenated (padded to
+    // the largest contribution); d unpacks each source's bytes into its receive pieces from that source, in order
+    for (int d = 0; d < world; d++) {
+      size_t mine_n = 0;
+      for (const Piece& p : sends)
+        if (p.peer == d && d != rank) mine_n += p.bytes;
+      uint64_t n64 = mine_n;
+      std::vector<uint64_t> sz(static_cast<size_t>(world));
+      allgather(&n64, 8, sz.data());
+      size_t mx = 1;
+      for (uint64_t x : sz) mx = std::max(mx, size_t(x));
+      std::vector<uint8_t> buf(mx, 0), all(d == rank ? size_t(world) * mx : 0);
+      size_t o = 0;
+      for (const Piece& p : sends)
+        if (p.peer == d && d != rank && p.bytes) {
+          HIP_TRY2(hipMemcpyAsync(buf.data() + o, p.ptr, p.bytes, hipMemcpyDeviceToHost, X.stream));
+          o += p.bytes;
+        }
+      HIP_TRY2(hipStreamSynchronize(X.stream));
+      std::vector<uint8_t> sink(d == rank ? 0 : size_t(world) * mx);
+      allgather(buf.data(), mx, d == rank ? all.data() : sink.data());
+      if (d != rank) continue;
+      std::vector<size_t> cur(size_t(world), 0);
+      for (const Piece& p : recvs) {
+        if (p.peer == rank || !p.bytes) continue;
+        size_t& c = cur[size_t(p.peer)];
+        if (c + p.bytes > sz[size_t(p.peer)]) throw PlanError(LK_ERR_DEVICE, "host transport: exchange size mismatch");
+        HIP_TRY2(hipMemcpyAsync(p.ptr, all.data() + size_t(p.peer) * mx + c, p.bytes, hipMemcpyHostToDevice, X.stream));
+        c += p.bytes;
+      }
+      HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed at the end of the round
     }
   }
 };
@@ -200,6 +247,23 @@ void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg) {
     memcpy(&c, b.data(), 4);
     throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(4));
   }
+}
+
+void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) {
+  Comm& C = need_comm(E);
+  HIP_TRY2(hipSetDevice(E.device));
+  // own pieces: device copies, matched in list order
+  std::vector<const Piece*> os, orv;
+  for (const Piece& p : sends)
+    if (p.peer == C.rank) os.push_back(&p);
+  for (const Piece& p : recvs)
+    if (p.peer == C.rank) orv.push_back(&p);
+  if (os.size() != orv.size()) throw PlanError(LK_ERR_DEVICE, "internal: own exchange pieces do not pair up");
+  for (size_t i = 0; i < os.size(); i++) {
+    if (os[i]->bytes != orv[i]->bytes) throw PlanError(LK_ERR_DEVICE, "internal: own exchange piece sizes differ");
+    if (os[i]->bytes) HIP_TRY2(hipMemcpyAsync(orv[i]->ptr, os[i]->ptr, os[i]->bytes, hipMemcpyDeviceToDevice, X.stream));
+  }
+  if (C.world > 1) C.exchange(E, X, sends, recvs);
 }
 
 void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc) {

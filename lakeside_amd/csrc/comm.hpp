@@ -28,4 +28,15 @@ void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t 
 // pointers and `cap` (slots) are replaced by the merged table's.
 void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long long& cap);
 
+// Point-to-point exchange of device buffers (all-to-all / gather building block): `sends` and `recvs` list pieces
+// (peer, device pointer, bytes); the pieces between one pair of ranks are matched in list order.  Pieces with
+// peer == this rank are copied on the device.  RCCL: one grouped ncclSend/ncclRecv set (every peer on its own xGMI
+// link at once).  Host transport: one all-gather round per destination rank.
+struct Piece {
+  int peer;
+  void* ptr;
+  size_t bytes;
+};
+void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs);
+
 }  // namespace lk

@@ -26,6 +26,7 @@
 
 #include "../../include/lakeside_gpu.h"
 #include "engine.hpp"
+#include "hll.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
 #include "codec.hpp"
@@ -141,20 +142,29 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   for (size_t i = 0; i < n; i++) o->perm[i] = uint32_t(i);
   std::sort(o->perm.begin(), o->perm.end(), [&](uint32_t a, uint32_t b) { return *v[a] < *v[b]; });
   o->rank.resize(n);
-  uint64_t h0 = 1469598103934665603ull, h1 = 0x84222325cbf29ce4ull;   // FNV-1a, two bases / primes
-  auto mix = [&](uint8_t b) {
-    h0 = (h0 ^ b) * 1099511628211ull;
-    h1 = (h1 ^ b) * 0x100000001b3ull * 0x9e3779b97f4a7c15ull;
+  // Fingerprint: MurmurHash3_x64_128 over the length-prefixed sorted values, chained over 1 MiB blocks (each block
+  // hashed with the previous digest folded into its seed and into the block's first 16 bytes).  A collision between
+  // two different value sets would merge partial tables under mismatched dim ids; at 128 bits that is not a
+  // practical risk (the former two FNV-1a streams were correlated).
+  uint64_t fp[2] = {uint64_t(n), 0x9e3779b97f4a7c15ull};
+  std::string blk;
+  blk.reserve((1u << 20) + 64);
+  auto flush = [&]() {
+    blk.insert(0, reinterpret_cast<const char*>(fp), 16);
+    hll::murmur3_x64_128(blk.data(), blk.size(), fp[0] ^ (fp[1] << 1), fp);
+    blk.clear();
   };
   for (size_t d = 0; d < n; d++) {
     o->rank[o->perm[d]] = uint32_t(d);
     const std::string& s = *v[o->perm[d]];
     const uint32_t len = uint32_t(s.size());
-    for (int k = 0; k < 4; k++) mix(uint8_t(len >> (8 * k)));
-    for (unsigned char c : s) mix(c);
+    blk.append(reinterpret_cast<const char*>(&len), 4);
+    blk.append(s);
+    if (blk.size() >= (1u << 20)) flush();
   }
-  o->fp[0] = h0;
-  o->fp[1] = h1 ^ uint64_t(n);
+  flush();
+  o->fp[0] = fp[0];
+  o->fp[1] = fp[1];
   slot = o;
   return slot;
 }

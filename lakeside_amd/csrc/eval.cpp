@@ -1032,19 +1032,108 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   if (hflags & FLAG_SKETCH_RANGE) throw PlanError(LK_ERR_ARG, "DDSketch: value outside the trackable range");
 
   // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
+  uint32_t nrows_out = 0;
+  bool rows_done = false;   // key-range path: rank 0's result rows are already in place
+  const char* kr_env = getenv("LK_KEYRANGE_MIN_CELLS");
+  const uint64_t kr_min = kr_env ? uint64_t(atoll(kr_env)) : (uint64_t(1) << 20);
+  const bool keyrange = dist && comm_world(E) > 1 && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
+                        !ces && nslots == 1 && ncells >= kr_min && ncells == nc;
   if (dist) {
     if (hash_mode) {
       unsigned long long cap0 = cap;
       comm_reduce_hash(E, *X, P, kagg, cap0);
       cap = cap0;
       nc = size_t(cap);
+    } else if (keyrange) {
+      // Large dense tables (C5: 10M-key group dims), SURVEY §8(e): the merged output key is the cell index, so the
+      // key space is cut into one contiguous range per rank.  All-to-all: every rank sends range j of its partial
+      // table to rank j (grouped send/recv: all xGMI links at once, 7/8 of a table per rank instead of every table
+      // into rank 0); rank j folds the W slices in rank order (merge_tables: the same deterministic fold) and
+      // finalizes its range; the ranges' rows, already in key order, are concatenated on rank 0 in rank order.
+      const int W = comm_world(E);
+      std::vector<uint64_t> kb(size_t(W) + 1);
+      for (int j = 0; j <= W; j++) kb[size_t(j)] = j == W ? uint64_t(nc) : (uint64_t(nc) * uint64_t(j) / uint64_t(W)) & ~63ull;
+      const size_t len = size_t(kb[size_t(rank) + 1] - kb[size_t(rank)]);
+      uint8_t* tb = reinterpret_cast<uint8_t*>(P.rows);   // [rows | cnt | hi | lo | ext], nc cells each
+      uint8_t* parts = static_cast<uint8_t*>(X->workspace("kr_parts", size_t(W) * 5 * len * 8 + 64));
+      std::vector<Piece> sends, recvs;
+      for (int p2 = 0; p2 < W; p2++)
+        for (int a = 0; a < 5; a++) {
+          const size_t l2 = size_t(kb[size_t(p2) + 1] - kb[size_t(p2)]);
+          sends.push_back(Piece{p2, tb + (size_t(a) * nc + kb[size_t(p2)]) * 8, l2 * 8});
+          recvs.push_back(Piece{p2, parts + (size_t(p2) * 5 + size_t(a)) * len * 8, len * 8});
+        }
+      comm_exchange(E, *X, sends, recvs);
+      TableRef T{reinterpret_cast<unsigned long long*>(parts), reinterpret_cast<unsigned long long*>(parts + len * 8),
+                 reinterpret_cast<double*>(parts + 2 * len * 8), reinterpret_cast<double*>(parts + 3 * len * 8),
+                 reinterpret_cast<unsigned long long*>(parts + 4 * len * 8)};
+      if (len) HIP_TRY(launch_merge_tables(T, reinterpret_cast<const unsigned long long*>(parts), W, len, kagg, st));
+      FParams Fk{};
+      Fk.rows = T.rows;
+      Fk.cnt = T.cnt;
+      Fk.hi = T.hi;
+      Fk.lo = T.lo;
+      Fk.ext = T.ext;
+      Fk.ngroups = ngroups;
+      Fk.nbuckets = nbuckets;
+      Fk.nglob_slots = 1;
+      Fk.agg = agg;
+      Fk.name_stride = strs[0].stride ? strs[0].stride : 1;
+      Fk.bucket_base = bucket_base;
+      Fk.step = P.step;
+      Fk.key_base = kb[size_t(rank)];
+      Fk.cell_base = kb[size_t(rank)];
+      Fk.nkeys = len;
+      const uint32_t nfk = finalize_blocks(len);
+      uint32_t* kc = static_cast<uint32_t*>(X->workspace("kr_counts", (size_t(nfk) + 2) * 4));
+      uint32_t mine_n = 0;
+      if (len) {
+        HIP_TRY(launch_finalize_count(Fk, kc, st));
+        HIP_TRY(hipMemcpyAsync(&mine_n, kc + nfk, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+      }
+      const uint64_t n64 = mine_n;
+      std::vector<uint64_t> ncnt(static_cast<size_t>(W)), noff(static_cast<size_t>(W));
+      uint64_t total_rows = 0;
+      {
+        const std::vector<std::string> all = comm_allgather_bytes(E, *X, std::string(reinterpret_cast<const char*>(&n64), 8));
+        for (int j = 0; j < W; j++) {
+          memcpy(&ncnt[size_t(j)], all[size_t(j)].data(), 8);
+          noff[size_t(j)] = total_rows;
+          total_rows += ncnt[size_t(j)];
+        }
+      }
+      if (total_rows >= (uint64_t(1) << 32)) throw PlanError(LK_ERR_UNSUPPORTED, "more than 2^32 result rows");
+      uint8_t* ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 24 + 64));
+      if (mine_n)
+        HIP_TRY(launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ob), reinterpret_cast<double*>(ob + size_t(mine_n) * 8),
+                                      reinterpret_cast<unsigned long long*>(ob + size_t(mine_n) * 16), nullptr, st));
+      HIP_TRY(hipStreamSynchronize(st));   // rows complete before they are sent
+      uint8_t* rb = rank == 0 ? static_cast<uint8_t*>(X->workspace("kr_rows_all", size_t(total_rows) * 24 + 64)) : nullptr;
+      std::vector<Piece> s2, r2;
+      for (int a = 0; a < 3; a++) s2.push_back(Piece{0, ob + size_t(a) * mine_n * 8, size_t(mine_n) * 8});
+      if (rank == 0)
+        for (int j = 0; j < W; j++)
+          for (int a = 0; a < 3; a++)
+            r2.push_back(Piece{j, rb + (size_t(a) * total_rows + noff[size_t(j)]) * 8, size_t(ncnt[size_t(j)]) * 8});
+      comm_exchange(E, *X, s2, r2);
+      if (rank == 0) {
+        nrows_out = uint32_t(total_rows);
+        res->alloc_rows(nrows_out, false);
+        if (nrows_out) {
+          HIP_TRY(hipMemcpyAsync(res->ts, rb, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+          HIP_TRY(hipMemcpyAsync(res->val, rb + size_t(nrows_out) * 8, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+          HIP_TRY(hipMemcpyAsync(res->gid, rb + size_t(nrows_out) * 16, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+        }
+        HIP_TRY(hipStreamSynchronize(st));
+        rows_done = true;
+      }
     } else {
       comm_reduce_table(E, *X, P, kagg, nc);
     }
   }
-  const bool emit = !dist || rank == 0;
+  const bool emit = (!dist || rank == 0) && !rows_done;
 
-  uint32_t nrows_out = 0;
   FParams F{};
   SParams S{};
   uint32_t nfb = 0;
@@ -1315,7 +1404,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   }
   HIP_TRY(hipStreamSynchronize(st));
   const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
-  res->alloc_rows(nrows_out, per_glob_rows);
+  if (!rows_done) res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
   if (ces) {
     for (size_t r = 0; r < nrows_out; r++) {
@@ -1334,7 +1423,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (per_glob_rows) res->glob[r] = k.glob;
       res->sketches.push_back(k.sk.serialize());
     }
-  } else if (nrows_out) {
+  } else if (nrows_out && !rows_done) {
     // Rows written by the kernel straight into the mapped pinned result block when it is pinned: no device->host
     // copies (small async D2H copies cost ~1 ms of completion latency each call on this stack, measured in C4).
     const bool direct = res->blk.pinned;
@@ -1439,10 +1528,11 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"table\":\"%s\","
-           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu}",
+           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\"}",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size(),
-           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes);
+           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
+           !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")));
   res->stats = buf;
   return LK_OK;
 }

@@ -58,7 +58,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   if (F.per_glob) {   // key = (bucket, glob, group): rows ascending in time, ties by glob (Commons.scala:391-392)
     const unsigned long long g = key % F.ngroups, t = key / F.ngroups;
     const unsigned long long gs = t % F.nglob_slots, b = t / F.nglob_slots;
-    const unsigned long long cell = (gs * F.nbuckets + b) * F.ngroups + g;
+    const unsigned long long cell = (gs * F.nbuckets + b) * F.ngroups + g - F.cell_base;
     if (F.rows[cell] == 0) return o;
     o.exists = true;
     o.value = cell_value(F, cell);
@@ -74,7 +74,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
   uint32_t best_rank = 0xffffffffu;
   for (uint32_t gs = 0; gs < F.nglob_slots; gs++) {
     for (unsigned long long g = g0; g < g0 + ng; g++) {
-      unsigned long long cell = ((unsigned long long)gs * F.nbuckets + b) * F.ngroups + g;
+      unsigned long long cell = ((unsigned long long)gs * F.nbuckets + b) * F.ngroups + g - F.cell_base;
       if (F.rows[cell] == 0) continue;
       unsigned long long c = F.cnt[cell];
       if (F.agg == AGG_SUM || F.agg == AGG_AVG) {
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(FB) void finalize_count(FParams F, uint32_t* block_
   const unsigned long long base = (unsigned long long)blockIdx.x * FB * FITEMS;
   for (int i = 0; i < FITEMS; i++) {
     unsigned long long key = base + (unsigned long long)i * FB + threadIdx.x;
-    if (key < F.nkeys && make_row(F, key).exists) n++;
+    if (key < F.nkeys && make_row(F, F.key_base + key).exists) n++;
   }
   for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = n;
@@ -162,9 +162,10 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
   uint32_t off = block_offsets[blockIdx.x];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   for (int i = 0; i < FITEMS; i++) {
-    unsigned long long key = base + (unsigned long long)i * FB + threadIdx.x;
+    const unsigned long long local = base + (unsigned long long)i * FB + threadIdx.x;
+    const unsigned long long key = F.key_base + local;
     OutRow r{false, 0, 0, 0};
-    if (key < F.nkeys) r = make_row(F, key);
+    if (local < F.nkeys) r = make_row(F, key);
     unsigned long long m = __ballot(r.exists);
     if (lane == 0) ws[wave] = __popcll(m);
     __syncthreads();

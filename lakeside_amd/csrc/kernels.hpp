@@ -25,6 +25,10 @@ struct FParams {
   int collapse;                    // merged without groupBys: one row per bucket (S19)
   int64_t bucket_base;
   int64_t step;
+  // key-range finalize (distributed): output keys [key_base, key_base + nkeys); the table arrays hold
+  // cells [cell_base, ...) of the full table (0, 0: the whole table)
+  unsigned long long key_base;
+  unsigned long long cell_base;
 };
 
 constexpr int AGG_AVG = 4;

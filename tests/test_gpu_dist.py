@@ -100,6 +100,47 @@ def test_dist_world2_host_transport_golden():
     mp.spawn(_worker, args=(2, _free_port()), nprocs=2, join=True)
 
 
+def _worker_keyrange(rank, world, port):
+    """Every dense merged table with groupBys takes the key-range all-to-all (threshold forced to 1 cell)."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ["LK_KEYRANGE_MIN_CELLS"] = "1"
+    import torch.distributed as dist
+
+    from lakeside_amd.evaluator import Engine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        used = 0
+        for case in _cases():
+            paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+            res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, _shard("modulo", len(paths), world),
+                                         case["glob_size"])
+            if rank == 0:
+                agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+                assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg,
+                                  f"keyrange world {world} {case['name']}")
+                ts = res.ts.tolist()
+                assert ts == sorted(ts), case["name"]
+                used += res.stats["reduce"] == "keyrange"
+            else:
+                assert len(res) == 0
+        if rank == 0:
+            assert used >= 3, used
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dist_world3_keyrange_golden():
+    """SURVEY §8(e) key-range all-to-all at an odd world size (uneven ranges, empty ranges on small tables)."""
+    import torch.multiprocessing as mp
+    mp.spawn(_worker_keyrange, args=(3, _free_port()), nprocs=3, join=True)
+
+
 @pytest.mark.timeout(120)
 def test_dist_world1_rccl_golden():
     from lakeside_amd.evaluator import Engine
@@ -187,6 +228,8 @@ def test_dist_world8_host_transport_c4_c5_shapes():
         assert_rows_equal(rows, want, "sum", f"world 8 {name}")
         if name == "c5_1m_hash":
             assert stats["table"] == "hash", stats
+        if name == "c5_1h":   # 20M dense cells: key-range all-to-all + per-rank finalize
+            assert stats["reduce"] == "keyrange", stats
 
 
 def _worker_err(rank, world, port):
