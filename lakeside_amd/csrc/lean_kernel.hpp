@@ -12,9 +12,12 @@
 //   one 16-B buffer load of the packed codes -> a pass mask:  SWAR (BW = 1, 2, 4, at most 4 passing codes: per
 //   32-bit word, xor with the code repeated, zero-field detect) or per code (a bit test of the pass mask);
 //   the passing rows (a divergent loop, two rows per trip) gather their value (and timestamp when the tile's zone
-//   map does not pin a single bucket) and accumulate into a per-thread register cell, spilling to an LDS table.
-// No list compaction, no workgroup barrier in the main loop.  VALU per row is a fraction of scan_tiles' (which
-// decodes every column generally, compacts rows through LDS and stages a late stage).
+//   map does not pin a single bucket) and accumulate into a per-thread register cell, spilling to an LDS table;
+//   dense blocks (most rows pass) are read row-major with coalesced loads instead;
+//   with late string columns (NL > 0) the wave's passing rows are first compacted into its LDS list and processed
+//   128 per trip with every lane busy (late-column lookups, late filter, value gather).
+// No workgroup barrier in the main loop.  VALU per row is a fraction of scan_tiles' (which decodes every column
+// generally and compacts rows through LDS).
 #pragma once
 #include <type_traits>
 
@@ -26,6 +29,8 @@ constexpr int LEAN_H = HCAP / 2;                                 // LDS cells (a
 constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a tile, upper bound
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
 constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
+
+constexpr uint32_t LEAN_LIST = 512;                                    // per-wave list of passing rows (late columns)
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -59,6 +64,7 @@ struct LeanLds {
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
+  uint32_t wlist[NL > 0 ? BLOCK / 64 : 1][NL > 0 ? LEAN_LIST : 1];   // late columns: each wave's passing rows
 };
 
 // The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
@@ -296,6 +302,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   }
   const bool one_bucket = tile_b >= 0;
   const uint32_t step32 = uint32_t(P.step);
+  // dense-block test only where a quarter or more of the chunk dictionary's codes pass (uniform; C2's 1 of 16 skips it)
+  const bool dense_codes = NL == 0 && 4u * npass >= dict_n;
   bool late_trivial = true;   // no filter leaf on a late column: the late stage only adds group terms (uniform)
 #pragma unroll
   for (int k = 0; k < NL; k++) late_trivial = late_trivial && P.strp[1 + k].lmask == 0u;
@@ -415,20 +423,68 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         m = f & valid;
       }
       const uint32_t rbase = v0 - vb2;   // tile row of value v0
-      // passing rows: two per trip (their loads in flight together)
-      while (m) {
-        const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
-        m &= m - 1ull;
-        const bool two = m != 0ull;
-        const uint32_t e2 = two ? (uint32_t(__builtin_ctzll(m)) >> shs) : e1;
-        if (two) m &= m - 1ull;
-        const uint32_t r1 = rbase + e1, r2 = rbase + e2;
-        uint32_t d1 = dim_u, d2 = dim_u;
-        if (npass > 1) {   // uniform: the rows' codes -> group terms
-          d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
-          d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
+      if (NL == 0 && dense_codes) {   // uniform
+        // Dense block: the wave's 64 chunks are 1024 row-contiguous rows and most chunks pass several rows.  The
+        // per-lane loop below would have each load instruction touch 64 different 128-B lines (8 B used of each,
+        // the other 120 B re-fetched by later trips -- evicted from L2 in between when every row passes), so the
+        // block is read row-major instead: trip j, lane L takes row 64j + L (one 512-B coalesced load per column);
+        // its pass bit and code come from the chunk's owner lane 4j + L/16 by cross-lane reads.
+        uint32_t f16 = uint32_t(m);
+        if (swar) {
+          f16 = 0;
+#pragma unroll
+          for (int e = 0; e < 16; e++) f16 |= uint32_t((m >> (e * BW + BW - 1)) & 1ull) << e;
         }
-        bool p1 = true, p2 = two;
+        const uint32_t v0l = uint32_t(__shfl(int(v0), 0));
+        const bool contig = live && valid == 0xffffu && v0 == v0l + 16u * uint32_t(lane);
+        if (__ballot(contig) == ~0ull && __popcll(__ballot(__popc(f16) >= 2u)) >= 48) {
+          const uint32_t rb0 = uni(rbase);
+          const uint32_t litv = lit ? 1u : 0u;
+#pragma unroll 1
+          for (int j0 = 0; j0 < 16; j0 += 4) {
+            v2u tt[4], xx[4];
+            bool pp[4];
+            uint32_t dd[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {   // issue the 4 trips' loads before any use
+              const int src = 4 * (j0 + u) + (lane >> 4);
+              const uint32_t e = uint32_t(lane) & 15u;
+              pp[u] = (uint32_t(__shfl(int(f16), src)) >> e) & 1u;
+              const uint32_t r = rb0 + 64u * uint32_t(j0 + u) + uint32_t(lane);
+              tt[u] = v2u{0u, 0u};
+              xx[u] = v2u{0u, 0u};
+              if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, pp[u] ? (vb0 + r) * 8u : OOB, 0, 0);
+              if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, pp[u] ? (vb1 + r) * 8u : OOB, 0, 0);
+              dd[u] = dim_u;
+              if (npass > 1) {   // uniform
+                const uint32_t a0 = uint32_t(__shfl(int(w0), src)), a1 = uint32_t(__shfl(int(w1), src));
+                const uint32_t a2 = uint32_t(__shfl(int(w2), src));
+                const uint32_t sl = uint32_t(__shfl(int(litv), src)), sv = uint32_t(__shfl(int(rval), src));
+                dd[u] = (L.lut[sl ? lean_code<BW>(a0, a1, a2, e) : sv] & DIM_MASK) * stride;
+              }
+              if (count_plan && pp[u]) {
+                if (!one_bucket) {
+                  const uint32_t l = (((vb0 + r) * 8u) >> 7) - line_t0;
+                  atomicOr(&L.lines_t[l >> 5], 1u << (l & 31u));
+                }
+                if (AGG != AGG_COUNT) {
+                  const uint32_t l = (((vb1 + r) * 8u) >> 7) - line_v0;
+                  atomicOr(&L.lines_v[l >> 5], 1u << (l & 31u));
+                }
+              }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+              if (pp[u])
+                row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x),
+                    __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x)), dd[u]);
+          }
+          m = 0;
+        }
+      }
+      // two rows (r1 live when a1, r2 when two) with group terms d1, d2: late columns, gather, accumulate
+      auto rows2 = [&](uint32_t r1, uint32_t r2, bool a1, bool two, uint32_t d1, uint32_t d2) __attribute__((always_inline)) {
+        bool p1 = a1, p2 = two;
         v2u t1 = v2u{0u, 0u}, t2 = v2u{0u, 0u}, x1 = v2u{0u, 0u}, x2 = v2u{0u, 0u};
         auto gather = [&]() __attribute__((always_inline)) {   // timestamps / values of the passing rows
           if (!one_bucket) {
@@ -464,7 +520,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
                 if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
               }
             };
-            issue(r1, true, lw1[k], lm1[k]);
+            issue(r1, a1, lw1[k], lm1[k]);
             issue(r2, two, lw2[k], lm2[k]);
           }
           if (late_trivial) gather();
@@ -502,7 +558,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
           if (!late_trivial) {
             const uint32_t lf = Sp->leaf_false;
             const uint32_t ix1 = (T1 & ~lf) | ((F1 | lf) << P.nleaves), ix2 = (T2 & ~lf) | ((F2 | lf) << P.nleaves);
-            p1 = (L.ltruth[ix1 >> 5] >> (ix1 & 31)) & 1u;
+            p1 = a1 && ((L.ltruth[ix1 >> 5] >> (ix1 & 31)) & 1u);
             p2 = two && ((L.ltruth[ix2 >> 5] >> (ix2 & 31)) & 1u);
             gather();
           }
@@ -527,6 +583,70 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
           row((int64_t)(((uint64_t)t1.y << 32) | t1.x), __longlong_as_double((long long)(((uint64_t)x1.y << 32) | x1.x)), d1);
         if (p2)
           row((int64_t)(((uint64_t)t2.y << 32) | t2.x), __longlong_as_double((long long)(((uint64_t)x2.y << 32) | x2.x)), d2);
+      };
+      if constexpr (NL == 0) {
+        // passing rows: two per trip (their loads in flight together)
+        while (m) {
+          const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
+          m &= m - 1ull;
+          const bool two = m != 0ull;
+          const uint32_t e2 = two ? (uint32_t(__builtin_ctzll(m)) >> shs) : e1;
+          if (two) m &= m - 1ull;
+          uint32_t d1 = dim_u, d2 = dim_u;
+          if (npass > 1) {   // uniform: the rows' codes -> group terms
+            d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
+            d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
+          }
+          rows2(rbase + e1, rbase + e2, true, two, d1, d2);
+        }
+      } else {
+        // Late columns: the wave's passing rows are compacted into its LDS list (tile row | code << 16, lane-major)
+        // and processed 128 per trip, every lane busy -- a per-lane loop would run as many trips as the lane with
+        // the most passing rows, each a chain of dependent late-column and value loads.
+        uint32_t f16 = uint32_t(m);
+        if (swar) {
+          f16 = 0;
+#pragma unroll
+          for (int e = 0; e < 16; e++) f16 |= uint32_t((m >> (e * BW + BW - 1)) & 1ull) << e;
+        }
+        const uint32_t cnt = uint32_t(__popc(f16));
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+          const uint32_t o = uint32_t(__shfl_up(int(inc), d, 64));
+          if (lane >= d) inc += o;
+        }
+        const uint32_t wtotal = uni(uint32_t(__shfl(int(inc), 63)));
+        const uint32_t pos0 = inc - cnt;
+        uint32_t* wl = L.wlist[tid >> 6];
+        for (uint32_t b0 = 0; b0 < wtotal; b0 += LEAN_LIST) {   // uniform
+          uint32_t f = f16, pos = pos0;
+          while (f) {
+            const uint32_t e = uint32_t(__builtin_ctz(f));
+            f &= f - 1u;
+            if (pos >= b0 && pos < b0 + LEAN_LIST)
+              wl[pos - b0] = (rbase + e) | ((lit ? lean_code<BW>(w0, w1, w2, e) : rval) << 16);
+            pos++;
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          const uint32_t nb = min(LEAN_LIST, wtotal - b0);
+          for (uint32_t j = 0; j < nb; j += 128) {   // uniform
+            const uint32_t i1 = j + uint32_t(lane), i2 = i1 + 64u;
+            const bool a1 = i1 < nb, a2 = i2 < nb;
+            const uint32_t x1 = a1 ? wl[i1] : 0u, x2 = a2 ? wl[i2] : 0u;
+            uint32_t d1 = dim_u, d2 = dim_u;
+            if (npass > 1) {
+              d1 = (L.lut[x1 >> 16] & DIM_MASK) * stride;
+              d2 = (L.lut[x2 >> 16] & DIM_MASK) * stride;
+            }
+            rows2(x1 & 0xffffu, x2 & 0xffffu, a1, a2, d1, d2);
+          }
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the list is rewritten by the next batch
+          __builtin_amdgcn_wave_barrier();
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
       }
     }
   };
