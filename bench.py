@@ -72,6 +72,9 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="segments timed on the CPU restatement (-1: all = full-size validation; 0: skip)")
     ap.add_argument("--gen-workers", type=int, default=4)
+    ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
+                    help="N > 1 exchange: RCCL over xGMI (default), or the host transport over gloo (rehearsal of the "
+                         "multi-rank path with several ranks on one GPU; RCCL refuses two ranks on one device)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -87,9 +90,12 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
-    torch.cuda.set_device(local_rank)
-    eng = Engine(local_rank)
-    if world > 1:
+    device = local_rank if args.comm == "rccl" else 0
+    torch.cuda.set_device(device)
+    eng = Engine(device)
+    if world > 1 and args.comm == "host":
+        eng.comm_init_host(world, rank)
+    elif world > 1:
         obj = [Engine.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0], world, rank)

@@ -303,15 +303,22 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
 
   std::vector<const FilterNode*> all_leaves;
   collect_leaves(R.filter.get(), all_leaves);
+  // Numeric comparison leaves (gt/ge/lt/le, BaseExpr.scala:488-498) compare a numeric column per row: such queries
+  // run on the general row scan (ex_scan AGG mode, ex_kernels.hip) instead of the fused string-filter kernels.
+  std::vector<std::string> nums;   // numeric filter columns
   for (auto* l : all_leaves) {
     if (l->extracted || l->computed) throw PlanError(LK_ERR_UNSUPPORTED, "extracted/computed filter fields");
-    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
-    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; })) {
-      if (l->op == "gt" || l->op == "ge" || l->op == "lt" || l->op == "le")
-        throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves are not on the hot path yet");
-      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
+    if (numeric_op(l->op)) {
+      if (std::find(nums.begin(), nums.end(), l->k) == nums.end()) nums.push_back(l->k);
+      continue;
     }
+    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
+    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; }))
+      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
   }
+  const bool numeric = !nums.empty();
+  if (numeric && (sketch || ces)) throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves in sketch queries");
+  if (numeric && dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed queries with numeric comparison leaves");
 
   // no segments: the worker answers one sentinel row (Commons.scala:393-396)
   if (R.segments.empty()) {
@@ -336,12 +343,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     return int(strs.size() - 1);
   };
   str_index(tagq ? R.tag_name : kName);   // the first string column is the leading group dim
-  for (auto* l : all_leaves) strs[str_index(l->k)].leaves.push_back(l);
+  for (auto* l : all_leaves)
+    if (!numeric_op(l->op)) strs[str_index(l->k)].leaves.push_back(l);
   std::vector<std::string> gbs;
   for (auto& g : R.group_bys)
     if (std::find(gbs.begin(), gbs.end(), g) == gbs.end()) gbs.push_back(g);
   for (auto& g : gbs) str_index(g);
   if (strs.size() > size_t(MAXSTR)) throw PlanError(LK_ERR_UNSUPPORTED, "too many string columns in one query");
+  for (auto& nm : nums)   // a column compared both as a string and as a number fails the glob's SQL either way
+    if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& sc) { return sc.name == nm; }) != strs.end())
+      throw PlanError(LK_ERR_UNSUPPORTED, "column " + nm + " used both as a string and as a number");
+  if (2 + strs.size() + nums.size() > size_t(MAXQCOL)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter columns");
   if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
   if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& s) { return s.name == kTimestamp || s.name == vcol; }) != strs.end())
     throw PlanError(LK_ERR_UNSUPPORTED, "filters / groupBys on the timestamp or value column");
@@ -357,6 +369,16 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (sc.leaves[j]->op == "has" || sc.leaves[j]->op == "exists") sc.hmask |= 1u << idx;
     }
   }
+  std::vector<NumLeaf> nleaves;
+  std::vector<std::string> bad_literal;   // fields whose numeric literal fails the SQL (per glob where they exist)
+  for (auto* l : all_leaves)
+    if (numeric_op(l->op)) {
+      const uint32_t idx = uint32_t(leaves.size());
+      leaves.push_back(LeafInfo{l, -1, int(idx)});
+      bool bad = false;
+      nleaves.push_back(make_num_leaf(*l, uint32_t(std::find(nums.begin(), nums.end(), l->k) - nums.begin()), idx, bad));
+      if (bad) bad_literal.push_back(l->k);
+    }
   std::vector<uint8_t> prog;
   postfix(R.filter.get(), leaves, prog);
   if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
@@ -445,6 +467,14 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
     for (auto& l : leaves)
       if (!nonexist.count(l.node->k) && !glob_has(gi, l.node->k)) g.skip = true;
+    for (auto& k : bad_literal)   // normalizedValue failed for a field this glob has
+      if (!nonexist.count(k)) g.skip = true;
+    // `<string column> > 1.5`: DuckDB cannot compare VARCHAR with a number (Binder Error) -> empty glob
+    for (auto& nm : nums)
+      for (int si : g.segs)
+        if (segs[si])
+          for (auto& [cname, pt] : segs[si]->schema)
+            if (cname == nm && pt == 6) g.skip = true;
     if (tagq) continue;
     if (g.step <= 0) throw PlanError(LK_ERR_ARG, "stepInMillis must be positive");
     if (step < 0) step = g.step;
@@ -669,13 +699,16 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
           throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
         if (qc == 0 && hc.ptype != 2) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
         if (qc == 1 && hc.ptype != 5) throw PlanError(LK_ERR_UNSUPPORTED, "value column must be DOUBLE");
-        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
+        if (qc >= 2 + int(strs.size()) && hc.ptype != 1 && hc.ptype != 2 && hc.ptype != 4 && hc.ptype != 5)
+          throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison on column " + name + " of an undecoded type");
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, uint32_t(hc.ptype)};
         alg_bytes += hc.compressed_bytes;
       };
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
       if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
       for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
       // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
       // name page has a small dictionary (lean_tile's test at page granularity)
       if (all_lean) {
@@ -728,7 +761,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       std::vector<const FilterNode*> ls;
       collect_leaves(n, ls);
       uint32_t m = 0;
-      for (auto* l : ls) m |= 1u << str_index(l->k);
+      for (auto* l : ls) m |= numeric_op(l->op) ? (1u << 31) : (1u << str_index(l->k));   // no StrCol for numbers
       return m;
     };
     // A conjunct of only `exists`/`has` leaves (IS NOT NULL: passes nearly every row, e.g. the one query-api adds
@@ -757,7 +790,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       const uint32_t m = cols_of(c);
       if (early >= 0 && m != (1u << early) && ((m >> early) & 1u)) mixed = true;
     }
-    if (early >= 0 && strs.size() >= 2 && !mixed) {
+    if (early >= 0 && strs.size() >= 2 && !mixed && !numeric) {
       std::vector<uint8_t> pe, pl;
       for (auto* c : conj) {
         std::vector<uint8_t>& dst = cols_of(c) == (1u << early) ? pe : pl;
@@ -904,7 +937,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // (<= 2 of them): NULL-free tiles with a small name dictionary go to scan_lean (lean_kernel.hpp), the rest to
   // scan_tiles
   const bool lean_shape = P.nstr == 1 || (P.nstr <= 3 && P.late_mask == ((1u << P.nstr) - 2u));
-  P.lean_split = (lean_shape && P.truth && agg != AGG_ROWS && !sketch && !getenv("LK_NO_LEAN_SPLIT")) ? (all_lean ? 2u : 1u) : 0u;
+  P.lean_split = (lean_shape && P.truth && agg != AGG_ROWS && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
+                    ? (all_lean ? 2u : 1u) : 0u;
+  if (numeric) P.lean = 0;   // the general row scan accumulates every table field
   if (sketch) {
     P.sketch = 1;
     P.dd_mult = dd::mapping().multiplier;
@@ -943,7 +978,28 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
     }
     launch_ms = ms_since(t_start);   // host staging done, scan enqueued
-    if (ncells) HIP_TRY(launch_scan(P, kagg, st));
+    if (ncells && numeric) {   // general row scan (numeric comparison leaves)
+      XParams XG{};
+      XG.segs = P.segs;
+      XG.nsegs = P.nsegs;
+      XG.max_tiles = P.max_tiles;
+      XG.strp = P.strp;
+      XG.nstr = P.nstr;
+      XG.nleaves = P.nleaves;
+      XG.nprog = P.nprog;
+      memcpy(XG.prog, P.prog, sizeof(XG.prog));
+      XG.truth = P.truth;
+      XG.mode = XMODE_AGG;
+      XG.nnum = uint32_t(nums.size());
+      XG.nnl = uint32_t(nleaves.size());
+      for (size_t i = 0; i < nleaves.size(); i++) XG.nl[i] = nleaves[i];
+      XG.agg = kagg;
+      XG.hash = hash_mode ? 1 : 0;
+      XG.q = P;
+      HIP_TRY(launch_ex_scan(XG, st));
+    } else if (ncells) {
+      HIP_TRY(launch_scan(P, kagg, st));
+    }
     HIP_TRY(hipEventRecord(X->ev_scan1, st));
     if (ncells) HIP_TRY(launch_fixup_table(P, nc, kagg, st));
     if (P.stamps) {

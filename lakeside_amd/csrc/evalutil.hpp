@@ -7,6 +7,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "kernels.hpp"
 #include "plan.hpp"
 #include "regex.hpp"
 
@@ -33,6 +34,11 @@ double ms_since(std::chrono::steady_clock::time_point t0);
 // Exemplar queries (no chart): exemplar.cpp.
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
                       int glob_size, unsigned flags, bool dist, lk_result* res);
+// Numeric comparison leaves (numleaf.cpp): gt / ge / lt / le; the normalized literal (PlanError(LK_ERR_ARG) where the
+// reference's SQL fails); the leaf's interval on numeric filter column `col`.
+bool numeric_op(const std::string& op);
+double normalized_value(const FilterNode& f);
+NumLeaf make_num_leaf(const FilterNode& f, uint32_t col, uint32_t leaf, bool& bad);
 // Java Double.toString / Float.toString text.
 template <class F>
 std::string java_float_text(F d);

@@ -28,8 +28,6 @@ namespace lk {
 
 namespace {
 
-constexpr int XNC = 1 + MAXSTR;   // column 0 = timestamp, 1.. = string columns (QSeg cols 2..)
-
 struct XHot {
   const uint8_t* vals;
   const uint8_t* defs;
@@ -70,35 +68,43 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
 
 }  // namespace
 
+template <int AGG, bool HASH>
+__device__ __forceinline__ void ex_merge(const QParams& q, unsigned long long cell, bool vok, double v) {
+  global_merge<AGG, HASH>(q, cell, 1u, vok ? 1u : 0u, vok ? v : 0.0, 0.0, vok ? dbl_order(v) : (AGG == AGG_MIN ? ~0ull : 0ull));
+}
+
 __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
-  __shared__ XHot H[XNC];
-  __shared__ LRun vr[XNC][RUN_CAP];
-  __shared__ LRun dr[XNC][RUN_CAP];
+  // column state by query column: 0 timestamp, 1 value (AGG), 2 .. 2+nstr strings, then numeric filter columns
+  __shared__ XHot H[MAXQCOL];
+  __shared__ LRun vr[MAXQCOL][RUN_CAP];
+  __shared__ LRun dr[MAXQCOL][RUN_CAP];
   __shared__ uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
-  __shared__ uint32_t wsum[XNC][BLOCK / 64];
+  __shared__ uint32_t wsum[MAXQCOL][BLOCK / 64];
   __shared__ uint32_t hist[XBINS];
 
   const QSeg* Sp = X.segs + blockIdx.y;
   const uint32_t t = blockIdx.x;
   if (t >= Sp->ntiles) return;
   const uint32_t g = Sp->glob_slot;
-  const int64_t lo = X.rlo[g], hi = X.rhi[g];
+  const bool aggm = X.mode == XMODE_AGG;
+  const int64_t lo = aggm ? Sp->win_lo : X.rlo[g], hi = aggm ? Sp->win_hi : X.rhi[g];
   const TileDesc* tdp = Sp->tiles + t;
   if (lo >= hi || tdp->ts_max < lo || tdp->ts_min >= hi) return;   // zone map outside the glob's open range
   const uint32_t nrows = tdp->nrows;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nc = 1 + int(X.nstr);
+  const int ns = int(X.nstr);
+  const int nc = 2 + ns + int(X.nnum);
 
   if (tid < nc) {
-    const int qc = tid == 0 ? 0 : tid + 1;
+    const int qc = tid;
     XHot h{};
-    h.present = Sp->cols[qc].present;
+    h.present = (qc == 1 && !aggm) ? 0u : Sp->cols[qc].present;
     if (h.present) {
       const TileCol tc = Sp->cols[qc].tcols[t];
       h.vals = Sp->base + tc.vals;
       h.defs = Sp->base + tc.defs;
       h.remap = Sp->cols[qc].remap + tc.remap;
-      h.tab = tid ? X.strp[tid - 1].strtab : nullptr;
+      h.tab = (qc >= 2 && qc < 2 + ns) ? X.strp[qc - 2].strtab : nullptr;
       h.vals_len = tc.vals_len;
       h.defs_len = tc.defs_len;
       h.vbase = tc.vbase;
@@ -109,25 +115,24 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
       h.kind = tc.kind;
       h.nulls = tc.has_nulls;
     }
-    H[tid] = h;
+    H[qc] = h;
   }
   if (X.truth)
     for (uint32_t i = tid; i < ((1u << (2 * X.nleaves)) + 31) / 32; i += BLOCK) truth[i] = X.truth[i];
   if (X.mode == XMODE_HIST)
     for (uint32_t i = tid; i < X.nbins; i += BLOCK) hist[i] = 0;
   __syncthreads();
-  for (int k = 0; k < nc; k++) {
-    if (!H[k].present) continue;
-    const int qc = k == 0 ? 0 : k + 1;
+  for (int qc = 0; qc < nc; qc++) {
+    if (!H[qc].present) continue;
     const TileCol* tc = Sp->cols[qc].tcols + t;
     const RunDesc* runs = Sp->cols[qc].runs;
-    for (uint32_t i = tid; i < H[k].nruns; i += BLOCK) {
+    for (uint32_t i = tid; i < H[qc].nruns; i += BLOCK) {
       const RunDesc r = runs[tc->run_lo + i];
-      vr[k][i] = LRun{r.start, r.off_lit, r.value};
+      vr[qc][i] = LRun{r.start, r.off_lit, r.value};
     }
-    for (uint32_t i = tid; i < H[k].ndruns; i += BLOCK) {
+    for (uint32_t i = tid; i < H[qc].ndruns; i += BLOCK) {
       const RunDesc r = runs[tc->drun_lo + i];
-      dr[k][i] = LRun{r.start, r.off_lit, r.value};
+      dr[qc][i] = LRun{r.start, r.off_lit, r.value};
     }
   }
   __syncthreads();
@@ -135,63 +140,100 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
   const uint32_t leaf_false = Sp->leaf_false;
   const int64_t hbase = X.mode == XMODE_HIST ? X.hbase[g] : 0;
   const int64_t hwidth = X.mode == XMODE_HIST ? X.hwidth[g] : 1;
-  uint32_t carry[XNC];
+  uint32_t carry[MAXQCOL];
 #pragma unroll
-  for (int k = 0; k < XNC; k++) carry[k] = 0;
+  for (int k = 0; k < MAXQCOL; k++) carry[k] = 0;
 
   for (uint32_t c0 = 0; c0 < nrows; c0 += BLOCK) {
     const uint32_t r = c0 + uint32_t(tid);
     const bool inb = r < nrows;
     uint32_t T = 0, F = 0;
-    bool ts_ok = false;
+    bool ts_ok = false, v_ok = false;
     int64_t ts = 0;
+    double v = 0.0;
+    unsigned long long gid = 0;
 #pragma unroll
-    for (int k = 0; k < XNC; k++) {
-      if (k >= nc) break;
-      const XHot& h = H[k];
+    for (int qc = 0; qc < MAXQCOL; qc++) {
+      if (qc >= nc) break;
+      const XHot& h = H[qc];
       bool ok = inb && h.present;
       uint32_t vi = h.vbase + r;
       if (h.present && h.nulls) {   // block-uniform
         const __amdgpu_buffer_rsrc_t drs = make_rsrc(h.defs, h.defs_len + 8);
         const uint32_t row = h.rip + r;
-        const int ri = find_run(dr[k], int(h.ndruns), row);
-        const bool bit = inb && (hybrid_get_buf(drs, dr[k][ri], row, 1) & 1u);
+        const int ri = find_run(dr[qc], int(h.ndruns), row);
+        const bool bit = inb && (hybrid_get_buf(drs, dr[qc][ri], row, 1) & 1u);
         const unsigned long long m = __ballot(bit);
         const uint32_t below = lanes_below(m);
-        if (lane == 0) wsum[k][wave] = uint32_t(__popcll(m));
+        if (lane == 0) wsum[qc][wave] = uint32_t(__popcll(m));
         __syncthreads();
         uint32_t before = 0, all = 0;
 #pragma unroll
         for (int w = 0; w < BLOCK / 64; w++) {
-          before += w < wave ? wsum[k][w] : 0u;
-          all += wsum[k][w];
+          before += w < wave ? wsum[qc][w] : 0u;
+          all += wsum[qc][w];
         }
         __syncthreads();
-        vi = h.vbase + carry[k] + before + below;
-        carry[k] += all;
+        vi = h.vbase + carry[qc] + before + below;
+        carry[qc] += all;
         ok = bit;
       }
-      if (k == 0) {
-        if (h.kind != PAGE_PLAIN64) ok = false;
+      if (qc < 2 || qc >= 2 + ns) {   // PLAIN numeric: timestamp, value, numeric filter column
+        const bool w8 = h.kind == PAGE_PLAIN64;
+        if (!w8 && h.kind != PAGE_PLAIN32) ok = false;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len);
-        const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? vi * 8u : OOB, 0, 0);
-        ts = int64_t((uint64_t(w.y) << 32) | w.x);
-        ts_ok = ok;
+        uint64_t raw = 0;
+        if (w8) {
+          const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? vi * 8u : OOB, 0, 0);
+          raw = (uint64_t(w.y) << 32) | w.x;
+        } else {
+          raw = __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? vi * 4u : OOB, 0, 0);
+        }
+        if (qc == 0) {
+          ts = int64_t(raw);
+          ts_ok = ok && w8;
+        } else if (qc == 1) {
+          v = __longlong_as_double((long long)raw);
+          v_ok = ok && w8;
+        } else {
+          const uint32_t pt = Sp->cols[qc].pad;   // Parquet physical type of this segment's column
+          const bool is_int = pt == 1u || pt == 2u;
+          const long long iv = pt == 2u ? (long long)raw : (long long)int32_t(uint32_t(raw));
+          const double dv = pt == 5u ? __longlong_as_double((long long)raw) : double(__uint_as_float(uint32_t(raw)));
+          for (uint32_t k = 0; k < X.nnl; k++) {
+            const NumLeaf& L = X.nl[k];
+            if (int(L.col) != qc - 2 - ns) continue;
+            if (!ok) continue;   // NULL: UNKNOWN
+            bool pass;
+            const double x = is_int ? double(iv) : dv;   // integers vs a DOUBLE (scientific) literal: cast first
+            if (is_int && !L.pad) {
+              pass = iv >= L.ilo && iv <= L.ihi;        // integers vs a decimal literal: exact
+            } else if (x != x) {
+              pass = L.nan_pass != 0;
+            } else {
+              pass = (x > L.dlo || (L.lo_incl && x == L.dlo)) && (x < L.dhi || (L.hi_incl && x == L.dhi));
+            }
+            T |= uint32_t(pass) << L.leaf;
+            F |= uint32_t(!pass) << L.leaf;
+          }
+        }
         continue;
       }
-      const StrParam& sp = X.strp[k - 1];
+      const StrParam& sp = X.strp[qc - 2];
       if (!h.present || h.nruns == 0u) ok = false;   // absent / no value in this tile: NULL
       if (ok) {
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len + 8);
-        const int ri = find_run(vr[k], int(h.nruns), vi);
-        const uint32_t idx = hybrid_get_buf(rs, vr[k][ri], vi, int(h.bw));
-        const uint32_t gid = h.remap[idx];
-        const uint32_t packed = h.tab ? h.tab[gid] : 0u;
+        const int ri = find_run(vr[qc], int(h.nruns), vi);
+        const uint32_t idx = hybrid_get_buf(rs, vr[qc][ri], vi, int(h.bw));
+        const uint32_t gl = h.remap[idx];
+        const uint32_t packed = h.tab ? h.tab[gl] : gl;
         const uint32_t bits = (packed >> 24) << sp.lbase;
         T |= bits & sp.lmask;
         F |= ~bits & sp.lmask;
+        gid += (unsigned long long)(packed & DIM_MASK) * sp.dim_stride;
       } else {
         F |= sp.hmask;   // IS NOT NULL on NULL: FALSE; other leaves NULL
+        gid += (unsigned long long)sp.dim_null * sp.dim_stride;
       }
     }
     T &= ~leaf_false;
@@ -204,7 +246,40 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
       pass = x_interpret(X, T, F);
     }
     pass = pass && ts_ok && ts >= lo && ts < hi;
-    if (X.mode == XMODE_HIST) {
+    if (X.mode == XMODE_AGG) {
+      if (pass) {
+        const QParams& q = X.q;
+        int64_t b;
+        bool ok = true;
+        if (q.metrics) {   // BaseExpr.scala:376-394: the raw timestamp, on the step grid
+          const int64_t d = ts - q.bucket_base;
+          b = d / q.step;
+          if (d - b * q.step != 0) {
+            atomicOr(q.flags, FLAG_METRICS_UNALIGNED);
+            ok = false;
+          }
+        } else {           // BaseExpr.scala:163-165: ts - ts % step
+          b = ((ts - ts % q.step) - q.bucket_base) / q.step;
+        }
+        if (ok && (b < 0 || (uint64_t)b >= q.nbuckets)) {
+          atomicOr(q.flags, FLAG_CELL_RANGE);
+          ok = false;
+        }
+        if (ok) {
+          const unsigned long long cell = ((unsigned long long)g * q.nbuckets + (unsigned long long)b) * q.ngroups + gid;
+          switch (X.agg * 2 + (X.hash ? 1 : 0)) {
+            case AGG_SUM * 2: ex_merge<AGG_SUM, false>(q, cell, v_ok, v); break;
+            case AGG_SUM * 2 + 1: ex_merge<AGG_SUM, true>(q, cell, v_ok, v); break;
+            case AGG_MIN * 2: ex_merge<AGG_MIN, false>(q, cell, v_ok, v); break;
+            case AGG_MIN * 2 + 1: ex_merge<AGG_MIN, true>(q, cell, v_ok, v); break;
+            case AGG_MAX * 2: ex_merge<AGG_MAX, false>(q, cell, v_ok, v); break;
+            case AGG_MAX * 2 + 1: ex_merge<AGG_MAX, true>(q, cell, v_ok, v); break;
+            case AGG_COUNT * 2: ex_merge<AGG_COUNT, false>(q, cell, v_ok, v); break;
+            default: ex_merge<AGG_COUNT, true>(q, cell, v_ok, v); break;
+          }
+        }
+      }
+    } else if (X.mode == XMODE_HIST) {
       if (pass) {
         int64_t b = (ts - hbase) / hwidth;
         b = b < 0 ? 0 : (b >= int64_t(X.nbins) ? int64_t(X.nbins) - 1 : b);

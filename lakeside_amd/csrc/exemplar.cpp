@@ -213,14 +213,16 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
 
   std::vector<const FilterNode*> all_leaves;
   collect_leaves(R.filter.get(), all_leaves);
+  std::vector<std::string> nums;   // numeric comparison columns (gt/ge/lt/le, BaseExpr.scala:488-498)
   for (auto* l : all_leaves) {
     if (l->extracted || l->computed) throw PlanError(LK_ERR_UNSUPPORTED, "extracted/computed filter fields");
-    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
-    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; })) {
-      if (l->op == "gt" || l->op == "ge" || l->op == "lt" || l->op == "le")
-        throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves are not on the hot path yet");
-      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
+    if (numeric_op(l->op)) {
+      if (std::find(nums.begin(), nums.end(), l->k) == nums.end()) nums.push_back(l->k);
+      continue;
     }
+    static const char* ok[] = {"eq", "!=", "in", "not_in", "regex", "contains", "has", "exists"};
+    if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; }))
+      throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
   }
   res->exemplar = true;
   res->per_glob = true;
@@ -244,6 +246,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   };
   std::vector<XStr> strs;
   for (auto* l : all_leaves) {
+    if (numeric_op(l->op)) continue;
     auto it = std::find_if(strs.begin(), strs.end(), [&](const XStr& s) { return s.name == l->k; });
     if (it == strs.end()) {
       strs.push_back(XStr{});
@@ -252,7 +255,11 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     }
     it->leaves.push_back(l);
   }
-  if (strs.size() > size_t(MAXSTR)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter columns in one query");
+  if (2 + strs.size() + nums.size() > size_t(MAXQCOL))
+    throw PlanError(LK_ERR_UNSUPPORTED, "too many filter columns in one query");
+  for (auto& nm : nums)
+    if (std::find_if(strs.begin(), strs.end(), [&](const XStr& sc) { return sc.name == nm; }) != strs.end())
+      throw PlanError(LK_ERR_UNSUPPORTED, "column " + nm + " used both as a string and as a number");
   if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
   std::vector<LeafInfo> leaves;
   for (size_t s = 0; s < strs.size(); s++) {
@@ -266,6 +273,16 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       if (l->op == "has" || l->op == "exists") sc.hmask |= 1u << idx;
     }
   }
+  std::vector<NumLeaf> nleaves;
+  std::vector<std::string> bad_literal;   // fields whose numeric literal fails the SQL (per glob where they exist)
+  for (auto* l : all_leaves)
+    if (numeric_op(l->op)) {
+      const uint32_t idx = uint32_t(leaves.size());
+      leaves.push_back(LeafInfo{l, -1, int(idx)});
+      bool bad = false;
+      nleaves.push_back(make_num_leaf(*l, uint32_t(std::find(nums.begin(), nums.end(), l->k) - nums.begin()), idx, bad));
+      if (bad) bad_literal.push_back(l->k);
+    }
   std::vector<uint8_t> prog;
   postfix(R.filter.get(), leaves, prog);
   if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
@@ -298,6 +315,10 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       if (!g.types.count(p)) g.skip = true;
     for (auto& l : leaves)
       if (!(g.leaf_false >> l.index & 1u) && !g.types.count(l.node->k)) g.skip = true;
+    for (auto& k : bad_literal)   // normalizedValue failed for a field this glob has
+      if (!(fset.count(k) && !g.types.count(k))) g.skip = true;
+    for (auto& nm : nums)   // a VARCHAR compared with a number: Binder Error -> empty glob
+      if (g.types.count(nm) && g.types[nm] == pq::BYTE_ARRAY) g.skip = true;
     g.cols = proj;
     for (auto& u : uni)
       if (std::find(g.cols.begin(), g.cols.end(), u) == g.cols.end()) g.cols.push_back(u);
@@ -367,11 +388,15 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
         if (want_string != hc.is_string)
           throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
         if (qc == 0 && hc.ptype != pq::INT64) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
-        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
+        if (qc >= 2 + int(strs.size()) && hc.ptype != pq::INT64 && hc.ptype != pq::DOUBLE && hc.ptype != pq::INT32 &&
+            hc.ptype != pq::FLOAT)
+          throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison on column " + name + " of an undecoded type");
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, uint32_t(hc.ptype)};
       };
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;
       for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
       rows_scanned += uint64_t(S.num_rows);
       max_tiles = std::max(max_tiles, q.ntiles);
       qsegs.push_back(q);
@@ -424,6 +449,9 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   P.nprog = uint32_t(prog.size());
   memcpy(P.prog, prog.data(), prog.size());
   P.truth = truth.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_truth);
+  P.nnum = uint32_t(nums.size());
+  P.nnl = uint32_t(nleaves.size());
+  for (size_t i = 0; i < nleaves.size(); i++) P.nl[i] = nleaves[i];
   int64_t* d_rng = reinterpret_cast<int64_t*>(dbuf + o_rng);
   P.rlo = d_rng;
   P.rhi = d_rng + ng;

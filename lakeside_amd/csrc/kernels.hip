@@ -51,6 +51,19 @@ __device__ __forceinline__ double cell_value(const FParams& F, unsigned long lon
   }
 }
 
+// query-api's merge of per-glob min/max values: Scala math.min / math.max = java.lang.Math (a NaN argument gives NaN;
+// -0.0 < +0.0), TimeGroupedSketchAggregator.scala:79-88.  (fmin/fmax would drop the NaN.)
+__device__ __forceinline__ double java_min(double a, double b) {
+  if (a != a || b != b) return __longlong_as_double(0x7ff8000000000000ll);
+  if (a == 0.0 && b == 0.0) return signbit(a) ? a : b;
+  return a < b ? a : b;
+}
+__device__ __forceinline__ double java_max(double a, double b) {
+  if (a != a || b != b) return __longlong_as_double(0x7ff8000000000000ll);
+  if (a == 0.0 && b == 0.0) return signbit(a) ? b : a;
+  return a > b ? a : b;
+}
+
 // Output key -> row. Per-glob: key = (glob, bucket, group). Merged: key = (bucket, group) or (bucket)
 // when the name dimension collapses (no groupBys).
 __device__ OutRow make_row(const FParams& F, unsigned long long key) {
@@ -85,7 +98,7 @@ __device__ OutRow make_row(const FParams& F, unsigned long long key) {
       } else if (F.agg == AGG_MIN || F.agg == AGG_MAX) {
         double v = c ? order_dbl(F.ext[cell]) : 0.0;   // a glob's NULL cell merges as 0.0
         if (!o.exists) ext = v;
-        else ext = (F.agg == AGG_MIN) ? fmin(ext, v) : fmax(ext, v);
+        else ext = (F.agg == AGG_MIN) ? java_min(ext, v) : java_max(ext, v);
       }
       cnt += c;
       nrows += F.rows[cell];
@@ -371,7 +384,7 @@ __global__ __launch_bounds__(SB) void runs_write(SParams S, const unsigned long 
           } else {
             const double v = cc ? order_dbl(S.ext[c]) : 0.0;
             if (!any) ext = v;
-            else ext = (S.agg == AGG_MIN) ? fmin(ext, v) : fmax(ext, v);
+            else ext = (S.agg == AGG_MIN) ? java_min(ext, v) : java_max(ext, v);
           }
         }
         cnt += cc;

@@ -111,7 +111,18 @@ hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws,
 // every tile meeting its glob's open range [rlo, rhi) and either counts passing rows per time bin (HIST) or appends
 // them as (timestamp, segment << 48 | tile << 16 | row) records (EMIT).
 constexpr uint32_t XBINS = 2048;
-enum XMode : uint32_t { XMODE_HIST = 0, XMODE_EMIT = 1 };
+enum XMode : uint32_t { XMODE_HIST = 0, XMODE_EMIT = 1, XMODE_AGG = 2 };
+// A numeric comparison leaf (`gt/ge/lt/le`, BaseExpr.scala:488-498) on numeric filter column `col` (QSeg column
+// 2 + nstr + col, its Parquet physical type in QCol.pad): TRUE iff the value lies in the interval, FALSE otherwise,
+// UNKNOWN on NULL.  Integer columns test [ilo, ihi] (exact); floating columns the double interval, NaN (ordered
+// greatest by DuckDB) passing iff nan_pass.
+struct NumLeaf {
+  uint32_t col, leaf;
+  uint32_t lo_incl, hi_incl, nan_pass;
+  uint32_t pad;                    // 1: integer columns compare as double (|literal| >= 1e7 prints in E notation)
+  double dlo, dhi;
+  long long ilo, ihi;
+};
 struct XParams {
   const QSeg* segs;
   uint32_t nsegs;
@@ -132,6 +143,14 @@ struct XParams {
   unsigned long long* out;         // EMIT: 2 words per record
   uint32_t* out_n;                 // EMIT: records appended (may exceed cap: only the first cap are written)
   uint32_t cap;
+  uint32_t nnum;                   // numeric filter columns
+  uint32_t nnl;                    // numeric leaves
+  NumLeaf nl[MAXLEAF];
+  // AGG (general scan: the queries the fused kernels do not take, e.g. numeric leaves): rows in the glob window
+  // aggregate into q's table (q.segs..q.strp as above; value column = QSeg column 1) with device atomics
+  int agg;                         // Agg (kernel aggregate)
+  int hash;                        // q's table is the hash-mode table
+  QParams q;
 };
 hipError_t launch_ex_scan(const XParams& X, hipStream_t stream);
 

@@ -18,8 +18,10 @@ Semantics follow SURVEY.md Appendix A (S1-S22); each function cites the referenc
 """
 from __future__ import annotations
 
+import functools
 import json
 import math
+import re
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
@@ -244,9 +246,7 @@ def check_hot_path(pr: PushDownRequest) -> None:
         if isinstance(q, Filter):
             if q.extracted or q.computed:
                 raise NotImplementedError("extracted/computed filter fields are outside the hot path")
-            if q.op in (GT, GE, LT, LE):
-                raise NotImplementedError("numeric comparisons are not on the hot path yet")
-            if q.op not in (EQ, NOT_EQUALS, IN, NOT_IN, REGEX, CONTAINS, HAS, EXISTS):
+            if q.op not in (EQ, NOT_EQUALS, IN, NOT_IN, REGEX, CONTAINS, HAS, EXISTS, GT, GE, LT, LE):
                 raise ValueError(f"Invalid operator {q.op}")
         elif isinstance(q, BinaryClause):
             if q.op not in ("and", "or"):
@@ -338,11 +338,160 @@ def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[s
     return union, nums, strs
 
 
+# ----------------------------------------------------------------------------------------------
+# Numeric comparison leaves (BaseExpr.scala:450-459, 488-498): `<label> > <normalizedValue>`
+# ----------------------------------------------------------------------------------------------
+NUMERIC_OPS = (GT, GE, LT, LE)
+
+
+class GlobSqlError(Exception):
+    """The glob's generated SQL fails (DuckDB error / exception in generateSql): an empty glob
+    (Commons.scala:249-253)."""
+
+
+_JAVA_DOUBLE = re.compile(r"[+-]?(NaN|Infinity|([0-9]+\.?[0-9]*|\.[0-9]+)([eE][+-]?[0-9]+)?[fFdD]?)")
+
+
+def java_parse_double(text: str) -> float:
+    """java.lang.Double.parseDouble (decimal grammar; surrounding whitespace, f/F/d/D suffix)."""
+    t = text.strip(" \t\n\r\x0b\x0c\x00")
+    if not _JAVA_DOUBLE.fullmatch(t):
+        raise GlobSqlError(f"NumberFormatException: {text!r}")
+    if t[-1] in "fFdD" and "Infinity" not in t:
+        t = t[:-1]
+    if "NaN" in t:
+        return float("nan")
+    if "Infinity" in t:
+        return float("-inf") if t.startswith("-") else float("inf")
+    return float(t)
+
+
+_QUANTITY = re.compile("([0-9]+(.[0-9]+)?)(\\w+|\u00b5s)", re.ASCII)
+_DUR = {**{u: lambda x: x * 1000000000.0 for u in ("s", "sec", "secs", "second", "seconds")},
+        **{u: lambda x: (x * 60) * 1000000000.0 for u in ("m", "min", "mins", "minute", "minutes")},
+        **{u: lambda x: x * 1000000.0 for u in ("ms", "milli", "millis", "millisecond", "milliseconds")},
+        **{u: lambda x: x * 1000.0 for u in ("\u00b5s", "micro", "micros", "microsecond", "microseconds")},
+        "ns": lambda x: x,
+        **{u: lambda x: (x * 3600) * 1000000000.0 for u in ("h", "hr", "hrs", "hour", "hours")},
+        **{u: lambda x: ((x * 24) * 3600) * 1000000000.0 for u in ("d", "day", "days")}}
+_SIZE = {**dict.fromkeys(("b", "byte", "bytes"), 1.0), **dict.fromkeys(("k", "kb", "kilobyte", "kilobytes"), 1000.0),
+         **dict.fromkeys(("m", "mb", "mbs", "megabyte"), 1e6),
+         **dict.fromkeys(("g", "gb", "gbs", "gigabyte", "gigabytes"), 1e9),
+         **dict.fromkeys(("t", "tb", "tbs", "terabyte", "terabytes"), 1e12),
+         **dict.fromkeys(("pb", "pbs", "petabyte", "petabytes"), 1e15),
+         **dict.fromkeys(("mib", "mibs", "mebibyte", "mebibytes"), 131072.0),
+         **dict.fromkeys(("kib", "kibs", "kibibyte", "kibibytes"), 128.0),
+         **dict.fromkeys(("gib", "gibs", "gibibyte", "gibibytes"), 134200000.0),
+         **dict.fromkeys(("tib", "tibs", "tibibyte", "tibibytes"), 137400000000.0),
+         **dict.fromkeys(("pib", "pibs", "pibibyte", "pibibytes"), 1126000000000000.0)}
+
+
+def parse_quantity(value: str, duration: bool) -> Optional[float]:
+    """QuantityParser.parseQuantity (core/.../utils/QuantityParser.scala:124-141): first match of
+    ([0-9]+(.[0-9]+)?)(\\w+|µs), unit lower-cased, normalized left to right in Double arithmetic."""
+    m = _QUANTITY.search(value)
+    if not m:
+        return None
+    x = java_parse_double(m.group(1))
+    unit = m.group(3).lower()
+    if duration:
+        f = _DUR.get(unit)
+        return None if f is None else f(x)
+    k = _SIZE.get(unit)
+    return None if k is None else x * k
+
+
+def normalized_value(f: Filter) -> float:
+    """BaseExpr.scala:450-459: the literal of a numeric comparison (NaN / Infinity print as identifiers: an error)."""
+    if f.dataType in ("duration", "datasize", "number") and len(f.v) != 1:
+        raise GlobSqlError("filter value is a list of values")
+    if f.dataType == "number":
+        c = java_parse_double(f.v[0])
+    elif f.dataType in ("duration", "datasize"):
+        q = parse_quantity(f.v[0], f.dataType == "duration")
+        c = 0.0 if q is None else q
+    else:
+        c = float("nan")
+    if not math.isfinite(c):
+        raise GlobSqlError(f"{f.k} {f.op} {c}")
+    return c
+
+
+class _NumCol:
+    """A numeric column of a glob: Python values (None = NULL) and its union kind ('int' / 'float')."""
+
+    def __init__(self, vals: list, kind: str):
+        self.vals = vals
+        self.kind = kind
+
+
+def _read_numeric(paths: Sequence[str], names: Sequence[str], sources=None):
+    """union_by_name read of numeric filter columns; a column stored as a string anywhere in the glob makes the
+    comparison a Binder Error (GlobSqlError)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    out = {}
+    files = []
+    for i, p in enumerate(paths):
+        pf = pq.ParquetFile(p if sources is None else pa.BufferReader(sources[i]))
+        want = [c for c in names if c in pf.schema_arrow.names]
+        files.append((pf.read(columns=want), pf.metadata.num_rows))
+    for c in names:
+        vals, kinds = [], set()
+        for t, n in files:
+            if c not in t.column_names:
+                vals.extend([None] * n)
+                continue
+            typ = t.schema.field(c).type
+            if pa.types.is_dictionary(typ):
+                typ = typ.value_type
+            if pa.types.is_integer(typ):
+                kinds.add("int")
+            elif pa.types.is_floating(typ):
+                kinds.add("float")
+            else:
+                raise GlobSqlError(f"cannot compare {typ} column {c} with a number")
+            vals.extend(t.column(c).to_pylist())
+        out[c] = _NumCol(vals, "int" if kinds <= {"int"} else "float")
+    return out
+
+
+def _num_leaf(f: Filter, col: Optional[_NumCol], n: int):
+    """x > c etc.: NULL -> UNKNOWN; NaN ordered greatest (DuckDB); an integer column compares exactly against a
+    decimal literal (|c| < 1e7: Double.toString prints it plain) and as DOUBLE against a scientific one."""
+    c = normalized_value(f)
+    t = np.zeros(n, bool)
+    fl = np.zeros(n, bool)
+    if col is None:
+        return t, fl
+    exact = col.kind == "int" and abs(c) < 1e7
+    for i, x in enumerate(col.vals):
+        if x is None:
+            continue
+        if not exact:
+            x = float(x)
+        if x != x:
+            ok = f.op in (GT, GE)
+        elif f.op == GT:
+            ok = x > c
+        elif f.op == GE:
+            ok = x >= c
+        elif f.op == LT:
+            ok = x < c
+        else:
+            ok = x <= c
+        t[i] = ok
+        fl[i] = not ok
+    return t, fl
+
+
 def _leaf(f: Filter, col: Optional[_Col], nonexistent: set, n: int):
     """One filter leaf under SQL three-valued logic -> (is_true, is_false) masks.
     Leaf compile: BaseExpr.scala:461-504; NULL semantics: SURVEY.md Appendix A S7."""
     if f.k in nonexistent:                       # BaseExpr.scala:462-464 -> literal `false`
         return np.zeros(n, bool), np.ones(n, bool)
+    if f.op in NUMERIC_OPS:
+        return _num_leaf(f, col, n)
     if col is None:                              # absent column referenced only under NOT: all NULL
         codes, dictionary = np.full(n, -1, np.int64), []
     else:
@@ -381,6 +530,22 @@ def _eval_filter(q, cols: Dict[str, _Col], nonexistent: set, n: int):
     if q.op == "and":
         return t1 & t2, f1 | f2
     return t1 | t2, f1 & f2
+
+
+def _check_numeric_literals(q, nonexistent: set) -> bool:
+    """generateSql's numeric leaves (BaseExpr.scala:450-459): a list of values for a normalized dataType throws for
+    every glob; the literal itself (normalizedValue, a lazy def) is computed only for fields that exist -- a bad
+    one fails that glob's SQL.  False: the glob's query fails."""
+    try:
+        for l in _leaves(q):
+            if l.op in NUMERIC_OPS:
+                if l.dataType in ("duration", "datasize", "number") and len(l.v) != 1:
+                    return False
+                if l.k not in nonexistent:
+                    normalized_value(l)
+    except GlobSqlError:
+        return False
+    return True
 
 
 def _leaf_columns(q) -> List[str]:
@@ -443,13 +608,20 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
     segs = [pr.segmentRequests[i] for i in seg_idx]
     vcol = value_column(be)
     fs = field_set(be)
-    strings = sorted(set(_leaf_columns(be.filter)) | set(chart.groupBys) | {NAME})
+    numcols = sorted({l.k for l in _leaves(be.filter) if l.op in NUMERIC_OPS})
+    strings = sorted((set(_leaf_columns(be.filter)) - set(numcols)) | set(chart.groupBys) | {NAME})
     if only is not None:
         paths = [paths[j] for j in only]
         sources = None if sources is None else [sources[j] for j in only]
     read_union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
+    try:
+        strs.update(_read_numeric(paths, [c for c in numcols if c in read_union], sources))
+    except GlobSqlError:
+        return []
     union = list(union) if union is not None else read_union
     nonexistent = fs - set(union)                                   # Commons.scala:224
+    if not _check_numeric_literals(be.filter, nonexistent):
+        return []
     # Columns the generated SQL references but that no file of the glob has: DuckDB raises a Binder
     # Error, which Commons.toGlobResultSet turns into an empty result (Commons.scala:249-253).  This
     # happens for a field used only under `not` (not in fieldSet), and for ts/name/value columns.
@@ -542,6 +714,25 @@ def evaluate_per_glob(pr: PushDownRequest, paths: Sequence[str], glob_size: int 
             for cells in evaluate_glob_cells(pr, glob_size, paths, sources)]
 
 
+def java_min(a: float, b: float) -> float:
+    """Scala math.min = java.lang.Math.min (TimeGroupedSketchAggregator.scala:79-83): NaN if either is NaN,
+    -0.0 below +0.0."""
+    if a != a or b != b:
+        return math.nan
+    if a == 0.0 and b == 0.0:
+        return -0.0 if (math.copysign(1, a) < 0 or math.copysign(1, b) < 0) else 0.0
+    return a if a < b else b
+
+
+def java_max(a: float, b: float) -> float:
+    """Scala math.max = java.lang.Math.max (TimeGroupedSketchAggregator.scala:84-88)."""
+    if a != a or b != b:
+        return math.nan
+    if a == 0.0 and b == 0.0:
+        return 0.0 if (math.copysign(1, a) > 0 or math.copysign(1, b) > 0) else -0.0
+    return a if a > b else b
+
+
 def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, Dict[str, str]]]:
     """query-api merge (S19): TimeGroupedSketchAggregator (TimeGroupedSketchAggregator.scala:57-114,
     148-170).  Cells merge by exact timestamp; with groupBys by the full tag map, otherwise all cells of a
@@ -575,9 +766,9 @@ def merge_glob_cells(pr: PushDownRequest, glob_cells) -> List[Tuple[int, float, 
             s = exact_sum(np.concatenate([c.values for c in cs]))
             val = s / n if n else math.nan
         elif agg == MIN:
-            val = min(c.agg_value(MIN) for c in cs)
+            val = functools.reduce(java_min, (c.agg_value(MIN) for c in cs))
         else:
-            val = max(c.agg_value(MAX) for c in cs)
+            val = functools.reduce(java_max, (c.agg_value(MAX) for c in cs))
         out.append((cs[0].ts, val, tags))
     out.sort(key=lambda r: (r[0], sorted(r[2].items()), r[1]))
     return out
@@ -649,9 +840,16 @@ def evaluate_tag_glob(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], pat
         raise NotImplementedError("synthetic (extracted/computed) tag queries are outside the hot path")
     segs = [pr.segmentRequests[i] for i in seg_idx]
     fs = filter_field_set(be.filter) | set(be.chart.groupBys if be.chart else [])
-    strings = sorted(set(_leaf_columns(be.filter)) | {tag})
+    numcols = sorted({l.k for l in _leaves(be.filter) if l.op in NUMERIC_OPS})
+    strings = sorted((set(_leaf_columns(be.filter)) - set(numcols)) | {tag})
     union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources)
+    try:
+        strs.update(_read_numeric(paths, [c for c in numcols if c in union], sources))
+    except GlobSqlError:
+        return []
     nonexistent = fs - set(union)
+    if not _check_numeric_literals(be.filter, nonexistent):
+        return []
     referenced = (set(_leaf_columns(be.filter)) - nonexistent) | {TIMESTAMP, tag}
     if not referenced <= set(union):                                  # Binder Error -> empty glob
         return []

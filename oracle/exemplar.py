@@ -152,8 +152,12 @@ def evaluate_exemplar_glob(pr: dx.PushDownRequest, seg_idx: Sequence[int], paths
         return []                                                    # Binder Error -> empty (Commons.scala:249-253)
     start = min(s.startTs for s in segs)
     end = max(s.endTs for s in segs)
-    strings = sorted(set(leafcols) - nonexistent)
+    numcols = sorted({l.k for l in dx._leaves(be.filter) if l.op in dx.NUMERIC_OPS} - nonexistent)
+    if any(types.get(c) == "string" for c in numcols) or not dx._check_numeric_literals(be.filter, nonexistent):
+        return []                                                    # VARCHAR vs number / bad literal: SQL error
+    strings = sorted(set(leafcols) - nonexistent - set(numcols))
     _, nums, strs = dx._read_glob(paths, [dx.TIMESTAMP], strings, sources)
+    strs.update(dx._read_numeric(paths, [c for c in numcols if c in types], sources))
     ts, tsv = nums[dx.TIMESTAMP]
     ts = ts.astype(np.int64)
     n = len(ts)
