@@ -236,7 +236,7 @@ def main():
             "data": f"synthetic sealed Parquet (tools/synth.cpp, seed 20240101+i), {S} x {args.rows} rows per GPU",
             "config": {"workload": f"{args.query.upper()}: {total} segments x {args.rows} rows, {q['desc']}",
                        "segments_per_gpu": S, "rows_per_segment": args.rows, "glob_size": 10,
-                       "parallelism": f"segment-sharded x{world}" + (", RCCL table reduce" if world > 1 else "")},
+                       "parallelism": f"segment-sharded x{world}" + ((", RCCL table reduce" if args.comm == "rccl" else ", host-transport table reduce (rehearsal)") if world > 1 else "")},
             "datapoints_per_sec": out_rows / (ms_per_step / 1e3),
             "rows_scanned": rows_total, "output_rows": out_rows,
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
