@@ -369,6 +369,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         em &= em ? em - 1 : 0ull;
       }
     }
+    // NL > 0: the next round's packed codes are loaded one round ahead, so they arrive while this round waits on its
+    // late-column and value loads (loads return in issue order: one memory round trip less per round)
+    auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
+      const bool lv = qq < total;
+      const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];
+      const uint32_t bn = (Rn.off_lit & 0x7fffffffu) + 2u * BW * (qq - Rn.cbk);
+      return __builtin_amdgcn_raw_buffer_load_b128(rs2, (lv && (Rn.off_lit & 0x80000000u)) ? (bn & ~3u) : OOB, 0, 0);
+    };
+    v4u xpre = v4u{0u, 0u, 0u, 0u};
+    if constexpr (NL > 0) xpre = chunk_load(uint32_t(tid));
     for (uint32_t q0 = 0; q0 < total; q0 += BLOCK) {   // uniform trip count
       const uint32_t q = q0 + uint32_t(tid);
       const bool live = q < total;
@@ -381,7 +391,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       const bool lit = (R.off_lit & 0x80000000u) != 0u;
       const uint32_t rval = R.value & 63u;
       const uint32_t byte = (R.off_lit & 0x7fffffffu) + 2u * BW * k;
-      const v4u x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      v4u x;
+      if constexpr (NL > 0) {
+        x = xpre;
+        xpre = chunk_load(q + BLOCK);
+      } else {
+        x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      }
       const uint32_t sh = (byte & 3u) * 8u;
       uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
       uint32_t w1 = __builtin_amdgcn_alignbit(x.z, x.y, sh);
