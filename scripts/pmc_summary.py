@@ -1,5 +1,5 @@
 """Summarise rocprofv3 --pmc CSVs: per directory, the mean counter values of the scan kernel's dispatches
-(the last dispatch of each counter set; scan_tiles only)."""
+(the last dispatch of each counter set; scan_tiles / scan_lean)."""
 import csv, glob, os, sys
 from collections import defaultdict
 
@@ -11,7 +11,7 @@ for d in sorted(glob.glob(os.path.join(root, "pmc*"))):
     vals = defaultdict(list)
     for f in files:
         for row in csv.DictReader(open(f)):
-            if "scan_tiles" not in row["Kernel_Name"]:
+            if "scan_tiles" not in row["Kernel_Name"] and "scan_lean" not in row["Kernel_Name"]:
                 continue
             vals[row["Counter_Name"]].append(float(row["Counter_Value"]))
     if not vals:
