@@ -50,6 +50,10 @@ QUERIES = {
                         "q2": {"k": "resource.service.name", "v": [], "op": "exists"}},
                 agg="count", group_bys=[], tag="resource.service.name",
                 desc="tag query resource.service.name where :eq _cardinalhq.name=metric_07, COUNT(*)"),
+    # exemplar raw scan (§8(f) f4) on C2 data: per glob the newest 1000 rows of metric_07 (ORDER BY ts DESC LIMIT 1000)
+    "exemplar": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                             "computed": False, "dataType": "string"}, agg=None, group_bys=[], exemplar=1000,
+                     desc="exemplar :eq _cardinalhq.name=metric_07, ORDER BY ts DESC LIMIT 1000 per glob"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
@@ -133,7 +137,11 @@ def main():
         f"{eng.segment_bytes / 1e9:.1f} GB, load {time.time() - t0:.0f}s")
 
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(total)]
-    req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag")))
+    if q.get("exemplar"):
+        req = json.dumps({"baseExpr": {"id": "A", "dataset": "logs", "filter": q["filter"], "limit": q["exemplar"]},
+                          "segmentRequests": segs})
+    else:
+        req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag")))
 
     def step(extra=0):
         if world > 1:
@@ -161,13 +169,13 @@ def main():
         res = step()
         scan_ms.append(res.stats["scan_ms"])
         total_ms.append(res.stats["total_ms"])
-        plan_ms.append(res.stats["plan_ms"])
-        device_ms.append(res.stats["device_ms"])
+        plan_ms.append(res.stats.get("plan_ms", 0.0))
+        device_ms.append(res.stats.get("device_ms", 0.0))
         launch_ms.append(res.stats.get("launch_ms", 0.0))
         sync_ms.append(res.stats.get("sync_ms", 0.0))
         alloc_ms.append(res.stats.get("alloc_ms", 0.0))
         copy_ms.append(res.stats.get("copy_ms", 0.0))
-        alg_bytes = res.stats["algorithmic_bytes"]
+        alg_bytes = res.stats.get("algorithmic_bytes", 0)
         out_rows = len(res)
     torch.cuda.synchronize()
     if world > 1:
@@ -210,7 +218,7 @@ def main():
         del a, b
 
     cpu, validated = None, None
-    if keep_cpu and not q.get("tag"):
+    if keep_cpu and not q.get("tag") and not q.get("exemplar"):
         cpu, validated = cpu_baseline_and_validate(args, q, req, [kept[i] for i in mine], res)
     for sgm in kept.values():
         sgm.free()

@@ -174,6 +174,8 @@ struct XGlob {
   std::map<std::string, int> types;       // union type per column
   // selection state
   bool open = false;
+  std::vector<int64_t> probes;            // ordered-end-first ranges to try before the whole window (zone maps)
+  size_t probe = 0;
   int64_t hlo = 0, hhi = 0;               // range still being narrowed
   uint64_t need = 0, above = 0;           // rows still wanted from [hlo, hhi); rows certainly in beyond it
   int64_t elo = 0, ehi = 0;               // final emit range
@@ -474,11 +476,50 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     g.elo = g.win_lo;
     g.ehi = g.win_hi;
   }
+  // Ordered end first: segments are written in time order, so the newest (DESC) rows sit in a few tiles.  From the
+  // zone maps, candidate boundaries covering the last 2^20, 2^23, ... rows of the glob; a HIST pass over
+  // [boundary, window end) that already counts `limit` passing rows holds the whole top `limit` (every row before
+  // the boundary is older than all of them); otherwise the next, wider boundary is tried.
+  {
+    std::vector<std::vector<std::pair<int64_t, int64_t>>> tl(ng);   // (ordered key, other end)
+    std::vector<std::vector<uint32_t>> tr(ng);
+    for (size_t q = 0; q < qsegs.size(); q++) {
+      const XGlob& g = globs[qseg_glob[q]];
+      for (const TileDesc& td : qseg_seg[q]->tiles) {
+        if (td.ts_max < g.win_lo || td.ts_min >= g.win_hi) continue;
+        tl[qseg_glob[q]].emplace_back(desc ? -td.ts_max : td.ts_min, desc ? td.ts_min : td.ts_max);
+        tr[qseg_glob[q]].push_back(td.nrows);
+      }
+    }
+    for (size_t gi = 0; gi < ng; gi++) {
+      XGlob& g = globs[gi];
+      if (!g.open) continue;
+      std::vector<size_t> ord(tl[gi].size());
+      for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](size_t a, size_t b) { return tl[gi][a].first < tl[gi][b].first; });
+      uint64_t rows = 0, goal = getenv("LK_EX_PROBE_ROWS") ? std::max<uint64_t>(1, strtoull(getenv("LK_EX_PROBE_ROWS"), nullptr, 10))
+                                                         : (uint64_t(1) << 20);   // env: tests only
+      int64_t edge = desc ? INT64_MAX : INT64_MIN;
+      for (size_t i : ord) {
+        rows += tr[gi][i];
+        edge = desc ? std::min(edge, tl[gi][i].second) : std::max(edge, tl[gi][i].second + 1);
+        if (rows >= goal) {
+          const int64_t b = desc ? std::max(edge, g.win_lo) : std::min(edge, g.win_hi);
+          if ((desc && b > g.win_lo) || (!desc && b < g.win_hi)) g.probes.push_back(b);
+          goal *= 8;
+        }
+      }
+    }
+  }
   bool first_upload = true;
   while (std::any_of(globs.begin(), globs.end(), [](const XGlob& g) { return g.open; })) {
     std::vector<uint32_t> nb(ng, 0);
     for (size_t gi = 0; gi < ng; gi++) {
       XGlob& g = globs[gi];
+      if (g.open && g.probe < g.probes.size()) {   // probing: [boundary, end) (DESC) / [start, boundary) (ASC)
+        g.hlo = desc ? g.probes[g.probe] : g.win_lo;
+        g.hhi = desc ? g.win_hi : g.probes[g.probe];
+      }
       const int64_t span = g.open ? g.hhi - g.hlo : 0;
       const int64_t w = span > 0 ? (span + XBINS - 1) / XBINS : 1;
       hr[gi] = g.open ? g.hlo : 0;
@@ -509,6 +550,18 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       if (!g.open) continue;
       const uint32_t* h = hh + gi * XBINS;
       const int64_t w = hr[3 * ng + gi];
+      if (g.probe < g.probes.size()) {
+        uint64_t tot = 0;
+        for (uint32_t k = 0; k < nb[gi]; k++) tot += h[k];
+        if (tot < g.need) {   // not enough rows past this boundary: a wider one, or the whole window
+          if (++g.probe >= g.probes.size()) {
+            g.hlo = g.win_lo;
+            g.hhi = g.win_hi;
+          }
+          continue;
+        }
+        g.probe = g.probes.size();   // the top `limit` lies in the probed range: narrow it as usual
+      }
       uint64_t cum = 0;
       int64_t split = -1;
       for (uint32_t k = 0; k < nb[gi]; k++) {

@@ -108,13 +108,26 @@ def test_exemplar_shapes(engine, tmp_path):
          {"limit": 100_000}, 4),
         ("contains_unicode", synth.leaf("_cardinalhq.message", "contains", "MSG 1"), {"limit": 333}, 1),
     ]
-    for label, filt, kw, gs in cases:
-        req = _request(filt, len(paths), limit=kw.get("limit"), order=kw.get("order"), reverse=kw.get("reverse", False))
-        got = _check(engine, req, paths, blobs, gs, label)
-        if label == "everything":
-            assert len(got) > 40_000                       # all passing rows of every glob
-        if label == "default":
-            assert len(got) > 1000 and {"attr.flag", "attr.ratio", "attr.count", "attr.big"} <= set(got.tag_names)
+    # second round: zone-map probing from the ordered end (LK_EX_PROBE_ROWS, tests only: probe boundaries every few
+    # thousand rows instead of 2^20, so these small globs go through it)
+    for probe in (None, "3000"):
+        if probe:
+            os.environ["LK_EX_PROBE_ROWS"] = probe
+        try:
+            for label, filt, kw, gs in cases:
+                req = _request(filt, len(paths), limit=kw.get("limit"), order=kw.get("order"),
+                               reverse=kw.get("reverse", False))
+                got = _check(engine, req, paths, blobs, gs, f"{label} probe={probe}")
+                _shape_asserts(label, got)
+        finally:
+            os.environ.pop("LK_EX_PROBE_ROWS", None)
+
+
+def _shape_asserts(label, got):
+    if label == "everything":
+        assert len(got) > 40_000                       # all passing rows of every glob
+    if label == "default":
+        assert len(got) > 1000 and {"attr.flag", "attr.ratio", "attr.count", "attr.big"} <= set(got.tag_names)
 
 
 def test_exemplar_refinement_and_ties(engine, tmp_path):

@@ -304,6 +304,7 @@ extern "C" int lk_synth_segment(const lk_synth_spec* spec, uint8_t** out, size_t
     cols.push_back(c);
   }
   if (sp.highcard_n) cols.push_back({"resource.container.id", DICT, sp.highcard_n, {}});
+  dict_col("_cardinalhq.message", 64, "request %02u handled");   // logs projection column (exemplar rows)
 
   const uint64_t rgr = sp.rg_rows ? sp.rg_rows : (1u << 20);
   const uint64_t nrg = (sp.rows + rgr - 1) / rgr;
