@@ -223,6 +223,29 @@ void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n) {
   }
 }
 
+void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n) {
+  Comm& C = need_comm(E);
+  if (C.world == 1) {
+    if (code) throw PlanError(code, msg);
+    return;
+  }
+  // blob: status (4 B) | n bytes | message
+  std::string mine(4 + n, '\0');
+  memcpy(&mine[0], &code, 4);
+  memcpy(&mine[4], host, n);
+  if (code) mine += msg;
+  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
+  for (int r = 0; r < C.world; r++) {
+    const std::string& b = all[size_t(r)];
+    if (b.size() < 4 + n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
+    int c;
+    memcpy(&c, b.data(), 4);
+    if (c) throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(4 + n));
+  }
+  for (auto& b : all)
+    for (size_t i = 0; i < n; i++) host[i] = std::max(host[i], uint8_t(b[4 + i]));
+}
+
 std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) {
   return need_comm(E).allgather_bytes(E, X, mine);
 }

@@ -20,6 +20,8 @@ std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::
 // Every rank reports its local status (0 = ok); if any rank failed, every rank throws the first failure
 // (PlanError with that rank's code), so no rank is left waiting in a later collective.
 void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg);
+// comm_agree and comm_allreduce_max_u8 in one all-gather (status, then the byte array).
+void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n);
 // Dense mode: reduce the partial aggregation table (P.rows/cnt/hi/lo/ext, nc cells) onto rank 0: counts by
 // sum, min/max by min/max on order-preserving bits (exact), compensated sums gathered and added in rank order.
 void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc);

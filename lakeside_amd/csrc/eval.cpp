@@ -390,9 +390,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   if (dist)
     for (size_t i = 0; i < n_paths; i++) mine[i] = (shard ? shard[i] : int32_t(i % size_t(world))) == rank;
   std::vector<std::shared_ptr<Segment>> segs(n_paths);
+  int load_err = 0;
+  std::string load_msg;
   {
     // A rank-local failure (I/O, Parquet, HBM) must not leave the other ranks waiting in the next collective:
-    // the ranks agree on a status first and fail together.
+    // the ranks agree on a status first and fail together (folded into the glob-union exchange below: one
+    // all-gather carries both).
     int err = 0;
     std::string msg;
     try {
@@ -407,7 +410,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       err = LK_ERR_IO;
       msg = e.what();
     }
-    if (dist) comm_agree(E, *X, err, msg);
+    load_err = err;
+    load_msg = msg;
   }
 
   // ---- globs ----
@@ -435,7 +439,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
       if (vc < 0 || segs[si]->cols[vc].any_nulls) exists.back() = 1;
     }
-  if (dist) comm_allreduce_max_u8(E, *X, exists.data(), exists.size());   // every rank sees every glob's union
+  // every rank sees every glob's union; a rank-local load failure fails every rank here
+  if (dist) comm_agree_max_u8(E, *X, load_err, load_msg, exists.data(), exists.size());
   const bool value_nulls = exists.back() != 0;
   auto glob_has = [&](size_t gi, const std::string& c) {
     size_t k = size_t(std::find(probe_cols.begin(), probe_cols.end(), c) - probe_cols.begin());

