@@ -211,7 +211,7 @@ struct lk_result {
   int64_t* ts = nullptr;                         // columns carved out of one pinned host block (pinned_acquire):
   double* val = nullptr;                         //   device-to-host copies run at full link rate and a freed
   uint32_t* glob = nullptr;                      //   result hands the block to the next one
-  unsigned long long* gid = nullptr;             // group id: Σ dim id × stride over the group dims
+  uint32_t* gid = nullptr;                       // group id: Σ dim id × stride over the group dims (< 2^32)
   lk::HostBlock blk;
   std::vector<std::string> tag_names;            // "name", groupBys, then queryTags keys
   struct TagCol {                                // a "name" / groupBy tag column
@@ -238,16 +238,16 @@ struct lk_result {
   lk_result& operator=(const lk_result&) = delete;
   ~lk_result() { lk::pinned_release(blk); }
   // with_glob = false (merged rows: every glob index is 0): the glob column is a shared read-only block of
-  // zeros, so the device writes 24 instead of 28 bytes per row over the host link.
+  // zeros, so the device writes 20 instead of 24 bytes per row over the host link.
   void alloc_rows(size_t n, bool with_glob = true) {
-    blk = lk::pinned_acquire(n * (with_glob ? 28 : 24) + 64);
+    blk = lk::pinned_acquire(n * (with_glob ? 24 : 20) + 64);
     nrows = n;
     auto* b = static_cast<uint8_t*>(blk.p);
     ts = reinterpret_cast<int64_t*>(b);
     val = reinterpret_cast<double*>(b + n * 8);
-    gid = reinterpret_cast<unsigned long long*>(b + n * 16);
+    gid = reinterpret_cast<uint32_t*>(b + n * 16);
     if (with_glob) {
-      glob = reinterpret_cast<uint32_t*>(b + n * 24);
+      glob = reinterpret_cast<uint32_t*>(b + n * 20);
     } else {
       zeros = lk::zero_block(n * 4);
       glob = static_cast<uint32_t*>(zeros.get());

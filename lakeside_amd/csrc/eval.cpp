@@ -1165,18 +1165,19 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         }
       }
       if (total_rows >= (uint64_t(1) << 32)) throw PlanError(LK_ERR_UNSUPPORTED, "more than 2^32 result rows");
-      uint8_t* ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 24 + 64));
+      uint8_t* ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 20 + 64));
       if (mine_n)
         HIP_TRY(launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ob), reinterpret_cast<double*>(ob + size_t(mine_n) * 8),
-                                      reinterpret_cast<unsigned long long*>(ob + size_t(mine_n) * 16), nullptr, st));
+                                      reinterpret_cast<uint32_t*>(ob + size_t(mine_n) * 16), nullptr, st));
       HIP_TRY(hipStreamSynchronize(st));   // rows complete before they are sent
-      uint8_t* rb = rank == 0 ? static_cast<uint8_t*>(X->workspace("kr_rows_all", size_t(total_rows) * 24 + 64)) : nullptr;
-      std::vector<Piece> s2, r2;
-      for (int a = 0; a < 3; a++) s2.push_back(Piece{0, ob + size_t(a) * mine_n * 8, size_t(mine_n) * 8});
+      uint8_t* rb = rank == 0 ? static_cast<uint8_t*>(X->workspace("kr_rows_all", size_t(total_rows) * 20 + 64)) : nullptr;
+      std::vector<Piece> s2, r2;   // [ts 8 B | value 8 B | group id 4 B] per row, column by column
+      const size_t wcol[3] = {8, 8, 4};
+      for (int a = 0; a < 3; a++) s2.push_back(Piece{0, ob + size_t(a) * mine_n * 8, size_t(mine_n) * wcol[a]});
       if (rank == 0)
         for (int j = 0; j < W; j++)
           for (int a = 0; a < 3; a++)
-            r2.push_back(Piece{j, rb + (size_t(a) * total_rows + noff[size_t(j)]) * 8, size_t(ncnt[size_t(j)]) * 8});
+            r2.push_back(Piece{j, rb + size_t(a) * total_rows * 8 + noff[size_t(j)] * wcol[a], size_t(ncnt[size_t(j)]) * wcol[a]});
       comm_exchange(E, *X, s2, r2);
       if (rank == 0) {
         nrows_out = uint32_t(total_rows);
@@ -1184,7 +1185,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         if (nrows_out) {
           HIP_TRY(hipMemcpyAsync(res->ts, rb, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
           HIP_TRY(hipMemcpyAsync(res->val, rb + size_t(nrows_out) * 8, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-          HIP_TRY(hipMemcpyAsync(res->gid, rb + size_t(nrows_out) * 16, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+          HIP_TRY(hipMemcpyAsync(res->gid, rb + size_t(nrows_out) * 16, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
         }
         HIP_TRY(hipStreamSynchronize(st));
         rows_done = true;
@@ -1480,7 +1481,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       const SkRow& k = sk_rows[r];
       res->ts[r] = k.ts;
       res->val[r] = k.sk.quantile(quantile);
-      res->gid[r] = k.gid;
+      res->gid[r] = uint32_t(k.gid);
       if (per_glob_rows) res->glob[r] = k.glob;
       res->sketches.push_back(k.sk.serialize());
     }
@@ -1492,14 +1493,14 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     uint8_t* ob = static_cast<uint8_t*>(X->workspace("out", nk * (8 + 8 + 8 + 4) + 1024));
     int64_t* o_ts = direct ? res->ts : reinterpret_cast<int64_t*>(ob);
     double* o_val = direct ? res->val : reinterpret_cast<double*>(ob + nk * 8);
-    unsigned long long* o_gid = direct ? res->gid : reinterpret_cast<unsigned long long*>(ob + nk * 16);
+    uint32_t* o_gid = direct ? res->gid : reinterpret_cast<uint32_t*>(ob + nk * 16);
     uint32_t* o_glob = per_glob_rows ? (direct ? res->glob : reinterpret_cast<uint32_t*>(ob + nk * 24)) : nullptr;
     if (hash_mode) HIP_TRY(launch_sparse_write(S, nocc, sws, o_ts, o_val, o_gid, o_glob, st));
     else HIP_TRY(launch_finalize_write(F, d_counts, o_ts, o_val, o_gid, o_glob, st));
     if (!direct) {
       HIP_TRY(hipMemcpyAsync(res->ts, o_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->val, o_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
-      HIP_TRY(hipMemcpyAsync(res->gid, o_gid, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY(hipMemcpyAsync(res->gid, o_gid, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
       if (per_glob_rows) HIP_TRY(hipMemcpyAsync(res->glob, o_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
     }
     HIP_TRY(hipStreamSynchronize(st));

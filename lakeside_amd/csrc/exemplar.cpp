@@ -724,7 +724,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     const Segment& S = *qseg_seg[c.qseg];
     res->ts[i] = c.ts;
     res->glob[i] = qseg_glob[c.qseg];
-    res->gid[i] = i;
+    res->gid[i] = uint32_t(i);
     res->val[i] = 0.0;
     for (size_t k = 0; k < ncols; k++) {
       if (!gok[i * ncols + k]) continue;

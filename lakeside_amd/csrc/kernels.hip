@@ -168,7 +168,7 @@ __global__ __launch_bounds__(1024) void finalize_scan(uint32_t* counts, uint32_t
 }
 
 __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* block_offsets, int64_t* out_ts,
-                                                   double* out_val, unsigned long long* out_gid,
+                                                   double* out_val, uint32_t* out_gid,
                                                    uint32_t* out_glob) {
   __shared__ uint32_t ws[FB / 64];
   const unsigned long long base = (unsigned long long)blockIdx.x * FB * FITEMS;
@@ -192,7 +192,7 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
       unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
       out_ts[pos] = F.bucket_base + (int64_t)b * F.step;
       out_val[pos] = r.value;
-      out_gid[pos] = r.gid;
+      out_gid[pos] = uint32_t(r.gid);
       if (out_glob) out_glob[pos] = r.glob;   // null: merged rows (glob 0, a shared zero block on the host)
     }
     off += tot;
@@ -345,7 +345,7 @@ __global__ __launch_bounds__(SB) void runs_count(const unsigned long long* k, un
 // One row per run of equal output keys: the run's cells combined as make_row combines dense cells.
 __global__ __launch_bounds__(SB) void runs_write(SParams S, const unsigned long long* k, const uint32_t* slot,
                                                  unsigned long long n, const uint32_t* block_offsets, int64_t* out_ts,
-                                                 double* out_val, unsigned long long* out_gid, uint32_t* out_glob) {
+                                                 double* out_val, uint32_t* out_gid, uint32_t* out_glob) {
   __shared__ uint32_t ws[SB / 64];
   const unsigned long long base = (unsigned long long)blockIdx.x * SB * SITEMS;
   uint32_t off = block_offsets[blockIdx.x];
@@ -408,7 +408,7 @@ __global__ __launch_bounds__(SB) void runs_write(SParams S, const unsigned long 
       const uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
       out_ts[pos] = S.bucket_base + (int64_t)b * S.step;
       out_val[pos] = value;
-      out_gid[pos] = gid;
+      out_gid[pos] = uint32_t(gid);
       if (out_glob) out_glob[pos] = S.per_glob ? glob : 0u;
     }
     off += tot;
@@ -607,7 +607,7 @@ hipError_t launch_sparse_sort(const SParams& S, const uint32_t* d_counts, unsign
 }
 
 hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws, int64_t* ts, double* val,
-                               unsigned long long* gid, uint32_t* glob, hipStream_t st) {
+                               uint32_t* gid, uint32_t* glob, hipStream_t st) {
   if (n == 0) return hipSuccess;
   SparseWs w = carve(ws, n, 64);
   hipLaunchKernelGGL(runs_write, dim3(sparse_blocks(n)), dim3(SB), 0, st, S, w.k1, w.s1, n, w.counts, ts, val, gid, glob);
@@ -640,14 +640,14 @@ hipError_t launch_finalize_count(const FParams& F, uint32_t* d_counts, hipStream
 }
 
 hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int64_t* ts, double* val,
-                                 unsigned long long* gid, uint32_t* glob, hipStream_t stream) {
+                                 uint32_t* gid, uint32_t* glob, hipStream_t stream) {
   uint32_t nb = finalize_blocks(F.nkeys);
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_write, dim3(nb), dim3(FB), 0, stream, F, d_counts, ts, val, gid, glob);
   return hipGetLastError();
 }
 
-hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
+hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, uint32_t* gid,
                            uint32_t* glob, hipStream_t stream) {
   hipError_t e = launch_finalize_count(F, d_counts, stream);
   if (e != hipSuccess) return e;

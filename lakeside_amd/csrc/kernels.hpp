@@ -105,7 +105,7 @@ hipError_t launch_sparse_count(const SParams& S, uint32_t* d_counts, hipStream_t
 hipError_t launch_sparse_sort(const SParams& S, const uint32_t* d_counts, unsigned long long n, int end_bit, void* ws,
                               uint32_t** d_nrows, hipStream_t stream);
 hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws, int64_t* ts, double* val,
-                               unsigned long long* gid, uint32_t* glob, hipStream_t stream);
+                               uint32_t* gid, uint32_t* glob, hipStream_t stream);
 
 // Exemplar scans (ex_kernels.hip).  ex_scan decodes the filter columns (QSeg cols 0 = timestamp, 2.. = strings) of
 // every tile meeting its glob's open range [rlo, rhi) and either counts passing rows per time bin (HIST) or appends
@@ -186,8 +186,8 @@ uint32_t finalize_blocks(unsigned long long nkeys);
 // memory (hipHostMalloc) directly, so no device->host copy follows.
 hipError_t launch_finalize_count(const FParams& F, uint32_t* d_counts, hipStream_t stream);
 hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int64_t* ts, double* val,
-                                 unsigned long long* gid, uint32_t* glob, hipStream_t stream);
-hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, unsigned long long* gid,
+                                 uint32_t* gid, uint32_t* glob, hipStream_t stream);
+hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, uint32_t* gid,
                            uint32_t* glob, hipStream_t stream);
 
 }  // namespace lk
