@@ -47,6 +47,12 @@ namespace lk {
 struct Comm {
   int world = 1;
   int rank = 0;
+  // Loopback (RCCL only, env LK_COMM_LOOPBACK=1 at lk_comm_init; tests): at world 1 every collective still runs --
+  // all-gathers through ncclAllGather, the table / record gathers and the key-range pieces through grouped
+  // ncclSend/ncclRecv to self -- and the merge reads what came back through RCCL, so the single-GPU box executes
+  // (and checks) every RCCL data-path call the 8-GPU run makes.
+  bool loopback = false;
+  bool active() const { return world > 1 || loopback; }
   virtual ~Comm() = default;
   // host blobs of every rank, rank order
   virtual std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) = 0;
@@ -67,7 +73,7 @@ struct RcclComm final : Comm {
   }
 
   std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) override {
-    if (world == 1) return {mine};
+    if (!active()) return {mine};
     HIP_TRY2(hipSetDevice(E.device));
     hipStream_t st = X.stream;
     uint64_t* dsz = static_cast<uint64_t*>(X.workspace("comm_sizes", size_t(world) * 8));
@@ -93,25 +99,26 @@ struct RcclComm final : Comm {
 
   void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
                       const std::vector<size_t>& off) override {
-    if (world == 1) return;
-    // grouped point-to-point: every peer streams into rank 0 over its own xGMI link at once
+    if (!active()) return;
+    // grouped point-to-point: every peer streams into rank 0 over its own xGMI link at once (loopback: rank 0's own
+    // block too, into slot 0)
     NCCL_TRY(ncclGroupStart());
     if (rank == 0) {
-      for (int r = 1; r < world; r++)
+      for (int r = loopback ? 0 : 1; r < world; r++)
         if (bytes[size_t(r)])
           NCCL_TRY(ncclRecv(static_cast<uint8_t*>(recv) + off[size_t(r)], bytes[size_t(r)], ncclUint8, r, comm, X.stream));
-    } else if (bytes[size_t(rank)]) {
-      NCCL_TRY(ncclSend(send, bytes[size_t(rank)], ncclUint8, 0, comm, X.stream));
     }
+    if ((rank != 0 || loopback) && bytes[size_t(rank)]) NCCL_TRY(ncclSend(send, bytes[size_t(rank)], ncclUint8, 0, comm, X.stream));
     NCCL_TRY(ncclGroupEnd());
   }
 
   void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) override {
+    // loopback: own pieces go through RCCL as well (send / recv to self, matched in list order)
     NCCL_TRY(ncclGroupStart());
     for (const Piece& p : sends)
-      if (p.peer != rank && p.bytes) NCCL_TRY(ncclSend(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
+      if ((p.peer != rank || loopback) && p.bytes) NCCL_TRY(ncclSend(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
     for (const Piece& p : recvs)
-      if (p.peer != rank && p.bytes) NCCL_TRY(ncclRecv(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
+      if ((p.peer != rank || loopback) && p.bytes) NCCL_TRY(ncclRecv(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
     NCCL_TRY(ncclGroupEnd());
   }
 };
@@ -201,6 +208,7 @@ struct HostComm final : Comm {
 }  // namespace
 
 int comm_world(const Engine& E) { return E.comm ? E.comm->world : 1; }
+bool comm_loopback(const Engine& E) { return E.comm && E.comm->loopback; }
 int comm_rank(const Engine& E) { return E.comm ? E.comm->rank : 0; }
 
 void Engine::comm_destroy() {
@@ -215,7 +223,7 @@ static Comm& need_comm(Engine& E) {
 
 void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n) {
   Comm& C = need_comm(E);
-  if (C.world == 1) return;
+  if (!C.active()) return;
   std::vector<std::string> all = C.allgather_bytes(E, X, std::string(reinterpret_cast<const char*>(host), n));
   for (auto& b : all) {
     if (b.size() != n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
@@ -225,7 +233,7 @@ void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n) {
 
 void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n) {
   Comm& C = need_comm(E);
-  if (C.world == 1) {
+  if (!C.active()) {
     if (code) throw PlanError(code, msg);
     return;
   }
@@ -258,7 +266,7 @@ void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg) {
     memcpy(&mine[0], &code, 4);
     mine += msg;
   }
-  if (C.world == 1) {
+  if (!C.active()) {
     if (code) throw PlanError(code, msg);
     return;
   }
@@ -284,22 +292,27 @@ void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const
   if (os.size() != orv.size()) throw PlanError(LK_ERR_DEVICE, "internal: own exchange pieces do not pair up");
   for (size_t i = 0; i < os.size(); i++) {
     if (os[i]->bytes != orv[i]->bytes) throw PlanError(LK_ERR_DEVICE, "internal: own exchange piece sizes differ");
-    if (os[i]->bytes) HIP_TRY2(hipMemcpyAsync(orv[i]->ptr, os[i]->ptr, os[i]->bytes, hipMemcpyDeviceToDevice, X.stream));
+    if (os[i]->bytes && !C.loopback)
+      HIP_TRY2(hipMemcpyAsync(orv[i]->ptr, os[i]->ptr, os[i]->bytes, hipMemcpyDeviceToDevice, X.stream));
   }
-  if (C.world > 1) C.exchange(E, X, sends, recvs);
+  if (C.active()) C.exchange(E, X, sends, recvs);
 }
 
 void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc) {
   Comm& C = need_comm(E);
-  if (C.world == 1) return;
+  if (!C.active()) return;
   // the table is one contiguous block [rows | cnt | hi | lo | ext] (eval.cpp)
   const size_t bytes = nc * 8 * 5;
   unsigned long long* parts =
       C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_parts", size_t(C.world) * bytes)) : nullptr;
   std::vector<size_t> sz(size_t(C.world), bytes), off(size_t(C.world));
   for (int r = 0; r < C.world; r++) off[size_t(r)] = size_t(r) * bytes;
+  // loopback: rank 0's own table makes the round trip into slot 0 (poisoned first, so a transfer that did not
+  // happen cannot pass), and the table is rebuilt from what arrived
+  if (C.loopback && C.rank == 0) HIP_TRY2(hipMemsetAsync(parts, 0xA5, bytes, X.stream));
   C.gather_to_root(E, X, P.rows, parts, sz, off);
   if (C.rank == 0) {
+    if (C.loopback) HIP_TRY2(hipMemcpyAsync(P.rows, parts, bytes, hipMemcpyDeviceToDevice, X.stream));
     TableRef T{P.rows, P.cnt, P.hi, P.lo, P.ext};
     HIP_TRY2(launch_merge_tables(T, parts, C.world, nc, agg, X.stream));
   }
@@ -307,7 +320,7 @@ void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t 
 
 void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long long& cap) {
   Comm& C = need_comm(E);
-  if (C.world == 1) return;
+  if (!C.active()) return;
   // this rank's occupied slots -> compact records [key | rows | cnt | hi | lo | ext]
   SParams S{};
   S.keys = P.hkeys;
@@ -342,6 +355,7 @@ void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long 
   }
   unsigned long long* parts =
       C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_rec_parts", total + 64)) : nullptr;
+  if (C.loopback && C.rank == 0 && sz[0]) HIP_TRY2(hipMemsetAsync(parts, 0xA5, sz[0], X.stream));
   HIP_TRY2(hipStreamSynchronize(X.stream));   // records complete before they are sent
   C.gather_to_root(E, X, recs, parts, sz, off);
   if (C.rank != 0) return;
@@ -359,7 +373,8 @@ void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long 
   HIP_TRY2(hipMemsetAsync(tb, 0, size_t(cap0) * 32, X.stream));
   HIP_TRY2(hipMemsetAsync(P.ext, agg == AGG_MIN ? 0xff : 0, size_t(cap0) * 8, X.stream));
   HIP_TRY2(hipMemsetAsync(P.hkeys, 0xff, size_t(cap0) * 8, X.stream));
-  HIP_TRY2(launch_merge_records(P, recs, n, agg, X.stream));
+  // rank 0's own records: as gathered through RCCL in loopback mode, else the local copy
+  HIP_TRY2(launch_merge_records(P, C.loopback ? parts : recs, n, agg, X.stream));
   for (int r = 1; r < C.world; r++)
     HIP_TRY2(launch_merge_records(P, parts + off[size_t(r)] / 8, sz[size_t(r)] / 48, agg, X.stream));
   cap = cap0;
@@ -395,6 +410,8 @@ int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
   auto* C = new lk::RcclComm();
   C->world = world;
   C->rank = rank;
+  const char* lb = getenv("LK_COMM_LOOPBACK");
+  C->loopback = world == 1 && lb && *lb == '1';
   ncclResult_t r = ncclCommInitRank(&C->comm, world, u, rank);
   if (r != ncclSuccess) {
     lk::set_error(std::string("RCCL: ncclCommInitRank: ") + ncclGetErrorString(r));

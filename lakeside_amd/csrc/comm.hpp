@@ -12,6 +12,8 @@ namespace lk {
 
 int comm_world(const Engine& E);
 int comm_rank(const Engine& E);
+// RCCL loopback test mode at world 1 (LK_COMM_LOOPBACK=1): collectives and point-to-point transfers run anyway.
+bool comm_loopback(const Engine& E);
 // Element-wise max of a small host byte array across ranks (glob column unions, null flags).
 void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n);
 // Concatenation, in rank order, of every rank's byte blob (variable length): one all-gather of the sizes,

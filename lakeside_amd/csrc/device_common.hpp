@@ -113,6 +113,21 @@ __device__ __forceinline__ void acc_reset(Acc& a, unsigned long long key) {
   a.ext = (AGG == AGG_MIN) ? ~0ull : 0ull;
 }
 
+// DDSketch bin of a value (sketches-java 0.8.2 LogarithmicMapping.index + DDSketch.accept): |v| <= dd_min -> the
+// zero bin; index = (int) (ln|v| * multiplier), minus one when negative (LogLikeIndexMapping.index's floor);
+// NaN / |v| > dd_max is untrackable (accept throws): FLAG_SKETCH_RANGE.
+__device__ __forceinline__ uint32_t dd_bin(const QParams& P, double v) {
+  const double a = fabs(v);
+  if (!(a <= P.dd_max)) {
+    atomicOr(P.flags, FLAG_SKETCH_RANGE);
+    return 0u;
+  }
+  if (a <= P.dd_min) return 0u;
+  const double x = log(a) * P.dd_mult;
+  const int32_t i = x >= 0.0 ? int32_t(x) : int32_t(x) - 1;
+  return uint32_t(1 + DD_BIAS + i) + (v < 0.0 ? DD_HALF : 0u);
+}
+
 __device__ __forceinline__ unsigned long long mix64(unsigned long long x) {   // splitmix64 finalizer
   x ^= x >> 30;
   x *= 0xbf58476d1ce4e5b9ull;

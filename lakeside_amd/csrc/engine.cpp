@@ -46,8 +46,21 @@ struct DeviceError : std::runtime_error {
 #define HIP_CHECK(x)                                                                          \
   do {                                                                                        \
     hipError_t _e = (x);                                                                      \
-    if (_e != hipSuccess)                                                                     \
+    if (_e != hipSuccess) {                                                                   \
+      (void)hipGetLastError(); /* a failed allocation must not poison the next launch */      \
       throw DeviceError(std::string("HIP: ") + #x + ": " + hipGetErrorString(_e));            \
+    }                                                                                         \
+  } while (0)
+
+// Call-context failures (workspace sync / free) surface as PlanError(LK_ERR_DEVICE): the distributed paths agree
+// on PlanErrors before the next collective, so no rank is left waiting.
+#define CTX_CHECK(x)                                                                            \
+  do {                                                                                          \
+    hipError_t _e = (x);                                                                        \
+    if (_e != hipSuccess) {                                                                     \
+      (void)hipGetLastError();                                                                  \
+      throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
+    }                                                                                           \
   } while (0)
 
 static constexpr size_t kAlign = 256;
@@ -711,18 +724,38 @@ size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep) {
   return freed;
 }
 
+// build_segment with the file's own faults as LK_ERR_IO: a truncated / corrupt footer, page or run (thrift and
+// Parquet parse errors) is a property of that one file -- the evaluation empties only its glob, as DuckDB's failing
+// read_parquet does (Commons.scala:249-253) -- while HIP failures and host OOM stay what they are.
+static std::shared_ptr<Segment> build_checked(Engine& E, const std::string& key, const uint8_t* data, size_t size) {
+  try {
+    return E.build_segment(key, data, size);
+  } catch (const DeviceError&) {
+    throw;
+  } catch (const PlanError&) {
+    throw;
+  } catch (const std::bad_alloc&) {
+    throw;
+  } catch (const std::exception& e) {
+    throw PlanError(LK_ERR_IO, std::string(e.what()) + " (" + key + ")");
+  }
+}
+
 int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size) {
   std::shared_ptr<Segment> S;
   try {
-    S = build_segment(key, data, size);
+    S = build_checked(*this, key, data, size);
   } catch (const DeviceError&) {
-    // HBM exhausted: make room by evicting least recently used segments (about twice the file), then retry once
+    // HBM exhausted: make room by evicting least recently used segments (about twice the file), then retry once.
+    // The failed hipMalloc left HIP's thread-local last error set: clear it, or the next launch on this thread
+    // would report it.
+    (void)hipGetLastError();
     {
       std::lock_guard<std::mutex> g(cache_mu);
       const size_t want = 2 * size + (64u << 20);
       if (evict_lru_locked(cache_bytes > want ? cache_bytes - want : 0, key) == 0) throw;
     }
-    S = build_segment(key, data, size);
+    S = build_checked(*this, key, data, size);
   }
   S->last_use = ++use_clock;
   std::lock_guard<std::mutex> g(cache_mu);
@@ -840,13 +873,14 @@ CallCtx::~CallCtx() {
 void* CallCtx::workspace(const std::string& name, size_t bytes) {
   auto& w = ws[name];
   if (w.cap < bytes) {
+    const size_t old_cap = w.cap;   // growth is 1.5x of the old capacity, so a growing workspace reallocates rarely
     if (w.p) {
-      HIP_CHECK(hipStreamSynchronize(stream));   // earlier work of this call may still read it
-      HIP_CHECK(hipFree(w.p));
+      CTX_CHECK(hipStreamSynchronize(stream));   // earlier work of this call may still read it
+      CTX_CHECK(hipFree(w.p));
       w.p = nullptr;
       w.cap = 0;
     }
-    const size_t cap = align_up(std::max(bytes, w.cap * 3 / 2), 1 << 20);
+    const size_t cap = align_up(std::max(bytes, old_cap * 3 / 2), 1 << 20);
     hipError_t e = hipMalloc(&w.p, cap);
     if (e != hipSuccess) {
       (void)hipGetLastError();
@@ -860,11 +894,13 @@ void* CallCtx::workspace(const std::string& name, size_t bytes) {
 
 void* CallCtx::pinned_buf(size_t bytes) {
   if (pinned_cap < bytes) {
-    HIP_CHECK(hipStreamSynchronize(stream));
-    HIP_CHECK(hipHostFree(pinned));
+    CTX_CHECK(hipStreamSynchronize(stream));
+    CTX_CHECK(hipHostFree(pinned));
     pinned = nullptr;
-    pinned_cap = align_up(bytes, 1 << 20);
-    HIP_CHECK(hipHostMalloc(&pinned, pinned_cap));
+    pinned_cap = 0;
+    const size_t cap = align_up(bytes, 1 << 20);
+    CTX_CHECK(hipHostMalloc(&pinned, cap));
+    pinned_cap = cap;
   }
   return pinned;
 }

@@ -24,6 +24,7 @@
 #include "engine.hpp"
 #include "kernels.hpp"
 #include "layout.hpp"
+#include "parquet.hpp"
 #include "plan.hpp"
 #include "ddsketch.hpp"
 #include "hll.hpp"
@@ -89,6 +90,38 @@ void unpack_strings(const std::string& blob, std::vector<std::string>& out) {
     out.emplace_back(blob, o, len);
     o += len;
   }
+}
+
+// union_by_name over a glob's files unifies a numeric column to the widest of its physical types in DuckDB's order
+// INTEGER < BIGINT < FLOAT < DOUBLE (the same rule exemplar.cpp's union_type applies to tag text).  Rank 0: not a
+// numeric type a value column can have.
+int value_rank(int ptype) {
+  switch (ptype) {
+    case pq::INT32: return 1;
+    case pq::INT64: return 2;
+    case pq::FLOAT: return 3;
+    case pq::DOUBLE: return 4;
+    default: return 0;
+  }
+}
+std::string json_escape(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '"' || c == '\\') o += '\\';
+    if (static_cast<unsigned char>(c) < 0x20) {
+      char b[8];
+      snprintf(b, sizeof(b), "\\u%04x", unsigned(static_cast<unsigned char>(c)));
+      o += b;
+    } else {
+      o += c;
+    }
+  }
+  return o;
+}
+
+int value_type_of_rank(int r) {
+  static const int t[5] = {-1, pq::INT32, pq::INT64, pq::FLOAT, pq::DOUBLE};
+  return t[r < 0 || r > 4 ? 0 : r];
 }
 
 struct GlobInfo {
@@ -382,6 +415,18 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::vector<uint8_t> prog;
   postfix(R.filter.get(), leaves, prog);
   if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
+  // Regex leaves RE2 rejects (LK_ERR_ARG) fail the SQL only of the globs where the leaf's field exists (glob loop
+  // below); a pattern RE2 takes but this matcher does not (LK_ERR_UNSUPPORTED) fails the call.
+  std::vector<uint8_t> bad_regex(leaves.size(), 0);
+  for (auto& l : leaves)
+    if (l.node->op == "regex" || l.node->op == "contains") {
+      try {
+        (void)compile_leaf_regex(*l.node);
+      } catch (const PlanError& e) {
+        if (e.code != LK_ERR_ARG) throw;
+        bad_regex[size_t(l.index)] = 1;
+      }
+    }
 
   // ---- segments: which ones this process evaluates ----
   const int world = dist ? comm_world(E) : 1;
@@ -390,24 +435,37 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   if (dist)
     for (size_t i = 0; i < n_paths; i++) mine[i] = (shard ? shard[i] : int32_t(i % size_t(world))) == rank;
   std::vector<std::shared_ptr<Segment>> segs(n_paths);
+  // A segment the worker cannot read (missing file, corrupt Parquet, a file shape the loader does not take) fails
+  // its glob's DuckDB query, which Commons.toGlobResultSet turns into an empty result for that glob alone
+  // (Commons.scala:249-253, 338-340): such segments are marked here and empty their glob below.
+  std::vector<uint8_t> seg_bad(n_paths, 0);
+  std::string bad_msg;   // the first such failure (stats)
   int load_err = 0;
   std::string load_msg;
   {
-    // A rank-local failure (I/O, Parquet, HBM) must not leave the other ranks waiting in the next collective:
-    // the ranks agree on a status first and fail together (folded into the glob-union exchange below: one
-    // all-gather carries both).
+    // A rank-local failure of the engine itself (HIP, HBM, host memory) must not leave the other ranks waiting in the
+    // next collective: the ranks agree on a status first and fail together (folded into the glob-union exchange
+    // below: one all-gather carries both).
     int err = 0;
     std::string msg;
     try {
-      for (size_t i = 0; i < n_paths; i++)
-        if (mine[i]) segs[i] = E.get_segment(paths[i], true);
+      for (size_t i = 0; i < n_paths; i++) {
+        if (!mine[i]) continue;
+        try {
+          segs[i] = E.get_segment(paths[i], true);
+        } catch (const PlanError& e) {
+          if (e.code != LK_ERR_IO && e.code != LK_ERR_UNSUPPORTED) throw;
+          seg_bad[i] = 1;
+          if (bad_msg.empty()) bad_msg = e.what();
+        }
+      }
     } catch (const PlanError& e) {
       if (!dist) throw;
       err = e.code;
       msg = e.what();
     } catch (const std::exception& e) {
       if (!dist) throw;
-      err = LK_ERR_IO;
+      err = LK_ERR_DEVICE;
       msg = e.what();
     }
     load_err = err;
@@ -427,21 +485,56 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     for (size_t j = i; j < std::min(n_paths, i + size_t(glob_size)); j++) g.segs.push_back(int(j));
     globs.push_back(std::move(g));
   }
-  // union of columns per glob (over the probe columns), and "value column may be NULL"
+  // Per glob: the union of columns (over the probe columns), "this glob's query fails" (a segment that did not load,
+  // or a column whose type the query cannot use), the union_by_name type of the value column, and "value column may
+  // be NULL".  Layout: [globs x np exists | globs fail | globs value-type rank | value NULLs].
   const size_t np = probe_cols.size();
-  std::vector<uint8_t> exists(globs.size() * np + 1, 0);
-  for (size_t gi = 0; gi < globs.size(); gi++)
+  const size_t ng = globs.size();
+  std::vector<uint8_t> exists(ng * np + 2 * ng + 1, 0);
+  uint8_t* gfail = exists.data() + ng * np;
+  uint8_t* gvrank = gfail + ng;
+  for (size_t gi = 0; gi < ng; gi++)
     for (int si : globs[gi].segs) {
+      if (seg_bad[si]) gfail[gi] = 1;
       if (!segs[si]) continue;
+      const Segment& S = *segs[si];
       for (size_t k = 0; k < np; k++)
-        if (segs[si]->all_columns.count(probe_cols[k])) exists[gi * np + k] = 1;
-      int vc = segs[si]->col_index(vcol);
+        if (S.all_columns.count(probe_cols[k])) exists[gi * np + k] = 1;
+      int vc = S.col_index(vcol);
       // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
-      if (vc < 0 || segs[si]->cols[vc].any_nulls) exists.back() = 1;
+      if (vc < 0 || S.cols[vc].any_nulls) exists.back() = 1;
+      // Column types per role.  read_parquet(union_by_name=True) (Commons.scala:213) unifies each column's type
+      // over the glob's files; a column the query cannot bind (the value column as text, a string filter /
+      // groupBy column stored as a number, a numeric comparison on text, INT96 / FIXED_LEN_BYTE_ARRAY, which the
+      // engine does not load) makes DuckDB fail the glob's SQL -> that glob is empty (Commons.scala:249-253).
+      auto bad = [&](const std::string& name, int role) -> bool {
+        if (!S.all_columns.count(name)) return false;   // absent: nonExistentFields / NULL, not an error
+        const int c = S.col_index(name);
+        if (c < 0) return true;
+        const HostCol& hc = S.cols[size_t(c)];
+        if (role == 0) return hc.ptype != pq::INT64 && hc.ptype != pq::INT32;   // BIGINT over INT32 / INT64 files
+        if (role == 2) return !hc.is_string;
+        return value_rank(hc.ptype) == 0;   // value column / numeric comparison column
+      };
+      if (bad(kTimestamp, 0)) gfail[gi] = 1;
+      if (!tagq) {
+        if (bad(vcol, 1)) gfail[gi] = 1;
+        else if (vc >= 0) gvrank[gi] = std::max<uint8_t>(gvrank[gi], uint8_t(value_rank(S.cols[size_t(vc)].ptype)));
+      }
+      for (auto& sc : strs)
+        if (bad(sc.name, 2)) gfail[gi] = 1;
+      for (auto& nm : nums)
+        if (bad(nm, 3)) gfail[gi] = 1;
     }
-  // every rank sees every glob's union; a rank-local load failure fails every rank here
+  // every rank sees every glob's union, failures and value type; a rank-local engine failure fails every rank here
   if (dist) comm_agree_max_u8(E, *X, load_err, load_msg, exists.data(), exists.size());
   const bool value_nulls = exists.back() != 0;
+  size_t nfailed = 0;
+  for (size_t gi = 0; gi < ng; gi++)
+    if (gfail[gi]) {
+      globs[gi].skip = true;
+      nfailed++;
+    }
   auto glob_has = [&](size_t gi, const std::string& c) {
     size_t k = size_t(std::find(probe_cols.begin(), probe_cols.end(), c) - probe_cols.begin());
     return exists[gi * np + k] != 0;
@@ -474,12 +567,11 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (!nonexist.count(l.node->k) && !glob_has(gi, l.node->k)) g.skip = true;
     for (auto& k : bad_literal)   // normalizedValue failed for a field this glob has
       if (!nonexist.count(k)) g.skip = true;
-    // `<string column> > 1.5`: DuckDB cannot compare VARCHAR with a number (Binder Error) -> empty glob
-    for (auto& nm : nums)
-      for (int si : g.segs)
-        if (segs[si])
-          for (auto& [cname, pt] : segs[si]->schema)
-            if (cname == nm && pt == 6) g.skip = true;
+    // a regex leaf RE2 rejects fails the SQL of every glob where its field exists (where it does not, the leaf is
+    // the literal `false` and the pattern is never compiled, BaseExpr.scala:462-464)
+    for (auto& l : leaves)
+      if (bad_regex[size_t(l.index)] && !nonexist.count(l.node->k)) g.skip = true;
+    // (`<string column> > 1.5`, a Binder Error -> empty glob, is among the column-type failures above)
     if (tagq) continue;
     if (g.step <= 0) throw PlanError(LK_ERR_ARG, "stepInMillis must be positive");
     if (step < 0) step = g.step;
@@ -591,8 +683,13 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       }
       std::vector<std::unique_ptr<re::Regex>> res(sc.leaves.size());
       std::vector<std::unique_ptr<std::unordered_set<std::string>>> sets(sc.leaves.size());
+      std::vector<char> skip_leaf(sc.leaves.size(), 0);   // a rejected pattern: every glob it could run in is empty
       for (size_t j = 0; j < sc.leaves.size(); j++) {
         const FilterNode* l = sc.leaves[j];
+        if (bad_regex[sc.lbase + j]) {
+          skip_leaf[j] = 1;
+          continue;
+        }
         if (l->op == "regex" || l->op == "contains") res[j] = std::make_unique<re::Regex>(compile_leaf_regex(*l));
         if ((l->op == "in" || l->op == "not_in") && l->v.size() > 8)
           sets[j] = std::make_unique<std::unordered_set<std::string>>(l->v.begin(), l->v.end());
@@ -604,7 +701,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         const std::string& v = gd.vals[gid];
         uint8_t bits = 0;
         for (size_t j = 0; j < sc.leaves.size(); j++)
-          if (leaf_eval(*sc.leaves[j], v, res[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
+          if (!skip_leaf[j] && leaf_eval(*sc.leaves[j], v, res[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
         lb->hit.push_back(bits);
       }
     }
@@ -669,17 +766,22 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
 
   // ---- per-segment query descriptors ----
-  std::vector<QSeg> qsegs;
+  // `qsegs` go to the fused kernels (scan_lean / scan_tiles: INT64 timestamps, DOUBLE values); `gsegs` to the general
+  // row scan (ex_scan AGG mode): every segment of a numeric-leaf query, and segments whose timestamp or value column
+  // needs union_by_name promotion (INT32 timestamps; INT32 / INT64 / FLOAT values, cast through FLOAT where the glob's
+  // value type is FLOAT).  Both kinds aggregate into the same table.
+  std::vector<QSeg> qsegs, gsegs;
   std::vector<uint32_t> seg_begin;
   uint32_t total_tiles = 0;
   uint64_t rows_scanned = 0, alg_bytes = 0;
-  bool all_lean = true;       // every scanned tile is scan_lean's (the general kernel need not run)
+  bool all_lean = true;       // every fused-kernel tile is scan_lean's (the general kernel need not run)
   int local_err = 0;          // distributed: a rank-local failure, agreed on with the other ranks after the scan
   std::string local_msg;
   try {
   for (size_t gi = 0; gi < globs.size() && nbuckets; gi++) {
     const GlobInfo& g = globs[gi];
     if (g.skip) continue;
+    const int vunion = value_type_of_rank(gvrank[gi]);   // the glob's union_by_name value type (-1: no value column)
     for (int si : g.segs) {
       if (!segs[si]) continue;
       const Segment& S = *segs[si];
@@ -692,21 +794,27 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       q.leaf_false = g.leaf_false;
       q.win_lo = g.win_lo;
       q.win_hi = g.win_hi;
+      bool general = numeric;
+      // (column types were checked per glob above: a type the query cannot bind emptied the glob)
       auto bind = [&](int qc, const std::string& name, bool want_string) {
         int c = S.col_index(name);
         if (c < 0) {
           if (S.all_columns.count(name))
-            throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has a physical type the kernels do not decode");
+            throw PlanError(LK_ERR_DEVICE, "internal: column " + name + " of an unloaded type in a live glob");
           return;
         }
         const HostCol& hc = S.cols[c];
         if (want_string != hc.is_string)
-          throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
-        if (qc == 0 && hc.ptype != 2) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
-        if (qc == 1 && hc.ptype != 5) throw PlanError(LK_ERR_UNSUPPORTED, "value column must be DOUBLE");
-        if (qc >= 2 + int(strs.size()) && hc.ptype != 1 && hc.ptype != 2 && hc.ptype != 4 && hc.ptype != 5)
-          throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison on column " + name + " of an undecoded type");
-        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, uint32_t(hc.ptype)};
+          throw PlanError(LK_ERR_DEVICE, "internal: column " + name + " of an unexpected type in a live glob");
+        uint32_t pad = uint32_t(hc.ptype);
+        if (qc == 0 && hc.ptype != pq::INT64) general = true;   // INT32 timestamps: sign-extended
+        if (qc == 1) {
+          if (hc.ptype != pq::DOUBLE) general = true;
+          // an integer value column in a glob whose value type is FLOAT is cast to FLOAT first (DuckDB's implicit
+          // BIGINT -> FLOAT of the union column), then aggregated as a float
+          if (vunion == pq::FLOAT && hc.ptype != pq::FLOAT) pad |= VCONV_VIA_FLOAT;
+        }
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, pad};
         alg_bytes += hc.compressed_bytes;
       };
       bind(0, kTimestamp, false);
@@ -714,6 +822,13 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
       for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
       for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
+      if (general) {
+        q.tile_begin = total_tiles;
+        seg_begin.push_back(total_tiles);
+        total_tiles += q.ntiles;
+        gsegs.push_back(q);
+        continue;
+      }
       // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
       // name page has a small dictionary (lean_tile's test at page granularity)
       if (all_lean) {
@@ -746,10 +861,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     local_err = e.code;
     local_msg = e.what();
     qsegs.clear();
+    gsegs.clear();
     total_tiles = 0;
   }
-  uint32_t max_tiles = 0;
+  uint32_t max_tiles = 0, gmax_tiles = 0;
   for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
+  for (auto& q : gsegs) gmax_tiles = std::max(gmax_tiles, q.ntiles);
   // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
   std::vector<uint32_t> truth, truth_early, truth_late;
   uint32_t late_mask = 0;
@@ -865,6 +982,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   size_t off = 0;
   auto reserve = [&](size_t n) { size_t o = (off + 255) / 256 * 256; off = o + n; return o; };
   const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
+  const size_t o_gsegs = reserve(gsegs.size() * sizeof(QSeg));
   const size_t o_truth = reserve(truth.size() * 4);
   const size_t o_truth_e = reserve(truth_early.size() * 4);
   const size_t o_truth_l = reserve(truth_late.size() * 4);
@@ -909,6 +1027,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   uint8_t* hbuf = static_cast<uint8_t*>(X->pinned_buf(stage_bytes));
   uint8_t* dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
+  memcpy(hbuf + o_gsegs, gsegs.data(), gsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
   if (late_mask) {
     memcpy(hbuf + o_truth_e, truth_early.data(), truth_early.size() * 4);
@@ -983,11 +1102,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       HIP_TRY(hipMemsetAsync(P.stamps, 0, nstamp * 8, st));
     }
     launch_ms = ms_since(t_start);   // host staging done, scan enqueued
-    if (ncells && numeric) {   // general row scan (numeric comparison leaves)
+    if (ncells && !qsegs.empty()) HIP_TRY(launch_scan(P, kagg, st));
+    if (ncells && !gsegs.empty()) {   // general row scan (numeric comparison leaves, union_by_name promotion)
       XParams XG{};
-      XG.segs = P.segs;
-      XG.nsegs = P.nsegs;
-      XG.max_tiles = P.max_tiles;
+      XG.segs = reinterpret_cast<const QSeg*>(dbuf + o_gsegs);
+      XG.nsegs = uint32_t(gsegs.size());
+      XG.max_tiles = gmax_tiles;
       XG.strp = P.strp;
       XG.nstr = P.nstr;
       XG.nleaves = P.nleaves;
@@ -1002,8 +1122,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       XG.hash = hash_mode ? 1 : 0;
       XG.q = P;
       HIP_TRY(launch_ex_scan(XG, st));
-    } else if (ncells) {
-      HIP_TRY(launch_scan(P, kagg, st));
     }
     HIP_TRY(hipEventRecord(X->ev_scan1, st));
     if (ncells) HIP_TRY(launch_fixup_table(P, nc, kagg, st));
@@ -1075,9 +1193,15 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         msg = e.what();
       }
     }
+    // A full hash table is reported as "full, can grow" or "full at its bound" (cap and cap_max are rank-local):
+    // the ranks agree on both, re-run together while any rank can grow -- each growing only its own full table --
+    // and fail together when any table is full at its bound (a rank must not leave while another
+    // re-runs into the next collective).
+    const bool my_full = hash_mode && (fl & FLAG_HASH_FULL);
+    if (my_full && cap < cap_max) fl = (fl & ~uint32_t(FLAG_HASH_FULL)) | FLAG_HASH_GROW;
     hflags = agree(err, msg, fl);
-    if (hash_mode && (hflags & FLAG_HASH_FULL) && cap < cap_max) {
-      cap = std::min<uint64_t>(cap_max, cap * 4);
+    if (hash_mode && !(hflags & FLAG_HASH_FULL) && (hflags & FLAG_HASH_GROW)) {
+      if (my_full) cap = std::min<uint64_t>(cap_max, cap * 4);
       continue;
     }
     break;
@@ -1097,7 +1221,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   bool rows_done = false;   // key-range path: rank 0's result rows are already in place
   const char* kr_env = getenv("LK_KEYRANGE_MIN_CELLS");
   const uint64_t kr_min = kr_env ? uint64_t(atoll(kr_env)) : (uint64_t(1) << 20);
-  const bool keyrange = dist && comm_world(E) > 1 && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
+  const bool keyrange = dist && (comm_world(E) > 1 || comm_loopback(E)) && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
                         !ces && nslots == 1 && ncells >= kr_min && ncells == nc;
   if (dist) {
     if (hash_mode) {
@@ -1585,17 +1709,20 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       res->owned.push_back(kv.second);
       res->qt_of_glob[gi].emplace_back(c, res->owned.back().c_str());
     }
-  char buf[768];
+  char buf[896];
   snprintf(buf, sizeof(buf),
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
-           "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"table\":\"%s\","
-           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\"}",
+           "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"general_segments\":%zu,"
+           "\"failed_globs\":%zu,\"table\":\"%s\","
+           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\"",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
-           (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size(),
-           hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
+           (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size() + gsegs.size(), gsegs.size(),
+           nfailed, hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
            !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")));
   res->stats = buf;
+  if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
+  res->stats += "}";
   return LK_OK;
 }
 

@@ -189,12 +189,22 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
         } else {
           raw = __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? vi * 4u : OOB, 0, 0);
         }
-        if (qc == 0) {
-          ts = int64_t(raw);
-          ts_ok = ok && w8;
+        if (qc == 0) {   // BIGINT over INT64 / INT32 files (union_by_name)
+          ts = w8 ? int64_t(raw) : int64_t(int32_t(uint32_t(raw)));
+          ts_ok = ok;
         } else if (qc == 1) {
-          v = __longlong_as_double((long long)raw);
-          v_ok = ok && w8;
+          // the value as the glob's union_by_name type, then as double (JDBC getDouble of the aggregate):
+          // DOUBLE as is, INT64 / INT32 / FLOAT exactly widened; integers in a FLOAT union rounded to float first
+          const uint32_t pad = Sp->cols[1].pad, pt = pad & 0xffu;
+          if (pt == 5u) {
+            v = __longlong_as_double((long long)raw);
+          } else if (pt == 4u) {
+            v = double(__uint_as_float(uint32_t(raw)));
+          } else {
+            const long long iv = pt == 2u ? (long long)raw : (long long)int32_t(uint32_t(raw));
+            v = (pad & VCONV_VIA_FLOAT) ? double(float(iv)) : double(iv);
+          }
+          v_ok = ok;
         } else {
           const uint32_t pt = Sp->cols[qc].pad;   // Parquet physical type of this segment's column
           const bool is_int = pt == 1u || pt == 2u;
@@ -266,7 +276,9 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
           ok = false;
         }
         if (ok) {
-          const unsigned long long cell = ((unsigned long long)g * q.nbuckets + (unsigned long long)b) * q.ngroups + gid;
+          unsigned long long cell = ((unsigned long long)g * q.nbuckets + (unsigned long long)b) * q.ngroups + gid;
+          // percentiles: rows per (cell, DDSketch bin of the value; NULL reads 0.0), as scan_tiles keys them
+          if (q.sketch) cell = cell * DD_NBINS + dd_bin(q, v_ok ? v : 0.0);
           switch (X.agg * 2 + (X.hash ? 1 : 0)) {
             case AGG_SUM * 2: ex_merge<AGG_SUM, false>(q, cell, v_ok, v); break;
             case AGG_SUM * 2 + 1: ex_merge<AGG_SUM, true>(q, cell, v_ok, v); break;

@@ -290,8 +290,18 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   if (prog.size() > size_t(MAXPROG)) throw PlanError(LK_ERR_UNSUPPORTED, "filter too large");
 
   // ---- segments and globs ----
+  // A segment that cannot be read (missing, corrupt, a shape the loader does not take) fails its glob's query only:
+  // that glob is empty, the others stream (Commons.scala:249-253, 338-340).
   std::vector<std::shared_ptr<Segment>> segs(n_paths);
-  for (size_t i = 0; i < n_paths; i++) segs[i] = E.get_segment(paths[i], true);
+  std::vector<uint8_t> seg_bad(n_paths, 0);
+  for (size_t i = 0; i < n_paths; i++) {
+    try {
+      segs[i] = E.get_segment(paths[i], true);
+    } catch (const PlanError& e) {
+      if (e.code != LK_ERR_IO && e.code != LK_ERR_UNSUPPORTED) throw;
+      seg_bad[i] = 1;
+    }
+  }
   if (glob_size <= 0) glob_size = 10;
   const std::vector<std::string> proj = logs ? std::vector<std::string>{kTimestamp, kValue, kName, kMessage}
                                              : std::vector<std::string>{kTimestamp, kValue, kSpanName, kSpanKind};
@@ -306,9 +316,17 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     for (int si : g.segs) {
       g.win_lo = std::min(g.win_lo, R.segments[si].start_ts);
       g.win_hi = std::max(g.win_hi, R.segments[si].end_ts);
+      if (seg_bad[si]) {
+        g.skip = true;
+        continue;
+      }
       for (auto& [name, pt] : segs[si]->schema) {
         if (!g.types.count(name)) uni.push_back(name);
-        g.types[name] = union_type(g.types.count(name) ? g.types[name] : -1, pt);
+        try {
+          g.types[name] = union_type(g.types.count(name) ? g.types[name] : -1, pt);
+        } catch (const PlanError&) {   // a union DuckDB cannot form / this engine does not decode: the glob fails
+          g.skip = true;
+        }
       }
     }
     for (auto& l : leaves)   // nonExistentFields -> literal false (Commons.scala:224, BaseExpr.scala:462-464)
@@ -372,7 +390,12 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   for (size_t gi = 0; gi < globs.size(); gi++) {
     XGlob& g = globs[gi];
     if (g.skip || g.win_lo >= g.win_hi || limit == 0) continue;
-    g.open = true;
+    // the glob's descriptors go in together: a column its query cannot bind empties the glob (Binder Error,
+    // Commons.scala:249-253), the other globs are unaffected
+    const size_t mark = qsegs.size();
+    const uint64_t rows_mark = rows_scanned;
+    const uint32_t tiles_mark = max_tiles;
+    try {
     for (size_t p = 0; p < g.segs.size(); p++) {
       const Segment& S = *segs[g.segs[p]];
       QSeg q{};
@@ -389,7 +412,8 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
         const HostCol& hc = S.cols[c];
         if (want_string != hc.is_string)
           throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
-        if (qc == 0 && hc.ptype != pq::INT64) throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64");
+        if (qc == 0 && hc.ptype != pq::INT64 && hc.ptype != pq::INT32)
+          throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64 or INT32");
         if (qc >= 2 + int(strs.size()) && hc.ptype != pq::INT64 && hc.ptype != pq::DOUBLE && hc.ptype != pq::INT32 &&
             hc.ptype != pq::FLOAT)
           throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison on column " + name + " of an undecoded type");
@@ -405,6 +429,17 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       qseg_seg.push_back(&S);
       qseg_pos.push_back(uint32_t(p));
       qseg_glob.push_back(uint32_t(gi));
+    }
+    g.open = true;
+    } catch (const PlanError& e) {
+      if (e.code != LK_ERR_UNSUPPORTED) throw;
+      g.skip = true;
+      qsegs.resize(mark);
+      qseg_seg.resize(mark);
+      qseg_pos.resize(mark);
+      qseg_glob.resize(mark);
+      rows_scanned = rows_mark;
+      max_tiles = tiles_mark;
     }
   }
   if (qsegs.size() > 65535) throw PlanError(LK_ERR_UNSUPPORTED, "more than 65535 segments in one evaluation");

@@ -87,8 +87,11 @@ struct QCol {               // one query column in one segment
   const TileCol* tcols;     // per tile
   const uint32_t* remap;
   uint32_t present;         // 0: column absent from this segment (all NULL)
-  uint32_t pad;
+  uint32_t pad;             // bits 0..7: Parquet physical type; value column: VCONV_* bits
 };
+// Value column of a segment whose glob unifies it to FLOAT while the file stores integers (union_by_name): the value
+// is cast to FLOAT (round to nearest) before it is aggregated.
+constexpr uint32_t VCONV_VIA_FLOAT = 0x100u;
 
 struct QSeg {
   const uint8_t* base;
@@ -170,7 +173,10 @@ struct QParams {
   unsigned long long* plan_bytes;
 };
 
-enum Flag : uint32_t { FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u };
+enum Flag : uint32_t {
+  FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u,
+  FLAG_HASH_GROW = 16u   // host only: this rank's hash table was full below its bound (agreed re-run)
+};
 
 // DDSketch bins (sketches-java LogarithmicMapping, relative accuracy 0.01): bin 0 = zero, 1 + DD_BIAS + i = positive
 // index i, 1 + DD_HALF + DD_BIAS + i = negative index i (|i| < DD_BIAS covers every finite double).

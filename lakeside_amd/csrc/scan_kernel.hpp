@@ -159,21 +159,6 @@ __device__ __forceinline__ bool interpret(const QParams& P, uint32_t T, uint32_t
   return st & 1;
 }
 
-// DDSketch bin of a value (sketches-java 0.8.2 LogarithmicMapping.index + DDSketch.accept): |v| <= dd_min -> the
-// zero bin; index = (int) (ln|v| * multiplier), minus one when negative (LogLikeIndexMapping.index's floor);
-// NaN / |v| > dd_max is untrackable (accept throws): FLAG_SKETCH_RANGE.
-__device__ __forceinline__ uint32_t dd_bin(const QParams& P, double v) {
-  const double a = fabs(v);
-  if (!(a <= P.dd_max)) {
-    atomicOr(P.flags, FLAG_SKETCH_RANGE);
-    return 0u;
-  }
-  if (a <= P.dd_min) return 0u;
-  const double x = log(a) * P.dd_mult;
-  const int32_t i = x >= 0.0 ? int32_t(x) : int32_t(x) - 1;
-  return uint32_t(1 + DD_BIAS + i) + (v < 0.0 ? DD_HALF : 0u);
-}
-
 // Uniform LDS-staged pointer -> SGPR pair.
 template <class T>
 __device__ __forceinline__ const T* uptr(const T* p) {

@@ -262,10 +262,15 @@ def check_hot_path(pr: PushDownRequest) -> None:
 # Regex: DuckDB regexp_matches(l, p, 'i') = RE2 partial match, case-insensitive (BaseExpr.scala:485-501)
 # ----------------------------------------------------------------------------------------------
 def re2_search(values: Sequence[Optional[str]], pattern: str) -> List[Optional[bool]]:
+    """RE2 search over the values; a pattern RE2 rejects fails the glob's SQL (GlobSqlError) whether or not the
+    glob holds any value (DuckDB compiles the constant pattern when it binds the query)."""
     import pyarrow as pa
     import pyarrow.compute as pc
-    return pc.match_substring_regex(pa.array(list(values), type=pa.string()), pattern,
-                                    ignore_case=True).to_pylist()
+    try:
+        return pc.match_substring_regex(pa.array(list(values) or [""], type=pa.string()), pattern,
+                                        ignore_case=True).to_pylist()[:len(values)]
+    except pa.ArrowInvalid as e:
+        raise GlobSqlError(f"regexp_matches: {e}") from e
 
 
 # ----------------------------------------------------------------------------------------------
@@ -297,11 +302,30 @@ def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[s
         tables.append((pf.read(columns=want, use_threads=True), pf.metadata.num_rows))
     nums = {}
     for c in numeric:
+        # union_by_name type of the column over the glob's files (DuckDB's common supertype, INTEGER < BIGINT <
+        # FLOAT < DOUBLE); text cannot be summed / bucketed: the glob's SQL fails (Binder Error)
+        kinds = set()
+        for t, _ in tables:
+            if c in t.column_names:
+                typ = t.schema.field(c).type
+                if pa.types.is_dictionary(typ):
+                    typ = typ.value_type
+                if pa.types.is_integer(typ):
+                    kinds.add("int")
+                elif pa.types.is_float32(typ):
+                    kinds.add("float32")
+                elif pa.types.is_floating(typ):
+                    kinds.add("float64")
+                else:
+                    raise GlobSqlError(f"column {c} of type {typ} in a numeric role")
+        via_f32 = "float32" in kinds and "float64" not in kinds   # integers of a FLOAT union are cast to FLOAT
         parts, valid = [], []
         for t, n in tables:
             if c in t.column_names:
                 a = t.column(c).combine_chunks() if t.num_rows else pa.array([], pa.float64())
                 arr = a.to_numpy(zero_copy_only=False)
+                if via_f32:
+                    arr = np.asarray(arr).astype(np.float32).astype(np.float64)
                 v = np.asarray(a.is_valid().to_numpy(zero_copy_only=False), dtype=bool) if a.null_count else \
                     np.ones(n, dtype=bool)
                 arr = np.where(v, arr, 0) if a.null_count else arr
@@ -508,9 +532,9 @@ def _leaf(f: Filter, col: Optional[_Col], nonexistent: set, n: int):
     elif f.op == NOT_IN:
         hit = [s not in f.v for s in dictionary]
     elif f.op == REGEX:
-        hit = [bool(b) for b in re2_search(dictionary, f.v[0])] if dictionary else []
+        hit = [bool(b) for b in re2_search(dictionary, f.v[0])]
     elif f.op == CONTAINS:
-        hit = [bool(b) for b in re2_search(dictionary, ".*" + f.v[0] + ".*")] if dictionary else []
+        hit = [bool(b) for b in re2_search(dictionary, ".*" + f.v[0] + ".*")]
     else:
         raise NotImplementedError(f.op)
     lut = np.array(list(hit) + [False], dtype=bool)
@@ -613,11 +637,11 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
     if only is not None:
         paths = [paths[j] for j in only]
         sources = None if sources is None else [sources[j] for j in only]
-    read_union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
     try:
+        read_union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
         strs.update(_read_numeric(paths, [c for c in numcols if c in read_union], sources))
-    except GlobSqlError:
-        return []
+    except Exception:   # missing / unreadable file, a column DuckDB cannot bind: that glob alone is empty
+        return []       # (Commons.scala:249-253: any exception -> (null, null, null) -> Source.empty)
     union = list(union) if union is not None else read_union
     nonexistent = fs - set(union)                                   # Commons.scala:224
     if not _check_numeric_literals(be.filter, nonexistent):
@@ -635,7 +659,10 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
     ts = ts.astype(np.int64)
     n = len(ts)
     win = ts_valid & (ts >= start) & (ts < end)                     # BaseExpr.scala:159-161
-    t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    try:
+        t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    except GlobSqlError:   # a regex RE2 rejects, on a field the glob has: the glob's SQL fails
+        return []
     keep = win & t
     if be.dataset == METRICS:
         bucket = ts                                                  # BaseExpr.scala:391-394
@@ -842,10 +869,10 @@ def evaluate_tag_glob(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], pat
     fs = filter_field_set(be.filter) | set(be.chart.groupBys if be.chart else [])
     numcols = sorted({l.k for l in _leaves(be.filter) if l.op in NUMERIC_OPS})
     strings = sorted((set(_leaf_columns(be.filter)) - set(numcols)) | {tag})
-    union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources)
     try:
+        union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources)
         strs.update(_read_numeric(paths, [c for c in numcols if c in union], sources))
-    except GlobSqlError:
+    except Exception:   # Commons.scala:249-253: the glob's query fails -> empty
         return []
     nonexistent = fs - set(union)
     if not _check_numeric_literals(be.filter, nonexistent):
@@ -858,7 +885,10 @@ def evaluate_tag_glob(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], pat
     ts, ts_valid = nums[TIMESTAMP]
     ts = ts.astype(np.int64)
     n = len(ts)
-    t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    try:
+        t, _ = _eval_filter(be.filter, strs, nonexistent, n)
+    except GlobSqlError:   # a regex RE2 rejects, on a field the glob has: the glob's SQL fails
+        return []
     keep = ts_valid & (ts >= start) & (ts < end) & t
     col = strs[tag]
     codes = col.codes[keep]

@@ -138,13 +138,16 @@ def evaluate_exemplar_glob(pr: dx.PushDownRequest, seg_idx: Sequence[int], paths
     segs = [pr.segmentRequests[i] for i in seg_idx]
     proj = [dx.TIMESTAMP, dx.VALUE] + ([dx.NAME, MESSAGE] if be.dataset == dx.LOGS else [SPAN_NAME, SPAN_KIND])
     tables, union, types = [], [], {}
-    for i, p in enumerate(paths):
-        t = pq.read_table(p if sources is None else pa.BufferReader(sources[i]))
-        tables.append(t)
-        for f in t.schema:
-            if f.name not in types:
-                union.append(f.name)
-            types[f.name] = union_type(types.get(f.name), _kind(f.type))
+    try:
+        for i, p in enumerate(paths):
+            t = pq.read_table(p if sources is None else pa.BufferReader(sources[i]))
+            tables.append(t)
+            for f in t.schema:
+                if f.name not in types:
+                    union.append(f.name)
+                types[f.name] = union_type(types.get(f.name), _kind(f.type))
+    except Exception:   # unreadable file / a union DuckDB cannot form: the glob's query fails -> empty
+        return []       # (Commons.scala:249-253)
     fs = dx.field_set(be)
     nonexistent = fs - set(union)
     leafcols = dx._leaf_columns(be.filter)
@@ -161,7 +164,10 @@ def evaluate_exemplar_glob(pr: dx.PushDownRequest, seg_idx: Sequence[int], paths
     ts, tsv = nums[dx.TIMESTAMP]
     ts = ts.astype(np.int64)
     n = len(ts)
-    t, _ = dx._eval_filter(be.filter, strs, nonexistent, n)
+    try:
+        t, _ = dx._eval_filter(be.filter, strs, nonexistent, n)
+    except dx.GlobSqlError:   # a regex RE2 rejects fails the glob's SQL
+        return []
     keep = np.nonzero(tsv & (ts >= start) & (ts < end) & t)[0]
     desc = be.order.upper() == "DESC"
     order = np.argsort(-ts[keep] if desc else ts[keep], kind="stable")   # ties: file order

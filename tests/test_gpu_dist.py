@@ -156,6 +156,49 @@ def test_dist_world1_rccl_golden():
         eng.close()
 
 
+@pytest.mark.timeout(300)
+def test_dist_world1_rccl_loopback_data_path():
+    """with LK_COMM_LOOPBACK=1 a world-1 RCCL communicator runs every collective of the 8-GPU path
+    on this box -- ncclAllGather of sizes and padded blobs (glob unions, fingerprints, agreements), grouped
+    ncclSend/ncclRecv to self for the dense table gather, the hash-record gather and the key-range all-to-all
+    (both legs) -- and the merge reads what came back through RCCL (poisoned receive buffers first).  Every golden
+    case through each reduce path equals the golden merged rows."""
+    from lakeside_amd.evaluator import Engine
+    saved = {k: os.environ.get(k) for k in ("LK_COMM_LOOPBACK", "LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS")}
+    os.environ["LK_COMM_LOOPBACK"] = "1"
+    eng = Engine(0)
+    try:
+        eng.comm_init(Engine.unique_id(), 1, 0)
+        seen = set()
+        for mode, env in [("gather_to_root", {}), ("keyrange", {"LK_KEYRANGE_MIN_CELLS": "1"}),
+                          ("records_to_root", {"LK_DENSE_MAX_CELLS": "1"})]:
+            for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            for case in _cases():
+                paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
+                agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+                assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg,
+                                  f"loopback {mode} {case['name']}")
+                ts = res.ts.tolist()
+                assert ts == sorted(ts), case["name"]
+                seen.add(res.stats["reduce"])
+            for case in _tag_cases():
+                paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
+                key = lambda t: sorted(t.items())   # noqa: E731
+                assert sorted(res.tags, key=key) == sorted(case["expected_merged"], key=key), f"loopback tag {mode}"
+        assert seen == {"gather_to_root", "keyrange", "records_to_root"}, seen
+    finally:
+        eng.close()
+        for k, v in saved.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
 # ---------------------------------------------------------------------------------------------------------
 # 8 ranks on the one GPU (host transport): the C4 and C5 shapes with a different dictionary on every rank
 # ---------------------------------------------------------------------------------------------------------
@@ -237,19 +280,24 @@ def _worker_err(rank, world, port):
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
 
-    from lakeside_amd.evaluator import Engine, LakesideError
+    from lakeside_amd.evaluator import Engine
+    from oracle import dataexpr as dx
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = Engine(0)
     try:
         eng.comm_init_host(world, rank)
         case = _cases()[0]
+        n = len(case["segments"])
         paths = [os.path.join(GOLDEN, p) for p in case["segments"]] + ["/nonexistent/segment.parquet"]
         req = dict(case["request"])
         req["segmentRequests"] = list(req["segmentRequests"]) + [req["segmentRequests"][0]]
-        shard = [0] * (len(paths) - 1) + [1]   # the missing file is rank 1's
-        with pytest.raises(LakesideError) as ei:
-            eng.eval_pushdown_dist(json.dumps(req), paths, shard, case["glob_size"])
-        assert "segment" in str(ei.value)
+        shard = [0] * n + [1]   # the missing file is rank 1's
+        res = eng.eval_pushdown_dist(json.dumps(req), paths, shard, case["glob_size"])
+        if rank == 0:   # its glob is empty on every rank; the other globs merge as usual (Commons.scala:249-253)
+            agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+            pr = dx.parse_pushdown(json.dumps(req))
+            assert_rows_equal(res.rows(), dx.evaluate_merged(pr, paths, case["glob_size"]), agg, "missing segment")
+            assert res.stats["failed_globs"] == 1, res.stats
         # the communicator is still usable afterwards: a good call succeeds on both ranks
         ok = eng.eval_pushdown_dist(json.dumps(case["request"]), paths[:-1], None, case["glob_size"])
         if rank == 0:
@@ -262,8 +310,42 @@ def _worker_err(rank, world, port):
 
 
 @pytest.mark.timeout(180)
-def test_dist_rank_local_error_fails_every_rank():
-    """A segment only rank 1 reads is missing: both ranks return an error (none waits in a collective) and the
-    next call works (agree on a status before each collective)."""
+def test_dist_rank_local_missing_segment_empties_its_glob():
+    """A segment only rank 1 reads is missing: the ranks agree that its glob failed (one all-gather), that glob is
+    empty everywhere and the others merge as the oracle says; no rank waits in a collective, the next call works."""
     import torch.multiprocessing as mp
     mp.spawn(_worker_err, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _worker_regrow(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    # ADVICE r2 (high): rank 0 starts with a 64-slot hash table that fills (can grow); rank 1's first table is
+    # already at its bound.  Both must re-run together until rank 0's table fits.
+    os.environ["LK_DENSE_MAX_CELLS"] = "1"
+    os.environ["LK_HASH_INIT_SLOTS"] = "64" if rank == 0 else str(1 << 16)
+    import torch.distributed as dist
+
+    from lakeside_amd.evaluator import Engine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        for case in _cases():
+            paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+            shard = [0] * (len(paths) - 1) + [1]   # uneven: rank 1 scans one segment
+            res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, shard, case["glob_size"])
+            if rank == 0:
+                agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+                assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"regrow {case['name']}")
+                assert res.stats["table"] == "hash", res.stats
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dist_hash_regrowth_uneven_shards():
+    import torch.multiprocessing as mp
+    mp.spawn(_worker_regrow, args=(2, _free_port()), nprocs=2, join=True)

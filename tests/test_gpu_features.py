@@ -255,8 +255,8 @@ def test_hbm_budget_lru_eviction():
         e.put_segment("s2", blobs[2])                              # over budget: s1 (LRU) goes
         assert e.segment_count == 2 and e.segment_bytes <= int(2.5 * one)
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
-        with pytest.raises(Exception):
-            e.eval_pushdown(req, ["s1"], 10, LK_MERGED)             # evicted, and not a file path
+        gone = e.eval_pushdown(req, ["s1"], 10, LK_MERGED)         # evicted, and not a file path: its glob
+        assert len(gone) == 0 and gone.stats["failed_globs"] == 1   # fails alone (Commons.scala:249-253)
         e.put_segment("s3", blobs[3])                              # s2 is now the LRU
         assert e.segment_count == 2
         e.put_segment("s0", blobs[0])

@@ -1,0 +1,175 @@
+"""Per-glob failure isolation and union_by_name value promotion (MI355X, through the C ABI).
+
+Reference: Commons.toGlobResultSet (core/src/main/scala/com/cardinal/utils/Commons.scala:200-254) runs one DuckDB
+query per glob over read_parquet([...], union_by_name=True) (213); ANY exception -- a missing or corrupt file, a
+column the SQL cannot bind, a bad regex -- becomes (null, null, null) -> Source.empty for that glob alone
+(249-253, 338-340), while the other globs stream.  union_by_name unifies a numeric column over the glob's files to
+the widest of INTEGER < BIGINT < FLOAT < DOUBLE, so a value column stored as INT64 / INT32 / FLOAT in some files is
+aggregated, not refused.  The GPU rows are compared with the oracle (oracle/dataexpr.py) on the same files.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from tests.parity import assert_rows_equal
+
+pytestmark = pytest.mark.gpu
+
+
+def _write(path, rng, hour, value_type="double", ts_type="int64", n=60_000, null_frac=0.05, with_service=True):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    t0 = synth.T0 + hour * synth.HOUR
+    ts = np.sort(rng.integers(t0, t0 + synth.HOUR, n))
+    if ts_type == "int32":   # an INT32 timestamp column: values that fit (seconds-scale offsets from 0)
+        ts = (ts - synth.T0).astype(np.int32)
+    vmask = rng.random(n) < null_frac
+    if value_type == "double":
+        val = pa.array(rng.lognormal(0, 2, n), pa.float64(), mask=vmask)
+    elif value_type == "float":
+        val = pa.array(rng.lognormal(0, 2, n).astype(np.float32), pa.float32(), mask=vmask)
+    elif value_type == "int64":   # beyond 2^24: a FLOAT union rounds them
+        val = pa.array(rng.integers(-(1 << 26), 1 << 26, n), pa.int64(), mask=vmask)
+    elif value_type == "int32":
+        val = pa.array(rng.integers(-(1 << 25), 1 << 25, n).astype(np.int32), pa.int32(), mask=vmask)
+    else:   # text: sum / min / max of a VARCHAR column fail the glob's SQL
+        val = pa.array([str(x) for x in rng.integers(0, 1000, n)], pa.string(), mask=vmask)
+    cols = {dx.TIMESTAMP: pa.array(ts), dx.VALUE: val,
+            synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 4, n)], pa.string(),
+                                 mask=rng.random(n) < null_frac)}
+    if with_service:
+        cols[synth.SERVICE] = pa.array([f"svc-{k:03d}" for k in rng.integers(0, 12, n)], pa.string(),
+                                       mask=rng.random(n) < null_frac)
+    t = pa.table(cols)
+    strings = [c for c in t.column_names if str(t.schema.field(c).type) == "string" and c != dx.VALUE]
+    pq.write_table(t, path, compression="NONE", use_dictionary=strings,
+                   column_encoding={c: "PLAIN" for c in t.column_names if c not in strings},
+                   row_group_size=30_000, data_page_size=1 << 16)
+    return path
+
+
+def _compare(engine, req_obj, paths, glob_size, agg, label):
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    from oracle import dataexpr as dx
+    req = json.dumps(req_obj)
+    pr = dx.parse_pushdown(req)
+    cells = dx.evaluate_glob_cells(pr, glob_size, paths)
+    res = engine.eval_pushdown(req, paths, glob_size, LK_PER_GLOB_ROWS)
+    got = res.per_glob(len(cells))
+    for gi, (g, cs) in enumerate(zip(got, cells)):
+        assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"{label} glob {gi}")
+    merged = engine.eval_pushdown(req, paths, glob_size, LK_MERGED)
+    assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, f"{label} merged")
+    return cells, res.stats
+
+
+@pytest.fixture(scope="module")
+def glob_files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("globs")
+    rng = np.random.default_rng(42)
+    f = {}
+    f["clean0"] = _write(str(d / "clean0.parquet"), rng, 0)
+    f["missing"] = str(d / "does_not_exist.parquet")
+    f["int64v"] = _write(str(d / "int64v.parquet"), rng, 1, value_type="int64")
+    f["double1"] = _write(str(d / "double1.parquet"), rng, 1)
+    f["clean2"] = _write(str(d / "clean2.parquet"), rng, 2)
+    f["clean3"] = _write(str(d / "clean3.parquet"), rng, 3, with_service=False)
+    f["int32v"] = _write(str(d / "int32v.parquet"), rng, 0, value_type="int32")
+    f["floatv"] = _write(str(d / "floatv.parquet"), rng, 0, value_type="float")
+    f["int64v_b"] = _write(str(d / "int64v_b.parquet"), rng, 2, value_type="int64")
+    f["int32v_b"] = _write(str(d / "int32v_b.parquet"), rng, 2, value_type="int32")
+    f["textv"] = _write(str(d / "textv.parquet"), rng, 3, value_type="text")
+    corrupt = str(d / "corrupt.parquet")
+    with open(f["clean2"], "rb") as src:
+        blob = src.read()
+    with open(corrupt, "wb") as dst:   # a truncated file: footer gone
+        dst.write(blob[: len(blob) // 2])
+    f["corrupt"] = corrupt
+    return f
+
+
+def _segs(n, step=60000):
+    from lakeside_amd import synth
+    return [synth.segment_request(i, step=step, hour=i % 4) for i in range(n)]
+
+
+@pytest.mark.parametrize("agg", ["sum", "min", "max", "count", "avg"])
+def test_three_globs_missing_path_int64_value_clean(engine, glob_files, agg):
+    """glob 0 holds a missing path, glob 1 a segment whose _cardinalhq.value is INT64 (with a DOUBLE
+    one: union DOUBLE), glob 2 is clean.  Glob 0 is empty, globs 1-2 equal the oracle, LK_MERGED equals the merge of
+    the surviving globs."""
+    from lakeside_amd import synth
+    f = glob_files
+    paths = [f["clean0"], f["missing"], f["int64v"], f["double1"], f["clean2"], f["clean3"]]
+    for gbs in ([], [synth.SERVICE]):
+        req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(len(paths)), agg, gbs)
+        cells, stats = _compare(engine, req, paths, 2, agg, f"{agg} by {gbs}")
+        assert cells[0] == [] and cells[1] and cells[2]
+        assert stats["failed_globs"] == 1 and stats["general_segments"] == 1, stats
+
+
+@pytest.mark.parametrize("agg", ["sum", "min", "max", "count"])
+def test_value_type_unions(engine, glob_files, agg):
+    """union_by_name over the value column: INT32 + FLOAT -> FLOAT (integers cast to FLOAT first: |v| > 2^24 round),
+    INT64 + INT32 -> BIGINT, a corrupt file fails only its own glob, and so does (for sum: a Binder Error) a VARCHAR
+    value column.  (min / max / count over a VARCHAR value column would run in DuckDB -- string order, then
+    getDouble of the text; the engine empties that glob instead: DESIGN.md §9.)"""
+    from lakeside_amd import synth
+    f = glob_files
+    paths = [f["int32v"], f["floatv"], f["int64v_b"], f["int32v_b"], f["corrupt"], f["clean0"]]
+    if agg == "sum":
+        paths += [f["textv"], f["double1"]]
+    req = synth.pushdown(synth.leaf(synth.NAME, "!=", "metric_03"), _segs(len(paths)), agg, [synth.SERVICE])
+    cells, stats = _compare(engine, req, paths, 2, agg, f"unions {agg}")
+    assert cells[0] and cells[1] and cells[2] == []
+    assert stats["failed_globs"] == (2 if agg == "sum" else 1), stats
+    if agg == "sum":
+        assert cells[3] == []
+
+
+def test_bad_regex_fails_only_globs_with_the_field(engine, glob_files):
+    """A pattern RE2 rejects fails the SQL of the globs where its field exists; in a glob without the field the
+    leaf is the literal `false` (BaseExpr.scala:462-464), so `NOT (regex)` passes every row there."""
+    from lakeside_amd import synth
+    f = glob_files
+    paths = [f["clean0"], f["double1"], f["clean3"]]   # clean3 has no resource.service.name
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"),
+            "q2": {"not": synth.leaf(synth.SERVICE, "regex", "svc-(0")}}
+    req = synth.pushdown(filt, _segs(len(paths)), "sum", [])
+    cells, stats = _compare(engine, req, paths, 1, "sum", "bad regex")
+    assert cells[0] == [] and cells[1] == [] and cells[2]
+
+
+def test_int32_timestamps_promoted(engine, tmp_path):
+    """INT32 timestamp files next to INT64 ones: BIGINT union, buckets from the widened values."""
+    from lakeside_amd import synth
+    rng = np.random.default_rng(7)
+    paths = [_write(str(tmp_path / "ts64.parquet"), rng, 0), _write(str(tmp_path / "ts32.parquet"), rng, 0,
+                                                                    ts_type="int32")]
+    segs = _segs(2)
+    for s in segs:   # the INT32 file's timestamps are offsets from T0: one window covers both
+        s["startTs"], s["endTs"] = 0, synth.T0 + synth.HOUR
+    req = synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_02"), segs, "count", [synth.SERVICE])
+    _compare(engine, req, paths, 2, "count", "int32 ts")
+
+
+def test_percentiles_over_promoted_values(engine, glob_files):
+    """DDSketch bins (percentile aggregations) of an INT64 value column on the general row scan equal the oracle's
+    sketches."""
+    from lakeside_amd import LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    from tests.test_gpu_features import _pct_rows_equal
+    f = glob_files
+    paths = [f["int64v"], f["double1"], f["int32v"], f["floatv"]]
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_01"), _segs(len(paths)), "p95", []))
+    pr = dx.parse_pushdown(req)
+    want = dx.evaluate_percentile_per_glob(pr, 2, paths)
+    res = engine.eval_pushdown(req, paths, 2, LK_PER_GLOB_ROWS)
+    for gi in range(len(want)):
+        got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
+               for r in range(len(res)) if int(res.globs[r]) == gi]
+        _pct_rows_equal(got, want[gi], 0.95, f"p95 promoted glob {gi}")
