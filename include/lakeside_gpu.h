@@ -10,7 +10,14 @@
  *
  * Conventions: 0 = success, negative = error (message in lk_last_error(), thread-local).  Never throws or
  * aborts across the ABI.  Inputs are borrowed for the duration of the call.  Results are owned by the
- * library until lk_result_free.  Calls on one engine are thread-safe (serialised per engine).
+ * library until lk_result_free.  Calls on one engine are thread-safe and re-entrant: each evaluation leases its
+ * own context (HIP stream, workspaces; up to "max_calls" in flight), so calls from several threads run
+ * concurrently, as the worker's glob queries do (Commons.scala:371-372); only distributed calls
+ * (lk_eval_pushdown_dist) are serialised, to keep every rank's collectives in one order.
+ *
+ * Errors: a failure that belongs to one glob's DuckDB query in the reference -- a missing or unreadable segment,
+ * corrupt Parquet, a column type the query cannot bind, a regex RE2 rejects -- empties that glob only
+ * (Commons.toGlobResultSet, Commons.scala:249-253); the call still succeeds ("failed_globs" in lk_result_stats).
  */
 #ifndef LAKESIDE_GPU_H
 #define LAKESIDE_GPU_H
@@ -79,7 +86,19 @@ const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col); /* 
  * row's value is getValueAtQuantile(NN / 100) of that sketch (BaseExpr.scala:59-61).  *len = 0 / NULL for other
  * aggregations.  Valid until lk_result_free. */
 const uint8_t* lk_result_sketch(const lk_result* r, size_t row, size_t* len);
-/* JSON: {"scan_ms":..,"total_ms":..,"rows_scanned":..,"algorithmic_bytes":..,"tiles":..,"cells":..} */
+/* Bulk tag export (replaces one lk_result_tag_value call per row and column; the reference materializes tags per
+ * row in Commons.toDataPoint, Commons.scala:399-462).  The name / groupBy tag columns are the first
+ * lk_result_num_group_columns columns.  Row r's value in such a column `col` is
+ *     dict[(lk_result_group_ids(r)[row] / stride) % ndim]       (NULL: the tag is absent, S15)
+ * with dict = lk_result_tag_dictionary(r, col, &stride, &ndim).  NULL dictionary (ndim 0): the column yields no
+ * tag (a hidden tag).  A row whose group tags are all absent takes its glob's queryTags (Commons.scala:450-452):
+ * lk_result_tag_value on the columns after the group columns.  Arrays are valid until lk_result_free; an
+ * engine-dictionary column's table is shared with the engine and costs O(1) once built. */
+const uint32_t* lk_result_group_ids(const lk_result* r);
+size_t lk_result_num_group_columns(const lk_result* r);
+const char* const* lk_result_tag_dictionary(const lk_result* r, size_t col, uint64_t* stride, uint64_t* ndim);
+/* JSON: {"scan_ms":..,"total_ms":..,"rows_scanned":..,"algorithmic_bytes":..,"tiles":..,"cells":..,
+ *        "failed_globs":..,"general_segments":..} */
 const char* lk_result_stats(const lk_result* r);
 void lk_result_free(lk_result* r);
 

@@ -41,6 +41,10 @@ SIGNATURES = [
     ("lk_result_num_tag_columns", _c.c_size_t, [_P]),
     ("lk_result_tag_name", _c.c_char_p, [_P, _c.c_size_t]),
     ("lk_result_tag_value", _c.c_char_p, [_P, _c.c_size_t, _c.c_size_t]),
+    ("lk_result_group_ids", _c.POINTER(_c.c_uint32), [_P]),
+    ("lk_result_num_group_columns", _c.c_size_t, [_P]),
+    ("lk_result_tag_dictionary", _c.POINTER(_c.c_void_p), [_P, _c.c_size_t, _c.POINTER(_c.c_uint64),
+                                                           _c.POINTER(_c.c_uint64)]),
     ("lk_result_stats", _c.c_char_p, [_P]),
     ("lk_result_sketch", _c.POINTER(_c.c_uint8), [_P, _c.c_size_t, _c.POINTER(_c.c_size_t)]),
     ("lk_result_free", None, [_P]),

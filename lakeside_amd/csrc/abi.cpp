@@ -149,6 +149,23 @@ const char* lk_result_tag_value(const lk_result* r, size_t row, size_t col) {
   if (!r || row >= r->nrows || col >= r->tag_names.size()) return nullptr;
   return r->tag(row, col);
 }
+const uint32_t* lk_result_group_ids(const lk_result* r) { return r ? r->gid : nullptr; }
+size_t lk_result_num_group_columns(const lk_result* r) { return (r && !r->exemplar) ? r->tcols.size() : 0; }
+const char* const* lk_result_tag_dictionary(const lk_result* r, size_t col, uint64_t* stride, uint64_t* ndim) {
+  if (stride) *stride = 1;
+  if (ndim) *ndim = 0;
+  if (!r || r->exemplar || col >= r->tcols.size()) return nullptr;
+  try {
+    const std::vector<const char*>* v = r->tag_dictionary(col);
+    if (!v) return nullptr;
+    if (stride) *stride = r->tcols[col].stride;
+    if (ndim) *ndim = r->tcols[col].ndim;
+    return v->data();
+  } catch (const std::exception& e) {
+    t_err = e.what();
+    return nullptr;
+  }
+}
 const char* lk_result_stats(const lk_result* r) { return r ? r->stats.c_str() : nullptr; }
 const uint8_t* lk_result_sketch(const lk_result* r, size_t row, size_t* len) {
   if (len) *len = 0;

@@ -182,6 +182,59 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   return slot;
 }
 
+std::shared_ptr<const std::vector<const char*>> Engine::dict_ptrs(const std::string& col, size_t n) {
+  std::lock_guard<std::mutex> g(ptrs_mu);
+  auto& slot = ptrs[col];
+  if (slot && slot->size() == n + 1) return slot;
+  auto v = std::make_shared<std::vector<const char*>>(n + 1, nullptr);
+  size_t from = 0;
+  if (slot && slot->size() <= n + 1) {   // the dictionary grew: values [0, old n) are unchanged (StableStrs)
+    from = slot->size() - 1;
+    memcpy(v->data(), slot->data(), from * sizeof(const char*));
+  }
+  GlobalDict& gd = dict(col);
+  std::vector<const std::string*> s(n - from);
+  {
+    std::lock_guard<std::mutex> dg(gd.mu);
+    for (size_t i = from; i < n; i++) s[i - from] = &gd.vals[i];   // stable addresses
+  }
+  for (size_t i = from; i < n; i++) {
+    const std::string& x = *s[i - from];
+    (*v)[i] = (x.empty() || x == "null") ? nullptr : x.c_str();
+  }
+  slot = v;
+  return slot;
+}
+
+}  // namespace lk
+
+const std::vector<const char*>* lk_result::tag_dictionary(size_t c) const {
+  if (c >= tcols.size() || tcols[c].hidden) return nullptr;
+  std::lock_guard<std::mutex> g(bulk_mu);
+  if (bulk.size() < tcols.size()) bulk.resize(tcols.size());
+  if (bulk[c]) return bulk[c].get();
+  const TagCol& t = tcols[c];
+  if (t.local.empty() && !t.order && t.engine && !t.null_value && t.dim_null == t.dict_n && t.ndim == t.dict_n + 1) {
+    bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n);   // dim id = engine global id: the engine's shared table
+    return bulk[c].get();
+  }
+  auto v = std::make_shared<std::vector<const char*>>(size_t(t.ndim), nullptr);
+  if (!t.local.empty()) {
+    for (size_t d = 0; d < v->size() && d < t.local.size(); d++) (*v)[d] = t.local[d];
+  } else if (t.dict) {
+    for (size_t d = 0; d < v->size(); d++) {
+      if (d == t.dim_null) continue;
+      const std::string& s = (*t.dict)[t.order ? t.order->perm[d] : d];
+      (*v)[d] = (s.empty() || s == "null") ? nullptr : s.c_str();
+    }
+  }
+  if (t.dim_null < v->size()) (*v)[t.dim_null] = t.null_value;
+  bulk[c] = v;
+  return v.get();
+}
+
+namespace lk {
+
 GlobalDict& Engine::dict(const std::string& col) {
   std::lock_guard<std::mutex> g(dict_mu);
   auto& p = dicts[col];

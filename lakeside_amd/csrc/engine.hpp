@@ -172,6 +172,12 @@ struct Engine {
   std::mutex order_mu;
   std::unordered_map<std::string, std::shared_ptr<const DictOrder>> orders;   // per column, latest size
   std::shared_ptr<const DictOrder> dict_order(const std::string& col, size_t n);
+  // Bulk tag export (lk_result_tag_dictionary): the column's first n dictionary values as C strings (nullptr for the
+  // null-like "" / "null", which drop the tag) plus a trailing nullptr (the dim id of NULL).  Cached per column and
+  // rebuilt (prefix copied) only when the dictionary has grown, so in steady state a result's dictionary costs O(1).
+  std::mutex ptrs_mu;
+  std::unordered_map<std::string, std::shared_ptr<const std::vector<const char*>>> ptrs;
+  std::shared_ptr<const std::vector<const char*>> dict_ptrs(const std::string& col, size_t n);
 
   explicit Engine(int dev);
   ~Engine();
@@ -222,8 +228,16 @@ struct lk_result {
     std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
     bool hidden = false;                         // tag name dropped by NoisyTagsDropper (tag queries)
     const char* null_value = nullptr;            // the tag's value for dim_null (nullptr: tag dropped)
+    lk::Engine* engine = nullptr;                // bulk export of an engine-dictionary column: its name and the
+    std::string col;                             //   dictionary size of this evaluation
+    size_t dict_n = 0;
   };
   std::vector<TagCol> tcols;
+  // Bulk tag export (lk_result_tag_dictionary): per tag column, dim id -> string (nullptr: tag absent), built on first
+  // use (engine-dictionary columns share the engine's cached table).
+  mutable std::mutex bulk_mu;
+  mutable std::vector<std::shared_ptr<const std::vector<const char*>>> bulk;
+  const std::vector<const char*>* tag_dictionary(size_t c) const;
   // Commons.scala:450-452: a row whose own tags are all absent takes its glob head's queryTags
   std::vector<std::vector<std::pair<size_t, const char*>>> qt_of_glob;   // (tag column, value) per glob
   bool per_glob = false;

@@ -1662,6 +1662,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     tc.dim_null = sc.dim_null;
     tc.dict = &E.dict(sc.name).vals;
     tc.order = sc.order;   // fingerprint-agreed dim: strings read through the sorted order, none copied
+    tc.engine = &E;
+    tc.col = sc.name;
+    tc.dict_n = sc.dict_n;
     if (!sc.restricted && (!sc.exchanged || sc.order)) continue;
     auto& m = tc.local;
     bool shared = false;

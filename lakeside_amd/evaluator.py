@@ -67,19 +67,41 @@ class Result:
 
     @property
     def tags(self) -> List[Dict[str, str]]:
+        """Per-row tag maps, decoded through the bulk export (lk_result_group_ids + lk_result_tag_dictionary: one
+        array read per row and group column, each distinct string decoded once); only the queryTags fallback and
+        a tag query's count column go through lk_result_tag_value, per row."""
         if self._tags is None:
             if self._owner is None:
                 raise ValueError("result closed before its tags were read")
             L = _lib.lib()
             h = self._owner.h
-            out = []
-            for r in range(len(self.ts)):
-                t = {}
-                for c, name in enumerate(self.tag_names):
+            n = len(self.ts)
+            out: List[Dict[str, str]] = [{} for _ in range(n)]
+            ng = L.lk_result_num_group_columns(h) if n else 0
+            own = np.zeros(n, dtype=bool)
+            if ng:
+                gid = np.asarray(_View(self._owner, L.lk_result_group_ids(h), n, "<u4")).astype(np.uint64)
+                for c in range(ng):
+                    stride, nd = ctypes.c_uint64(), ctypes.c_uint64()
+                    p = L.lk_result_tag_dictionary(h, c, ctypes.byref(stride), ctypes.byref(nd))
+                    if not p or nd.value == 0:
+                        continue
+                    d = (gid // np.uint64(stride.value)) % np.uint64(nd.value)
+                    uniq, inv = np.unique(d, return_inverse=True)
+                    text = [ctypes.string_at(p[int(u)]).decode() if p[int(u)] else None for u in uniq]
+                    name = self.tag_names[c]
+                    present = np.array([s is not None for s in text], dtype=bool)[inv]
+                    own |= present
+                    for r in np.nonzero(present)[0].tolist():
+                        out[r][name] = text[inv[r]]
+            for c in range(ng, len(self.tag_names)):
+                name = self.tag_names[c]
+                for r in range(n):
+                    if own[r] and name != "count":
+                        continue   # queryTags apply only to rows whose own tags are all absent
                     v = L.lk_result_tag_value(h, r, c)
                     if v is not None:
-                        t[name] = v.decode()
-                out.append(t)
+                        out[r][name] = v.decode()
             self._tags = out
         return self._tags
 
