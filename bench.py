@@ -122,10 +122,13 @@ def main():
     kept = {}
     t0 = time.time()
     bytes_loaded = 0
+    load_s = 0.0   # disk->HBM load alone (footer + page walk + run tables + remap + upload), synthesis excluded
     with cf.ThreadPoolExecutor(args.gen_workers) as ex:
         for n, fut in enumerate(cf.as_completed([ex.submit(gen, i) for i in mine])):
             i, seg = fut.result()
+            tl = time.perf_counter()
             eng.put_segment_ptr(keys[i], seg.ptr, seg.size)
+            load_s += time.perf_counter() - tl
             bytes_loaded += seg.size
             if keep_cpu:
                 kept[i] = seg
@@ -134,7 +137,8 @@ def main():
             if n % 8 == 7:
                 log(f"rank {rank}: {n + 1}/{S} segments generated + loaded to HBM ({time.time() - t0:.0f}s)")
     log(f"rank {rank}: {S} segments ({bytes_loaded / 1e9:.1f} GB Parquet) resident, HBM cache "
-        f"{eng.segment_bytes / 1e9:.1f} GB, load {time.time() - t0:.0f}s")
+        f"{eng.segment_bytes / 1e9:.1f} GB; Parquet -> HBM load {load_s:.2f} s ({bytes_loaded / load_s / 1e9:.2f} GB/s, "
+        f"{load_s / S * 1e3:.0f} ms/segment; synthesis + load {time.time() - t0:.0f}s)")
 
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(total)]
     if q.get("exemplar"):
@@ -227,12 +231,17 @@ def main():
     # command (scripts/gpu_bench_prof.sh -> scripts/pmc_traffic.py; separate runs, as counters must be collected
     # alone), committed under profiles/ -- read here only when it profiled this query at this size.
     traffic, traffic_src = None, None
-    pmc_file = os.path.join(ROOT, "profiles", f"r02_pmc_{args.query}.json")
-    if os.path.exists(pmc_file):
+    pmc_file = None
+    for rnd in ("r03", "r02"):   # the newest committed PMC summary of this query
+        cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.query}.json")
+        if os.path.exists(cand):
+            pmc_file = cand
+            break
+    if pmc_file:
         pmc = json.load(open(pmc_file))
         if pmc.get("query") == args.query and pmc.get("algorithmic_bytes_per_launch") == alg_bytes:
             traffic = pmc["hbm_bytes_per_launch"]
-            traffic_src = (f"profiles/r02_pmc_{args.query}.json: rocprofv3 --pmc FETCH_SIZE (x{pmc['fetch_correction']} "
+            traffic_src = (f"profiles/{os.path.basename(pmc_file)}: rocprofv3 --pmc FETCH_SIZE (x{pmc['fetch_correction']} "
                            f"gfx950 correction, calibrated in profiles/r02_gather_fetchsize.json) + WRITE_SIZE passes "
                            f"over this bench command; scan kernel {pmc.get('scan_kernel_ms')} ms in that run")
 
@@ -246,6 +255,11 @@ def main():
                        "segments_per_gpu": S, "rows_per_segment": args.rows, "glob_size": 10,
                        "parallelism": f"segment-sharded x{world}" + ((", RCCL table reduce" if args.comm == "rccl" else ", host-transport table reduce (rehearsal)") if world > 1 else "")},
             "datapoints_per_sec": out_rows / (ms_per_step / 1e3),
+            "load": {"what": "Parquet bytes -> HBM segment cache (lk_segment_put: footer, page walk, run tables, "
+                             "dictionary remap, upload), synthetic generation excluded; not in value",
+                     "segments": S, "parquet_bytes": bytes_loaded, "seconds": load_s,
+                     "gbs": bytes_loaded / load_s / 1e9 if load_s else None,
+                     "ms_per_segment": load_s / S * 1e3},
             "rows_scanned": rows_total, "output_rows": out_rows,
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -284,7 +298,11 @@ def cpu_baseline_and_validate(args, q, req, segs, gpu_res):
     from oracle import cpu as lkcpu
     from oracle import dataexpr as dx
     from tests.parity import assert_rows_equal
-    threads = int(os.environ.get("OMP_NUM_THREADS") or os.cpu_count() or 1)
+    # The job's CPU share: the affinity mask, capped by OMP_NUM_THREADS where the pool sets it (the GPU box allots
+    # 16 host cores per GPU and sets OMP_NUM_THREADS=16; os.cpu_count() there is the whole host).
+    affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(affinity, int(omp)) if omp else affinity
     n = len(segs) if args.cpu_sample < 0 else min(len(segs), args.cpu_sample)
     blobs = [(s.ptr, s.size) for s in segs[:n]]
     pr = dx.parse_pushdown(req)
@@ -310,7 +328,9 @@ def cpu_baseline_and_validate(args, q, req, segs, gpu_res):
             validated = {"ok": False, "rows": len(rows), "error": str(e)[:500]}
         log(f"validation: {validated}")
     return ({"value": n * args.rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
-             "cpu_model": _cpu_model(), "nproc": os.cpu_count(),
+             "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
+             "core_limit": (f"OMP_NUM_THREADS={omp} (the job's CPU share on this box; {affinity} CPUs in the affinity "
+                            f"mask, {os.cpu_count()} on the host)") if omp else f"all {affinity} CPUs of the affinity mask",
              "sample": f"{n} of the workload's {len(segs)} segments ({n * args.rows} rows), same query, "
                        f"oracle/cpu/lkcpu.cpp (C++17 + OpenMP restatement, {threads} threads, median of 3)"},
             validated)

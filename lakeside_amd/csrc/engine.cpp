@@ -632,6 +632,13 @@ void build_tiles(Builder& B) {
             t.ts_min = std::min(t.ts_min, x);
             t.ts_max = std::max(t.ts_max, x);
           }
+        } else if (c == ts_col && p.d.kind == PAGE_PLAIN32 && S.cols[c].ptype == pq::INT32) {
+          for (uint32_t v = va; v < ve; v++) {   // INT32 timestamps (BIGINT in a union_by_name glob)
+            int32_t x;
+            memcpy(&x, p.host_vals + size_t(v) * 4, 4);
+            t.ts_min = std::min<int64_t>(t.ts_min, x);
+            t.ts_max = std::max<int64_t>(t.ts_max, x);
+          }
         }
       }
       (void)tile_index;

@@ -225,4 +225,54 @@ def evaluate_push_down_request(engine: Engine, query_id: str, local_parquet: boo
     return res.per_glob(nglobs)
 
 
-__all__ = ["Engine", "Result", "LakesideError", "evaluate_push_down_request", "LK_MERGED", "LK_PER_GLOB_ROWS"]
+def merge_sorted_fold(streams: Sequence[Sequence[Row]], reverse: bool) -> List[Row]:
+    """`sources.fold(Source.empty)(_ mergeSorted _)` under Commons.pushDownResponseOrdering (Commons.scala:116-132,
+    391-392; WorkerApi.scala:169-173): timestamp order (negated when reverseSort); Akka's MergeSorted emits the
+    left head when it is strictly less, the right head otherwise."""
+    out: List[Row] = []
+    for s in streams:
+        m: List[Row] = []
+        i = j = 0
+        while i < len(out) and j < len(s):
+            a, b = out[i][0], s[j][0]
+            if (a > b) if reverse else (a < b):
+                m.append(out[i])
+                i += 1
+            else:
+                m.append(s[j])
+                j += 1
+        m.extend(out[i:])
+        m.extend(s[j:])
+        out = m
+    return out
+
+
+def stream_cached_segment(engine: Engine, payload: str, is_cached, path_of, query_id: str = "") -> List[Row]:
+    """WorkerApi.streamCachedSegment (query-worker/src/main/scala/com/cardinal/queryworker/WorkerApi.scala:121-182),
+    the worker's HTTP entry, over the engine:
+      * the request's segments split into locally cached ones (`is_cached(segment_request)` -- the Caffeine cache
+        lookup, 131-147) and sealed ones;
+      * each non-empty part runs streamDataRoute -> evaluatePushDownRequest (101-119) with localParquet = true
+        (globs of 10) or false (globs of 5); `path_of(segment_request, local)` resolves its Parquet path
+        (Commons.toParquetFilePath, Commons.scala:256-278);
+      * the two streams fold with mergeSorted (169-173): List(lcSource, sealedSource).fold(Source.empty)(_ mergeSorted _).
+    Returns the worker's row stream [(ts, value, tags)] in emission order (wire.worker_sse frames it as SSE).  A part
+    with no segments contributes nothing (no sentinel: that is only evaluatePushDownRequest's own empty case)."""
+    req = json.loads(payload)
+    chart = req.get("baseExpr", {}).get("chart") or {}
+    reverse = bool(req.get("reverseSort", False)) and chart.get("rollup") is None   # pushDownResponseOrdering
+    segs = req.get("segmentRequests", [])
+    parts = ([s for s in segs if is_cached(s)], True), ([s for s in segs if not is_cached(s)], False)
+    streams = []
+    for part, local in parts:
+        if not part:
+            continue
+        sub = dict(req)
+        sub["segmentRequests"] = part
+        per_glob = evaluate_push_down_request(engine, query_id, local, json.dumps(sub), [path_of(s, local) for s in part])
+        streams.append(merge_sorted_fold(per_glob, reverse))   # evaluatePushDownRequest's fold over its globs
+    return merge_sorted_fold(streams, reverse)
+
+
+__all__ = ["Engine", "Result", "LakesideError", "evaluate_push_down_request", "stream_cached_segment",
+           "merge_sorted_fold", "LK_MERGED", "LK_PER_GLOB_ROWS"]

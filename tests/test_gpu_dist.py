@@ -331,6 +331,7 @@ def _worker_regrow(rank, world, port):
     eng = Engine(0)
     try:
         eng.comm_init_host(world, rank)
+        regrown = 0
         for case in _cases():
             paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
             shard = [0] * (len(paths) - 1) + [1]   # uneven: rank 1 scans one segment
@@ -338,7 +339,10 @@ def _worker_regrow(rank, world, port):
             if rank == 0:
                 agg = case["request"]["baseExpr"]["chart"]["aggregation"]
                 assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"regrow {case['name']}")
-                assert res.stats["table"] == "hash", res.stats
+                assert res.stats["table"] == "hash" or res.stats["cells"] == 0, res.stats
+                regrown += res.stats["attempts"] > 1
+        if rank == 0:
+            assert regrown >= 3, regrown   # rank 0 re-ran with larger tables while rank 1 sat at its bound
         dist.barrier()
     finally:
         eng.close()

@@ -93,8 +93,12 @@ def glob_files(tmp_path_factory):
 
 
 def _segs(n, step=60000):
+    """Segment requests whose window covers the four hours the files span."""
     from lakeside_amd import synth
-    return [synth.segment_request(i, step=step, hour=i % 4) for i in range(n)]
+    out = [synth.segment_request(i, step=step, hour=i % 4) for i in range(n)]
+    for s in out:
+        s["startTs"], s["endTs"] = synth.T0, synth.T0 + 4 * synth.HOUR
+    return out
 
 
 @pytest.mark.parametrize("agg", ["sum", "min", "max", "count", "avg"])
@@ -133,12 +137,12 @@ def test_value_type_unions(engine, glob_files, agg):
 
 def test_bad_regex_fails_only_globs_with_the_field(engine, glob_files):
     """A pattern RE2 rejects fails the SQL of the globs where its field exists; in a glob without the field the
-    leaf is the literal `false` (BaseExpr.scala:462-464), so `NOT (regex)` passes every row there."""
+    leaf is the literal `false` (BaseExpr.scala:462-464) and `eq OR regex` keeps the eq rows there."""
     from lakeside_amd import synth
     f = glob_files
     paths = [f["clean0"], f["double1"], f["clean3"]]   # clean3 has no resource.service.name
-    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"),
-            "q2": {"not": synth.leaf(synth.SERVICE, "regex", "svc-(0")}}
+    filt = {"op": "or", "q1": synth.leaf(synth.NAME, "eq", "metric_01"),
+            "q2": synth.leaf(synth.SERVICE, "regex", "svc-(0")}
     req = synth.pushdown(filt, _segs(len(paths)), "sum", [])
     cells, stats = _compare(engine, req, paths, 1, "sum", "bad regex")
     assert cells[0] == [] and cells[1] == [] and cells[2]
@@ -173,3 +177,37 @@ def test_percentiles_over_promoted_values(engine, glob_files):
         got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
                for r in range(len(res)) if int(res.globs[r]) == gi]
         _pct_rows_equal(got, want[gi], 0.95, f"p95 promoted glob {gi}")
+
+
+def test_worker_entry_local_and_sealed_streams(engine, glob_files):
+    """WorkerApi.streamCachedSegment (WorkerApi.scala:121-182): cached segments evaluate with globs of 10, the
+    others with globs of 5, the two streams fold with mergeSorted.  The stream equals the oracle's per-glob rows
+    of both parts as a multiset (globs are not merged in the worker), ascending in time; a missing sealed segment
+    empties only its glob."""
+    from lakeside_amd import synth
+    from lakeside_amd.evaluator import stream_cached_segment
+    from lakeside_amd.wire import parse_sse, worker_sse
+    from oracle import dataexpr as dx
+    f = glob_files
+    files = [f["clean0"], f["double1"], f["clean2"], f["clean3"], f["int64v"], f["missing"], f["clean0"],
+             f["double1"], f["clean2"]]
+    segs = _segs(len(files))
+    for i, s in enumerate(segs):
+        s["segmentId"] = f"seg{i}"
+    cached = {"seg0", "seg2", "seg4", "seg6", "seg8"}
+    by_id = {s["segmentId"]: p for s, p in zip(segs, files)}
+    for agg in ("sum", "max"):
+        req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), segs, agg, [synth.SERVICE])
+        rows = stream_cached_segment(engine, json.dumps(req), lambda s: s["segmentId"] in cached,
+                                     lambda s, local: by_id[s["segmentId"]], "q")
+        assert [r[0] for r in rows] == sorted(r[0] for r in rows)
+        want = []
+        for part, gsize in ([s for s in segs if s["segmentId"] in cached], 10), \
+                           ([s for s in segs if s["segmentId"] not in cached], 5):
+            sub = dict(req, segmentRequests=part)
+            pr = dx.parse_pushdown(json.dumps(sub))
+            for g in dx.evaluate_per_glob(pr, [by_id[s["segmentId"]] for s in part], gsize):
+                want.extend(g)
+        assert_rows_equal(rows, want, agg, f"worker entry {agg}")
+        frames = list(parse_sse("".join(worker_sse(rows, agg))))
+        assert len(frames) == len(rows) and all(fr["message"]["sketchType"] == "map" for fr in frames)
