@@ -12,7 +12,7 @@ LIB     = lakeside_amd/liblakeside_gpu.so
 SYNTH   = lakeside_amd/liblakeside_synth.so
 RELIB   = lakeside_amd/liblakeside_regex.so
 
-HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h

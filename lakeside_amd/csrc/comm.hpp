@@ -43,4 +43,10 @@ struct Piece {
 };
 void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs);
 
+// Agreed dim space of an unrestricted group dimension over the ranks (dims.cpp; collective: every rank calls it in
+// the same order).  The cached union is reused while no rank's dictionary changed (one all-gather); `rebuilt` says a
+// new one was built; `ms` is the agreement's wall time on this rank.
+std::shared_ptr<DimUnion> agree_dim_union(Engine& E, CallCtx& X, const std::string& col, uint32_t dict_n, double& ms,
+                                          bool& rebuilt);
+
 }  // namespace lk

@@ -171,7 +171,10 @@ __device__ __forceinline__ void global_merge(const QParams& P, unsigned long lon
     double old = atomicAdd(&P.hi[cell], hi);   // returning atomic: old is exact -> TwoSum recovers the error
     double s, e;
     two_sum(old, hi, s, e);
-    atomicAdd(&P.lo[cell], lo + e);
+    // The correction is often exactly 0 (integer-valued data, a first add into an empty cell): adding 0.0 is a
+    // no-op, so skip that scattered memory-side atomic (each costs one request to HBM, MI355X_MICROARCH §atomics).
+    const double c = lo + e;
+    if (c != 0.0) atomicAdd(&P.lo[cell], c);
   } else if (AGG == AGG_MIN) {
     atomicMin(&P.ext[cell], ext);
   } else if (AGG == AGG_MAX) {

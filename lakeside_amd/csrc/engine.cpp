@@ -139,6 +139,36 @@ void pinned_release(HostBlock b) {
   }
 }
 
+// LSD radix sort of (key, payload) pairs by the 128-bit key (16-bit digits, lo then hi word: stable, so the result
+// is ordered by (hi, lo)).
+static void radix_sort_keys(std::vector<Key128>& k, std::vector<uint32_t>& v) {
+  const size_t n = k.size();
+  std::vector<Key128> k2(n);
+  std::vector<uint32_t> v2(n);
+  std::vector<size_t> cnt(65537);
+  for (int pass = 0; pass < 8; pass++) {
+    const int word = pass / 4, shift = (pass % 4) * 16;   // lo word first
+    auto digit = [&](const Key128& x) { return size_t(((word ? x.hi : x.lo) >> shift) & 0xffffu); };
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (size_t i = 0; i < n; i++) cnt[digit(k[i]) + 1]++;
+    if (cnt[1] == n) continue;   // one digit value everywhere: the pass is the identity
+    for (size_t d = 1; d <= 65536; d++) cnt[d] += cnt[d - 1];
+    for (size_t i = 0; i < n; i++) {
+      const size_t o = cnt[digit(k[i])]++;
+      k2[o] = k[i];
+      v2[o] = v[i];
+    }
+    k.swap(k2);
+    v.swap(v2);
+  }
+}
+
+Key128 value_key(const std::string& s) {
+  uint64_t h[2];
+  hll::murmur3_x64_128(s.data(), s.size(), 0x6c616b65ull /* "lake" */, h);
+  return Key128{h[0], h[1]};
+}
+
 std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size_t n) {
   std::lock_guard<std::mutex> g(order_mu);
   auto& slot = orders[col];
@@ -151,35 +181,40 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   }
   auto o = std::make_shared<DictOrder>();
   o->n = n;
+  o->keys.resize(n);
   o->perm.resize(n);
-  for (size_t i = 0; i < n; i++) o->perm[i] = uint32_t(i);
-  std::sort(o->perm.begin(), o->perm.end(), [&](uint32_t a, uint32_t b) { return *v[a] < *v[b]; });
-  o->rank.resize(n);
-  // Fingerprint: MurmurHash3_x64_128 over the length-prefixed sorted values, chained over 1 MiB blocks (each block
-  // hashed with the previous digest folded into its seed and into the block's first 16 bytes).  A collision between
-  // two different value sets would merge partial tables under mismatched dim ids; at 128 bits that is not a
-  // practical risk (the former two FNV-1a streams were correlated).
-  uint64_t fp[2] = {uint64_t(n), 0x9e3779b97f4a7c15ull};
-  std::string blk;
-  blk.reserve((1u << 20) + 64);
-  auto flush = [&]() {
-    blk.insert(0, reinterpret_cast<const char*>(fp), 16);
-    hll::murmur3_x64_128(blk.data(), blk.size(), fp[0] ^ (fp[1] << 1), fp);
-    blk.clear();
-  };
-  for (size_t d = 0; d < n; d++) {
-    o->rank[o->perm[d]] = uint32_t(d);
-    const std::string& s = *v[o->perm[d]];
-    const uint32_t len = uint32_t(s.size());
-    blk.append(reinterpret_cast<const char*>(&len), 4);
-    blk.append(s);
-    if (blk.size() >= (1u << 20)) flush();
+  for (size_t i = 0; i < n; i++) {
+    o->keys[i] = value_key(*v[i]);
+    o->perm[i] = uint32_t(i);
   }
-  flush();
+  radix_sort_keys(o->keys, o->perm);
+  for (size_t i = 1; i < n; i++)   // two distinct values of one dictionary on one 128-bit key: refuse, never merge
+    if (o->keys[i] == o->keys[i - 1])
+      throw PlanError(LK_ERR_UNSUPPORTED, "dictionary of " + col + ": 128-bit value-key collision");
+  o->rank.resize(n);
+  for (size_t d = 0; d < n; d++) o->rank[o->perm[d]] = uint32_t(d);
+  // Fingerprint of the value set: MurmurHash3_x64_128 over the sorted keys, chained over 1 MiB blocks.
+  uint64_t fp[2] = {uint64_t(n), 0x9e3779b97f4a7c15ull};
+  const char* base = reinterpret_cast<const char*>(o->keys.data());
+  const size_t bytes = n * sizeof(Key128), blk = size_t(1) << 20;
+  for (size_t off = 0; off < bytes || off == 0; off += blk) {
+    uint64_t h[2];
+    hll::murmur3_x64_128(base + off, std::min(blk, bytes - off), fp[0] ^ (fp[1] << 1), h);
+    fp[0] ^= h[0];
+    fp[1] = fp[1] * 0x100000001b3ull ^ h[1];
+    if (bytes == 0) break;
+  }
   o->fp[0] = fp[0];
   o->fp[1] = fp[1];
   slot = o;
   return slot;
+}
+
+DimUnion::~DimUnion() {
+  if (d_dim_of_gid) {
+    (void)hipSetDevice(device);
+    (void)hipFree(d_dim_of_gid);
+  }
 }
 
 std::shared_ptr<const std::vector<const char*>> Engine::dict_ptrs(const std::string& col, size_t n) {
@@ -214,12 +249,18 @@ const std::vector<const char*>* lk_result::tag_dictionary(size_t c) const {
   if (bulk.size() < tcols.size()) bulk.resize(tcols.size());
   if (bulk[c]) return bulk[c].get();
   const TagCol& t = tcols[c];
+  if (t.shared && !t.null_value && t.shared->size() == t.ndim) {   // an agreed union dim: its shared text table
+    bulk[c] = t.shared;
+    return bulk[c].get();
+  }
   if (t.local.empty() && !t.order && t.engine && !t.null_value && t.dim_null == t.dict_n && t.ndim == t.dict_n + 1) {
     bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n);   // dim id = engine global id: the engine's shared table
     return bulk[c].get();
   }
   auto v = std::make_shared<std::vector<const char*>>(size_t(t.ndim), nullptr);
-  if (!t.local.empty()) {
+  if (t.shared) {
+    for (size_t d = 0; d < v->size() && d < t.shared->size(); d++) (*v)[d] = (*t.shared)[d];
+  } else if (!t.local.empty()) {
     for (size_t d = 0; d < v->size() && d < t.local.size(); d++) (*v)[d] = t.local[d];
   } else if (t.dict) {
     for (size_t d = 0; d < v->size(); d++) {

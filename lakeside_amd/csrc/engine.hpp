@@ -114,14 +114,38 @@ struct CallCtx {
 
 struct Comm;   // comm.cpp
 
-// The sorted order of a column's engine dictionary (its first n values) and a 128-bit fingerprint of the sorted
-// values: ranks holding the same value set agree on a distributed group-dim space by comparing fingerprints
-// instead of exchanging dictionaries.
+// A column's engine dictionary (its first n values) keyed by value hash: every value's 128-bit MurmurHash3 key,
+// sorted, and a fingerprint of the sorted keys.  Ranks agree on a distributed group-dim space through these keys
+// (DimUnion) instead of exchanging and sorting strings; ranks holding the same value set compare fingerprints only.
+struct Key128 {
+  uint64_t hi = 0, lo = 0;
+  bool operator<(const Key128& o) const { return hi != o.hi ? hi < o.hi : lo < o.lo; }
+  bool operator==(const Key128& o) const { return hi == o.hi && lo == o.lo; }
+};
 struct DictOrder {
   size_t n = 0;
-  std::vector<uint32_t> perm;   // dim id (sorted position) -> engine global id
-  std::vector<uint32_t> rank;   // engine global id -> dim id
+  std::vector<Key128> keys;     // sorted (position = dim id of the value set alone)
+  std::vector<uint32_t> perm;   // position -> engine global id
+  std::vector<uint32_t> rank;   // engine global id -> position
   uint64_t fp[2] = {0, 0};
+};
+
+// The agreed group-dim space of an unrestricted dimension over the ranks of a distributed evaluation: the sorted
+// union U of every rank's value keys (dim id = position in U; U's size = NULL's dim id).  Built collectively once
+// per set of rank dictionaries and cached (agree_key = every rank's (n, fingerprint)), so a steady-state query
+// agrees with one small all-gather.
+struct DimUnion {
+  std::string agree_key;
+  size_t dict_n = 0;
+  uint32_t size = 0;                          // |U|
+  std::shared_ptr<const std::vector<uint32_t>> dim_of_gid;   // this rank: engine global id -> dim id
+  std::shared_ptr<std::vector<const char*>> text;            // dim id -> value (nullptr: null-like or unknown here);
+                                                             // [size] = nullptr (NULL); complete on rank 0
+  std::deque<std::string> owned;              // values this rank received from the ranks that hold them
+  std::shared_ptr<const DictOrder> order;
+  uint32_t* d_dim_of_gid = nullptr;           // device copy (the scan's lookup table for this dim)
+  int device = 0;
+  ~DimUnion();
 };
 
 // Process-wide pool of pinned host blocks for result columns (engine.cpp).
@@ -178,6 +202,8 @@ struct Engine {
   std::mutex ptrs_mu;
   std::unordered_map<std::string, std::shared_ptr<const std::vector<const char*>>> ptrs;
   std::shared_ptr<const std::vector<const char*>> dict_ptrs(const std::string& col, size_t n);
+  // distributed group-dim unions, latest per column (DimUnion); used under comm_mu
+  std::unordered_map<std::string, std::shared_ptr<DimUnion>> unions;
 
   explicit Engine(int dev);
   ~Engine();
@@ -224,6 +250,8 @@ struct lk_result {
     unsigned long long stride = 1, ndim = 1;
     uint32_t dim_null = 0;                       // dim id of NULL: tag absent
     std::vector<const char*> local;              // dim id -> string (nullptr: absent); empty: read `dict`
+    std::shared_ptr<const std::vector<const char*>> shared;   // distributed union dim: dim id -> string (DimUnion)
+    std::shared_ptr<const void> keep;            // keeps the strings `shared` points to alive
     const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id, or perm[dim id])
     std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
     bool hidden = false;                         // tag name dropped by NoisyTagsDropper (tag queries)
@@ -289,6 +317,7 @@ struct lk_result {
     if (t.hidden) return nullptr;
     const uint32_t d = uint32_t((gid[row] / t.stride) % t.ndim);
     if (d == t.dim_null) return t.null_value;
+    if (t.shared) return (*t.shared)[d];
     if (!t.local.empty()) return t.local[d];
     const std::string& s = (*t.dict)[t.order ? t.order->perm[d] : d];
     return (s.empty() || s == "null") ? nullptr : s.c_str();

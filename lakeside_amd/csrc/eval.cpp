@@ -55,42 +55,20 @@ struct StrCol {
   uint32_t lbase = 0, lmask = 0, hmask = 0;
   uint32_t dict_n = 0;                    // snapshot of the global dictionary size
   std::vector<int> dim_of_cand_null;      // restricted: candidate positions that collapse to absent
-  // distributed, unrestricted dim: the sorted union of every rank's dictionary (dim id = position), and
-  // this engine's global id -> position
+  // distributed, unrestricted dim: the agreed union of every rank's value keys (dims.cpp; dim id = position)
   bool exchanged = false;
-  std::vector<std::string> uvals;
-  std::vector<uint32_t> upos;
-  std::shared_ptr<const DictOrder> order;   // exchanged by fingerprint: dim id = sorted position (no uvals/upos)
-  // the string of dim id d (d != dim_null); `gd` is this column's engine dictionary (caller holds its lock)
-  const std::string& dim_value(uint32_t d, const GlobalDict& gd) const {
-    return restricted ? cand[d] : !exchanged ? gd.vals[d] : order ? gd.vals[order->perm[d]] : uvals[d];
+  std::shared_ptr<DimUnion> uni;
+  // the value of dim id d (d != dim_null); `gd` is this column's engine dictionary (caller holds its lock).  A union
+  // dim's null-like values read as "" (their tag drops either way).
+  std::string_view dim_value(uint32_t d, const GlobalDict& gd) const {
+    if (restricted) return cand[d];
+    if (!exchanged) return gd.vals[d];
+    const char* t = (*uni->text)[d];
+    return t ? std::string_view(t) : std::string_view();
   }
   // engine global id -> dim id of an exchanged dim
-  uint32_t exchanged_dim(uint32_t gid) const { return order ? order->rank[gid] : upos[gid]; }
+  uint32_t exchanged_dim(uint32_t gid) const { return (*uni->dim_of_gid)[gid]; }
 };
-
-// Length-prefixed encoding of a dictionary's values (the exchange blob) and its inverse.
-std::string pack_strings(const StableStrs& vals, size_t n) {
-  std::string out;
-  for (size_t i = 0; i < n; i++) {
-    const uint32_t len = uint32_t(vals[i].size());
-    out.append(reinterpret_cast<const char*>(&len), 4);
-    out.append(vals[i]);
-  }
-  return out;
-}
-
-void unpack_strings(const std::string& blob, std::vector<std::string>& out) {
-  size_t o = 0;
-  while (o + 4 <= blob.size()) {
-    uint32_t len;
-    memcpy(&len, blob.data() + o, 4);
-    o += 4;
-    if (o + len > blob.size()) throw PlanError(LK_ERR_DEVICE, "internal: truncated dictionary exchange");
-    out.emplace_back(blob, o, len);
-    o += len;
-  }
-}
 
 // union_by_name over a glob's files unifies a numeric column to the widest of its physical types in DuckDB's order
 // INTEGER < BIGINT < FLOAT < DOUBLE (the same rule exemplar.cpp's union_type applies to tag text).  Rank 0: not a
@@ -104,6 +82,11 @@ int value_rank(int ptype) {
     default: return 0;
   }
 }
+int value_type_of_rank(int r) {
+  static const int t[5] = {-1, pq::INT32, pq::INT64, pq::FLOAT, pq::DOUBLE};
+  return t[r < 0 || r > 4 ? 0 : r];
+}
+
 std::string json_escape(const std::string& s) {
   std::string o;
   for (char c : s) {
@@ -117,11 +100,6 @@ std::string json_escape(const std::string& s) {
     }
   }
   return o;
-}
-
-int value_type_of_rank(int r) {
-  static const int t[5] = {-1, pq::INT32, pq::INT64, pq::FLOAT, pq::DOUBLE};
-  return t[r < 0 || r > 4 ? 0 : r];
 }
 
 struct GlobInfo {
@@ -187,6 +165,7 @@ void collect_leaves(const FilterNode* n, std::vector<const FilterNode*>& out) {
 }
 
 bool null_like(const std::string& s) { return s.empty() || s == "null"; }
+bool null_like(std::string_view s) { return s.empty() || s == "null"; }
 
 // Conjuncts of the filter's top-level AND chain (a AND (b AND c) -> a, b, c).
 void conjuncts(const FilterNode* n, std::vector<const FilterNode*>& out) {
@@ -590,6 +569,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // finalization (rekey_minmax).  Everywhere else they can share a cell.
   const bool min_max_nulls = (agg == AGG_MIN || agg == AGG_MAX) && value_nulls;
   const bool collapse_in_table = merged && !min_max_nulls;
+  double dims_ms = 0;      // distributed group-dim agreement (stats)
+  int dims_rebuilt = 0;
   for (size_t s = 0; s < strs.size(); s++) {
     StrCol& sc = strs[s];
     sc.is_dim = (s == 0) || std::find(gbs.begin(), gbs.end(), sc.name) != gbs.end();
@@ -601,44 +582,24 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (!sc.is_dim) continue;
     if (restricted_values(R.filter.get(), sc.name, sc.cand)) {
       sc.restricted = true;
-      sc.ndim = uint32_t(sc.cand.size()) + 1;     // + absent
+      // A passing row holds one of the candidates (the filter is `col IN cand AND ...`): NULL / absent / other
+      // values never reach a cell, so the absent slot is needed only where a null-like candidate ("" / "null")
+      // is itself folded into it.  Without it the dim has cand.size() ids and dim_null is past them (C5: the
+      // name dim of `:eq name` no longer doubles the 10M-group cell space).
+      const bool nl_cand = std::any_of(sc.cand.begin(), sc.cand.end(), [](const std::string& v) { return null_like(v); });
+      sc.ndim = uint32_t(sc.cand.size()) + ((nl_cand || sc.cand.empty()) ? 1u : 0u);
       sc.dim_null = uint32_t(sc.cand.size());
-    } else if (dist && [&] {
-                 // Every rank holds its own engine dictionary; the dim space is the sorted union of all ranks'
-                 // values.  When every rank holds the same value set (same count and 128-bit fingerprint of the
-                 // sorted values) the union is each rank's own sorted dictionary: no exchange, and the sort is
-                 // cached per dictionary size.
-                 sc.order = E.dict_order(sc.name, sc.dict_n);
-                 uint64_t key[3] = {uint64_t(sc.order->n), sc.order->fp[0], sc.order->fp[1]};
-                 const std::string mine(reinterpret_cast<const char*>(key), sizeof(key));
-                 for (const std::string& b : comm_allgather_bytes(E, *X, mine))
-                   if (b != mine) return false;
-                 return true;
-               }()) {
-      if (sc.dict_n + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
-      sc.exchanged = true;
-      sc.ndim = sc.dict_n + 1;
-      sc.dim_null = sc.dict_n;
     } else if (dist) {
-      // Value sets differ: all-gather the dictionaries and build the sorted union (identical on every rank, so
-      // the partial tables align).
-      sc.order.reset();
-      std::string mine;
-      {
-        std::lock_guard<std::mutex> g(gd.mu);
-        mine = pack_strings(gd.vals, sc.dict_n);
-      }
-      for (const std::string& blob : comm_allgather_bytes(E, *X, mine)) unpack_strings(blob, sc.uvals);
-      std::sort(sc.uvals.begin(), sc.uvals.end());
-      sc.uvals.erase(std::unique(sc.uvals.begin(), sc.uvals.end()), sc.uvals.end());
-      if (sc.uvals.size() + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
+      // Every rank holds its own engine dictionary: the dim space is the agreed union of the ranks' value keys
+      // (dims.cpp), cached while no rank's dictionary changes.
+      double ms = 0;
+      bool rebuilt = false;
+      sc.uni = agree_dim_union(E, *X, sc.name, sc.dict_n, ms, rebuilt);
+      dims_ms += ms;
+      dims_rebuilt += rebuilt ? 1 : 0;
       sc.exchanged = true;
-      sc.ndim = uint32_t(sc.uvals.size()) + 1;
-      sc.dim_null = uint32_t(sc.uvals.size());
-      std::lock_guard<std::mutex> g(gd.mu);
-      sc.upos.resize(sc.dict_n);
-      for (uint32_t i = 0; i < sc.dict_n; i++)
-        sc.upos[i] = uint32_t(std::lower_bound(sc.uvals.begin(), sc.uvals.end(), gd.vals[i]) - sc.uvals.begin());
+      sc.ndim = sc.uni->size + 1;
+      sc.dim_null = sc.uni->size;
     } else {
       if (sc.dict_n + 1 > DIM_MASK) throw PlanError(LK_ERR_UNSUPPORTED, "group dimension too large");
       sc.ndim = sc.dict_n + 1;
@@ -666,6 +627,10 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
     need_tab[s] = !sc.leaves.empty() || sc.restricted || sc.exchanged ||
                   (sc.is_dim && collapse_in_table && null_like_present) || (!sc.is_dim && sc.leaves.empty());
+    // an agreed union dim without leaves reads its global id -> dim id table straight from HBM (built once with the
+    // agreement), unless null-like values must fold into dim_null in this query's table
+    if (sc.exchanged && sc.leaves.empty() && !(collapse_in_table && null_like_present) && sc.uni->d_dim_of_gid)
+      need_tab[s] = false;
     if (!need_tab[s]) continue;
     // Leaf outcomes over the column's dictionary (values [0, dict_n) are immutable: StableStrs), cached per
     // (column, leaves) and extended only over values added since: a regex runs once per distinct value.
@@ -1004,8 +969,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     GlobalDict& gd = E.dict(kName);
     std::lock_guard<std::mutex> g(gd.mu);
     for (uint32_t d = 0; d < strs[0].ndim; d++) {
-      const std::string* v = d == strs[0].dim_null ? nullptr : &strs[0].dim_value(d, gd);
-      if (v && !null_like(*v)) order.emplace_back(TagList{{"name", *v}}, d);
+      const std::string_view v = d == strs[0].dim_null ? std::string_view() : strs[0].dim_value(d, gd);
+      if (!null_like(v)) order.emplace_back(TagList{{"name", std::string(v)}}, d);
       else order.emplace_back(qt, d);
     }
     std::sort(order.begin(), order.end());
@@ -1037,6 +1002,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (need_tab[s]) {
       memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
       strp[s].strtab = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
+    } else if (strs[s].exchanged) {
+      strp[s].strtab = strs[s].uni->d_dim_of_gid;   // resident (dims.cpp)
     }
   memcpy(hbuf + o_strp, strp.data(), strp.size() * sizeof(StrParam));
   memset(hbuf + o_flags, 0, 16);
@@ -1378,7 +1345,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         const uint32_t d = uint32_t((keys[i] % ngroups) / (sc.stride ? sc.stride : 1) % sc.ndim);
         if (gi2) kstr[i] += ':';
         if (d != sc.dim_null && sc.stride) {
-          const std::string& v = sc.dim_value(d, gd);
+          const std::string_view v = sc.dim_value(d, gd);
           if (!null_like(v)) kstr[i] += v;
         }
       }
@@ -1437,9 +1404,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         GlobalDict& gd = E.dict(sc.name);
         std::lock_guard<std::mutex> g(gd.mu);
         std::unordered_map<uint32_t, bool> nl;
+        if (drop) continue;   // the name is no key tag (its column is hidden): no group term
         for (size_t i = 0; i < nocc; i++) {
           uint32_t d = uint32_t((cellv[i] % ngroups) / sc.stride % sc.ndim);
-          if (drop) d = sc.dim_null;
           if (d != sc.dim_null) {
             auto it = nl.find(d);
             if (it == nl.end()) it = nl.emplace(d, null_like(sc.dim_value(d, gd))).first;
@@ -1456,7 +1423,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         name_of.resize(nocc);
         for (size_t i = 0; i < nocc; i++) {
           const uint32_t d = uint32_t(kg[i] / strs[0].stride % strs[0].ndim);
-          if (d != strs[0].dim_null) name_of[i] = strs[0].dim_value(d, gd);
+          if (d != strs[0].dim_null) name_of[i] = std::string(strs[0].dim_value(d, gd));
         }
       }
       std::map<std::tuple<uint64_t, uint32_t, unsigned long long>, size_t> at;   // (bucket, glob, key) -> row
@@ -1661,11 +1628,15 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     tc.ndim = sc.ndim;
     tc.dim_null = sc.dim_null;
     tc.dict = &E.dict(sc.name).vals;
-    tc.order = sc.order;   // fingerprint-agreed dim: strings read through the sorted order, none copied
     tc.engine = &E;
     tc.col = sc.name;
     tc.dict_n = sc.dict_n;
-    if (!sc.restricted && (!sc.exchanged || sc.order)) continue;
+    if (sc.exchanged) {   // the agreed union's text table, shared (no copy): 10M-value dims cost nothing here
+      tc.shared = sc.uni->text;
+      tc.keep = sc.uni;
+      continue;
+    }
+    if (!sc.restricted) continue;
     auto& m = tc.local;
     bool shared = false;
     for (size_t c2 = 0; c2 < c && !shared; c2++)   // a groupBy listed twice shares the first column's strings
@@ -1677,10 +1648,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     m.assign(sc.ndim, nullptr);
     for (uint32_t d = 0; d < sc.ndim; d++) {
       if (d == sc.dim_null) continue;
-      std::string& v = sc.restricted ? sc.cand[d] : sc.uvals[d];
+      const std::string& v = sc.cand[d];
       if (null_like(v)) continue;
-      if (sc.restricted) res->owned.push_back(v);              // a few filter candidates: copied
-      else res->owned.push_back(std::move(v));                 // the distributed union (large): moved
+      res->owned.push_back(v);                                 // a few filter candidates: copied
       m[d] = res->owned.back().c_str();
     }
   }
@@ -1718,11 +1688,13 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"general_segments\":%zu,"
            "\"failed_globs\":%zu,\"table\":\"%s\","
-           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\"",
+           "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\","
+           "\"dims_ms\":%.6f,\"dims_rebuilt\":%d",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size() + gsegs.size(), gsegs.size(),
            nfailed, hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
-           !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")));
+           !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")), dims_ms,
+           dims_rebuilt);
   res->stats = buf;
   if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
   res->stats += "}";

@@ -229,9 +229,11 @@ def _worker8(rank, world, port, q):
                     s.free()
             segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
             req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), segs, "sum", gbs))
-            res = eng.eval_pushdown_dist(req, keys, shard, 10)
+            first = eng.eval_pushdown_dist(req, keys, shard, 10)
+            res = eng.eval_pushdown_dist(req, keys, shard, 10)   # the agreed dim space is reused
             if rank == 0:
-                results[name] = (req, res.rows(), res.stats)
+                results[name] = (req, res.rows(), res.stats, first.stats)
+                assert first.rows() == res.rows()
             else:
                 assert len(res) == 0
         dist.barrier()
@@ -256,7 +258,7 @@ def test_dist_world8_host_transport_c4_c5_shapes():
     procs = mp.start_processes(_worker8, args=(8, _free_port(), q), nprocs=8, join=False, start_method="spawn")
     results = q.get(timeout=800)
     procs.join()
-    for name, (req, rows, stats) in results.items():
+    for name, (req, rows, stats, first) in results.items():
         pr = dx.parse_pushdown(req)
         per = 2 if name == "c4" else 1
         n = per * 8
@@ -271,8 +273,13 @@ def test_dist_world8_host_transport_c4_c5_shapes():
         assert_rows_equal(rows, want, "sum", f"world 8 {name}")
         if name == "c5_1m_hash":
             assert stats["table"] == "hash", stats
-        if name == "c5_1h":   # 20M dense cells: key-range all-to-all + per-rank finalize
+        if name == "c5_1h":   # 10M dense cells: key-range all-to-all + per-rank finalize
             assert stats["reduce"] == "keyrange", stats
+        if name != "c4":
+            # every rank's container dictionary differs: the first call builds the union of the ranks' value keys
+            # (dims.cpp), the second reuses it with one small all-gather
+            assert first["dims_rebuilt"] == 1 and stats["dims_rebuilt"] == 0, (first, stats)
+            assert stats["dims_ms"] < 5.0, stats
 
 
 def _worker_err(rank, world, port):
