@@ -20,8 +20,13 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
 #include <algorithm>
 #include <cstring>
+#include <map>
 #include <string>
 
 #include "../../include/lakeside_gpu.h"
@@ -44,16 +49,43 @@ namespace lk {
       throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
   } while (0)
 
+// Shared host result blocks (one node; comm_emit_begin): rank 0 owns a small pool of POSIX shared-memory blocks,
+// every rank maps and registers them with HIP once per block generation, and each rank's GPU writes its key range's
+// result rows straight into rank 0's result over its own PCIe link.
+struct ShmMap {
+  std::string name;
+  uint64_t gen = 0;
+  void* host = nullptr;
+  void* dev = nullptr;
+  size_t cap = 0;
+  bool owner = false;           // rank 0: created (and unlinks) it
+  std::weak_ptr<void> lease;    // rank 0: the result currently holding the block
+  void release() {
+    if (host) {
+      (void)hipHostUnregister(host);
+      (void)hipGetLastError();
+      munmap(host, cap);
+    }
+    if (owner && !name.empty()) shm_unlink(name.c_str());
+    host = dev = nullptr;
+    cap = 0;
+  }
+};
+
 struct Comm {
   int world = 1;
   int rank = 0;
+  std::map<int, ShmMap> shm;    // by block index (rank 0's pool / this rank's mappings of it)
+  uint64_t shm_gen = 0;
   // Loopback (RCCL only, env LK_COMM_LOOPBACK=1 at lk_comm_init; tests): at world 1 every collective still runs --
   // all-gathers through ncclAllGather, the table / record gathers and the key-range pieces through grouped
   // ncclSend/ncclRecv to self -- and the merge reads what came back through RCCL, so the single-GPU box executes
   // (and checks) every RCCL data-path call the 8-GPU run makes.
   bool loopback = false;
   bool active() const { return world > 1 || loopback; }
-  virtual ~Comm() = default;
+  virtual ~Comm() {
+    for (auto& kv : shm) kv.second.release();
+  }
   // host blobs of every rank, rank order
   virtual std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) = 0;
   // `bytes[r]` of device memory from every rank r into rank 0's `recv` at offsets `off[r]` (slot 0 is left
@@ -378,6 +410,100 @@ void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long 
   for (int r = 1; r < C.world; r++)
     HIP_TRY2(launch_merge_records(P, parts + off[size_t(r)] / 8, sz[size_t(r)] / 48, agg, X.stream));
   cap = cap0;
+}
+
+// ---- shared host result blocks ----
+namespace {
+bool map_block(ShmMap& m, const std::string& name, size_t cap, bool create) {
+  const int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
+  if (fd < 0) return false;
+  if (create && ftruncate(fd, off_t(cap)) != 0) {
+    close(fd);
+    shm_unlink(name.c_str());
+    return false;
+  }
+  void* p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) {
+    if (create) shm_unlink(name.c_str());
+    return false;
+  }
+  void* d = nullptr;
+  if (hipHostRegister(p, cap, hipHostRegisterMapped) != hipSuccess || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    (void)hipHostUnregister(p);
+    (void)hipGetLastError();
+    munmap(p, cap);
+    if (create) shm_unlink(name.c_str());
+    return false;
+  }
+  m.name = name;
+  m.host = p;
+  m.dev = d;
+  m.cap = cap;
+  m.owner = create;
+  return true;
+}
+}  // namespace
+
+EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes) {
+  Comm& C = need_comm(E);
+  HIP_TRY2(hipSetDevice(E.device));
+  EmitTarget T;
+  // rank 0 picks a free block of >= bytes (growing or adding one) and announces (pid, block, generation, size)
+  uint64_t hdr[5] = {0, 0, 0, 0, 0};   // ok, pid, block, gen, cap
+  std::shared_ptr<void> lease;
+  if (C.rank == 0) {
+    int pick = -1;
+    for (auto& kv : C.shm)
+      if (kv.second.lease.expired() && kv.second.cap >= bytes) { pick = kv.first; break; }
+    if (pick < 0)
+      for (auto& kv : C.shm)
+        if (kv.second.lease.expired()) { pick = kv.first; break; }
+    if (pick < 0 && C.shm.size() < 8) pick = int(C.shm.size());
+    if (pick >= 0) {
+      ShmMap& m = C.shm[pick];
+      bool ok = m.host && m.cap >= bytes;
+      if (!ok) {
+        const size_t cap = std::max<size_t>((std::max(bytes, m.cap * 3 / 2) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1),
+                                            size_t(2) << 20);
+        m.release();
+        const uint64_t gen = ++C.shm_gen;
+        const std::string name = "/lakeside-" + std::to_string(getpid()) + "-" + std::to_string(pick) + "-" +
+                                 std::to_string(gen);
+        ok = map_block(m, name, cap, true);
+        m.gen = gen;
+      }
+      if (ok) {
+        lease = std::make_shared<int>(0);
+        m.lease = lease;
+        hdr[0] = 1;
+        hdr[1] = uint64_t(getpid());
+        hdr[2] = uint64_t(pick);
+        hdr[3] = m.gen;
+        hdr[4] = m.cap;
+      }
+    }
+  }
+  const std::vector<std::string> all = C.allgather_bytes(E, X, std::string(reinterpret_cast<const char*>(hdr), sizeof(hdr)));
+  if (all.empty() || all[0].size() < sizeof(hdr)) return T;
+  memcpy(hdr, all[0].data(), sizeof(hdr));
+  if (!hdr[0]) return T;   // no block on rank 0: every rank takes the gather path
+  const int b = int(hdr[2]);
+  ShmMap& m = C.shm[b];
+  if (C.rank != 0 && (!m.host || m.gen != hdr[3])) {
+    m.release();
+    const std::string name = "/lakeside-" + std::to_string(hdr[1]) + "-" + std::to_string(b) + "-" + std::to_string(hdr[3]);
+    if (map_block(m, name, size_t(hdr[4]), false)) m.gen = hdr[3];
+  }
+  // a rank that could not map the block reports it with its rows (comm_emit_end fails the call on every rank)
+  T.ok = true;   // uniform over the ranks: rank 0 offered a block
+  T.host = static_cast<uint8_t*>(m.host);
+  T.dev = static_cast<uint8_t*>(m.dev);
+  T.cap = m.cap;
+  T.lease = lease;
+  T.mapped = m.host != nullptr;
+  return T;
 }
 
 }  // namespace lk

@@ -43,6 +43,22 @@ struct Piece {
 };
 void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs);
 
+// Shared host result block of a key-range reduce (one node): rank 0 offers a block of >= `bytes` from its pool of
+// POSIX shared-memory blocks (pinned by every rank once per block generation), every rank maps it, and each rank's
+// GPU writes its range's rows into it at the range's row offset -- the result rows cross all the node's PCIe links
+// at once instead of funnelling through rank 0's.  Collective.  ok == false on every rank when rank 0 has no block
+// (the caller gathers the rows into rank 0 instead); `mapped` == false on a rank that could not map it (the caller
+// reports that in its completion status, which fails the call everywhere).  Rank 0's `lease` keeps the block out of
+// the pool while its result lives.
+struct EmitTarget {
+  bool ok = false, mapped = false;
+  uint8_t* host = nullptr;
+  uint8_t* dev = nullptr;
+  size_t cap = 0;
+  std::shared_ptr<void> lease;
+};
+EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes);
+
 // Agreed dim space of an unrestricted group dimension over the ranks (dims.cpp; collective: every rank calls it in
 // the same order).  The cached union is reused while no rank's dictionary changed (one all-gather); `rebuilt` says a
 // new one was built; `ms` is the agreement's wall time on this rank.

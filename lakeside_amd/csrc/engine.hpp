@@ -296,6 +296,19 @@ struct lk_result {
     }
   }
   std::shared_ptr<void> zeros;                   // glob column of merged rows (see alloc_rows)
+  std::shared_ptr<void> shared_block;            // rows adopted from a shared host block (adopt_rows)
+  // Merged rows another party wrote into a host block laid out [ts | value | group id] x n (the distributed key-range
+  // emit, comm_emit_begin): the result reads them in place and holds `lease` until it is freed.
+  void adopt_rows(void* host, size_t n, std::shared_ptr<void> lease) {
+    auto* b = static_cast<uint8_t*>(host);
+    nrows = n;
+    ts = reinterpret_cast<int64_t*>(b);
+    val = reinterpret_cast<double*>(b + n * 8);
+    gid = reinterpret_cast<uint32_t*>(b + n * 16);
+    zeros = lk::zero_block(n * 4);
+    glob = static_cast<uint32_t*>(zeros.get());
+    shared_block = std::move(lease);
+  }
 
   // exemplar rows: every row's tag strings, materialized ([row][tag column]; nullptr: tag absent)
   bool exemplar = false;

@@ -1186,6 +1186,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // ---- multi-GPU: reduce partial tables to rank 0 over RCCL ----
   uint32_t nrows_out = 0;
   bool rows_done = false;   // key-range path: rank 0's result rows are already in place
+  const char* emit_mode = "local";
   const char* kr_env = getenv("LK_KEYRANGE_MIN_CELLS");
   const uint64_t kr_min = kr_env ? uint64_t(atoll(kr_env)) : (uint64_t(1) << 20);
   const bool keyrange = dist && (comm_world(E) > 1 || comm_loopback(E)) && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
@@ -1256,6 +1257,30 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         }
       }
       if (total_rows >= (uint64_t(1) << 32)) throw PlanError(LK_ERR_UNSUPPORTED, "more than 2^32 result rows");
+      // Parallel emission: every rank's GPU writes its range's rows straight into rank 0's result -- a shared host
+      // block, columns [ts | value | group id] of total_rows each -- at the range's row offset, so the rows cross
+      // every PCIe link of the node at once (otherwise: all rows into rank 0's device, then over its one link).
+      const char* se = getenv("LK_SHM_EMIT");
+      EmitTarget ET;
+      if (total_rows && !(se && *se == '0')) ET = comm_emit_begin(E, *X, size_t(total_rows) * 20);
+      if (ET.ok) {
+        const size_t N = size_t(total_rows), o = size_t(noff[size_t(rank)]);
+        int wst = ET.mapped ? 0 : LK_ERR_DEVICE;
+        if (ET.mapped && mine_n) {
+          if (launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ET.dev) + o,
+                                    reinterpret_cast<double*>(ET.dev + N * 8) + o,
+                                    reinterpret_cast<uint32_t*>(ET.dev + N * 16) + o, nullptr, st) != hipSuccess)
+            wst = LK_ERR_DEVICE;
+        }
+        if (hipStreamSynchronize(st) != hipSuccess) wst = LK_ERR_DEVICE;
+        comm_agree(E, *X, wst, "shared result block: mapping or write failed");   // every range written
+        if (rank == 0) {
+          nrows_out = uint32_t(total_rows);
+          res->adopt_rows(ET.host, N, ET.lease);
+          rows_done = true;
+        }
+        emit_mode = "shared_host_block";
+      } else {
       uint8_t* ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 20 + 64));
       if (mine_n)
         HIP_TRY(launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ob), reinterpret_cast<double*>(ob + size_t(mine_n) * 8),
@@ -1280,6 +1305,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         }
         HIP_TRY(hipStreamSynchronize(st));
         rows_done = true;
+      }
+      emit_mode = "gather_to_root";
       }
     } else {
       comm_reduce_table(E, *X, P, kagg, nc);
@@ -1689,12 +1716,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"general_segments\":%zu,"
            "\"failed_globs\":%zu,\"table\":\"%s\","
            "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\","
-           "\"dims_ms\":%.6f,\"dims_rebuilt\":%d",
+           "\"dims_ms\":%.6f,\"dims_rebuilt\":%d,\"emit\":\"%s\"",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size() + gsegs.size(), gsegs.size(),
            nfailed, hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
            !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")), dims_ms,
-           dims_rebuilt);
+           dims_rebuilt, emit_mode);
   res->stats = buf;
   if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
   res->stats += "}";
