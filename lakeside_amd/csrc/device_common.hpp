@@ -164,10 +164,11 @@ __device__ __forceinline__ void global_merge(const QParams& P, unsigned long lon
     cell = hash_slot(P.hkeys, P.hmask, P.flags, cell);
     if (cell == EMPTY) return;
   }
-  if (!(P.lean & LEAN_NO_ROWS)) atomicAdd(&P.rows[cell], (unsigned long long)rows);
+  if (!(P.lean & (LEAN_NO_ROWS | LEAN_SUM_EXISTS))) atomicAdd(&P.rows[cell], (unsigned long long)rows);
   if (cnt == 0) return;
-  if (!(P.lean & (LEAN_NO_CNT | LEAN_NO_ROWS))) atomicAdd(&P.cnt[cell], (unsigned long long)cnt);
+  if (!(P.lean & (LEAN_NO_CNT | LEAN_NO_ROWS | LEAN_SUM_EXISTS))) atomicAdd(&P.cnt[cell], (unsigned long long)cnt);
   if (AGG == AGG_SUM) {
+    if (P.lean & LEAN_SUM_EXISTS) hi = hi + 0.0;   // never -0.0: the empty cell's marker (layout.hpp)
     double old = atomicAdd(&P.hi[cell], hi);   // returning atomic: old is exact -> TwoSum recovers the error
     double s, e;
     two_sum(old, hi, s, e);

@@ -1022,6 +1022,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
   if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
+  // dense SUM (not AVG, which needs the row counts): existence from the -0.0 marker, no rows atomics at all
+  if (P.lean == LEAN_NO_CNT && agg == AGG_SUM && !hash_mode && !sketch && !ces && !getenv("LK_NO_SUM_EXISTS"))
+    P.lean |= LEAN_SUM_EXISTS;
   // single string column (filter and group dim on `name` only): NULL-free tiles with a small chunk dictionary go
   // to scan_lean (lean_kernel.hpp), the rest to scan_tiles
   // single string column (filter and group dim on `name` only), or name early with every other string column late
@@ -1053,6 +1056,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     P.hmask = hashed ? ncl - 1 : 0;
     HIP_TRY(hipMemsetAsync(tb, 0, ncl * 16, st));
     if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + ncl * 16, 0, ncl * 16, st));
+    if (kagg == AGG_SUM && (P.lean & LEAN_SUM_EXISTS))
+      HIP_TRY(launch_fill_u64(reinterpret_cast<unsigned long long*>(P.hi), ncl, NEG_ZERO_BITS, st));
     if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, ncl * 8, st));
     if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, ncl * 8, st));
     if (hashed) HIP_TRY(hipMemsetAsync(P.hkeys, 0xff, ncl * 8, st));

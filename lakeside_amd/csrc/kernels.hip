@@ -481,7 +481,12 @@ __global__ __launch_bounds__(256) void fixup_table(QParams P, unsigned long long
   const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= nc) return;
   if (P.hkeys && P.hkeys[i] == EMPTY) return;
-  if (P.lean & LEAN_NO_ROWS) {
+  if (P.lean & LEAN_SUM_EXISTS) {
+    const bool e = (unsigned long long)__double_as_longlong(P.hi[i]) != NEG_ZERO_BITS;
+    P.rows[i] = e ? 1ull : 0ull;
+    P.cnt[i] = e ? 1ull : 0ull;
+    if (!e) P.hi[i] = 0.0;
+  } else if (P.lean & LEAN_NO_ROWS) {
     const unsigned long long ident = agg == AGG_MIN ? ~0ull : 0ull;
     const unsigned long long e = P.ext[i] != ident ? 1ull : 0ull;
     P.rows[i] = e;
@@ -517,6 +522,18 @@ hipError_t launch_merge_records(const QParams& P, const unsigned long long* recs
     case AGG_MAX: hipLaunchKernelGGL(merge_records<AGG_MAX>, g, b, 0, st, P, recs, n); break;
     default: hipLaunchKernelGGL(merge_records<AGG_COUNT>, g, b, 0, st, P, recs, n); break;
   }
+  return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void fill_u64(unsigned long long* p, unsigned long long n, unsigned long long v) {
+  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (unsigned long long)gridDim.x * 256)
+    p[i] = v;
+}
+
+hipError_t launch_fill_u64(unsigned long long* p, unsigned long long n, unsigned long long v, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const unsigned long long blocks = std::min<unsigned long long>((n + 255) / 256, 8192);
+  hipLaunchKernelGGL(fill_u64, dim3(uint32_t(blocks)), dim3(256), 0, st, p, n, v);
   return hipGetLastError();
 }
 

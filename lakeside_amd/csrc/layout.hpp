@@ -188,6 +188,12 @@ constexpr uint32_t HASH_MAX_PROBE = 4096;
 // (LEAN_NO_CNT: `cnt` is not accumulated), and for min/max a cell exists iff its extreme left the identity
 // (LEAN_NO_ROWS: neither `rows` nor `cnt` is accumulated).  fixup_table restores both after the scan, so every
 // later stage (merge, finalize) reads an ordinary table.  Each dropped field is one memory-side atomic per flush.
-constexpr uint32_t LEAN_NO_CNT = 1u, LEAN_NO_ROWS = 2u;   // linear probes before a hash-mode insert reports the table full
+constexpr uint32_t LEAN_NO_CNT = 1u, LEAN_NO_ROWS = 2u;
+// LEAN_SUM_EXISTS (dense SUM tables, no NULL value): `hi` starts at -0.0, which no add can produce again (partials
+// are normalized by + 0.0 -- exact for DuckDB's SUM, whose running value starts at +0.0 and so never is -0.0), so
+// "hi != -0.0" says the cell exists and `rows` needs no atomic either: one scattered atomic per flushed cell instead
+// of two or three (fixup_table restores rows / cnt and hi = +0.0 of empty cells).
+constexpr uint32_t LEAN_SUM_EXISTS = 4u;
+constexpr unsigned long long NEG_ZERO_BITS = 0x8000000000000000ull;
 
 }  // namespace lk
