@@ -11,13 +11,14 @@ OBJDIR  = build/obj
 LIB     = lakeside_amd/liblakeside_gpu.so
 SYNTH   = lakeside_amd/liblakeside_synth.so
 RELIB   = lakeside_amd/liblakeside_regex.so
+TXLIB   = lakeside_amd/liblakeside_text.so
 
-HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/jdtoa.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
 
-all: $(LIB) $(SYNTH) $(RELIB)
+all: $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
 
 $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
@@ -34,6 +35,10 @@ $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 $(RELIB): $(SRC)/regex.cpp $(SRC)/regex_capi.cpp $(SRC)/regex.hpp $(SRC)/unicode_tables.inc include/lakeside_regex.h
 	g++ $(CXXFLAGS_HOST) -shared -o $@ $(SRC)/regex.cpp $(SRC)/regex_capi.cpp
 
+# host-only Java 17 number text (CPU differential tests against the oracle's restatement)
+$(TXLIB): $(SRC)/jdtoa.cpp $(SRC)/evalutil.hpp include/lakeside_text.h
+	g++ $(CXXFLAGS_HOST) -I$(ROCM)/include -D__HIP_PLATFORM_AMD__ -shared -o $@ $(SRC)/jdtoa.cpp
+
 $(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
 	g++ -O3 -std=c++17 -fPIC -shared -pthread -Wall -o $@ tools/synth.cpp
 
@@ -44,7 +49,7 @@ asm: $(SRC)/kernels.hip $(HDRS)
 	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(SRC)/scan_$$a.hip -o build/scan_$$a.s; done
 
 clean:
-	rm -rf build $(LIB) $(SYNTH) $(RELIB)
+	rm -rf build $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
 
 
 .PHONY: all clean asm exp-depth3

@@ -39,8 +39,8 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
 bool numeric_op(const std::string& op);
 double normalized_value(const FilterNode& f);
 NumLeaf make_num_leaf(const FilterNode& f, uint32_t col, uint32_t leaf, bool& bad);
-// Java Double.toString / Float.toString text.
-template <class F>
-std::string java_float_text(F d);
+// Java 17 Double.toString / Float.toString text (jdtoa.cpp).
+std::string java_text(double d);
+std::string java_text(float f);
 
 }  // namespace lk

@@ -46,52 +46,6 @@ namespace lk {
       throw PlanError(LK_ERR_DEVICE, std::string("HIP: ") + #x + ": " + hipGetErrorString(_e)); \
   } while (0)
 
-// Java Double.toString / Float.toString text (what DuckDB's JDBC getString returns for DOUBLE / FLOAT): the shortest
-// round-trip digits, laid out plain for 1e-3 <= |x| < 1e7 ("100.0", "0.001") and as d.dddE<exp> otherwise
-// ("1.0E7", "1.5E-4").  (JDK >= 19 prints the shortest digits; JDK 17's FloatingDecimal differs in rare cases.)
-template <class F>
-std::string java_float_text(F d) {
-  if (std::isnan(d)) return "NaN";
-  if (std::isinf(d)) return d > 0 ? "Infinity" : "-Infinity";
-  if (d == F(0)) return std::signbit(d) ? "-0.0" : "0.0";
-  char buf[64];
-  const auto r = std::to_chars(buf, buf + sizeof buf, d, std::chars_format::scientific);
-  std::string sci(buf, r.ptr);
-  const bool neg = sci[0] == '-';
-  if (neg) sci.erase(0, 1);
-  const size_t e = sci.find('e');
-  int exp = std::stoi(sci.substr(e + 1));
-  std::string digits;
-  for (size_t i = 0; i < e; i++)
-    if (sci[i] != '.') digits += sci[i];
-  if (digits.size() == 1) {
-    // Java prints at least two significant digits: the 2-digit decimal closest to the exact value (4.9E-324)
-    const auto r2 = std::to_chars(buf, buf + sizeof buf, std::fabs(d), std::chars_format::scientific, 1);
-    const std::string s2(buf, r2.ptr);
-    const size_t e2 = s2.find('e');
-    exp = std::stoi(s2.substr(e2 + 1));
-    digits = std::string(1, s2[0]) + s2[2];
-    while (digits.size() > 1 && digits.back() == '0') digits.pop_back();
-  }
-  std::string out = neg ? "-" : "";
-  const double a = std::fabs(double(d));
-  if (a >= 1e-3 && a < 1e7) {
-    if (exp >= 0) {
-      std::string ip = digits.substr(0, std::min(digits.size(), size_t(exp) + 1));
-      while (ip.size() < size_t(exp) + 1) ip += '0';
-      std::string fp = digits.size() > size_t(exp) + 1 ? digits.substr(size_t(exp) + 1) : "0";
-      out += ip + "." + fp;
-    } else {
-      out += "0." + std::string(size_t(-exp - 1), '0') + digits;
-    }
-  } else {
-    out += digits.substr(0, 1) + "." + (digits.size() > 1 ? digits.substr(1) : "0") + "E" + std::to_string(exp);
-  }
-  return out;
-}
-template std::string java_float_text<double>(double);
-template std::string java_float_text<float>(float);
-
 namespace {
 
 const char* const kMessage = "_cardinalhq.message";   // Commons.scala:59
@@ -141,8 +95,8 @@ std::string value_text(unsigned long long raw, int pt, int ut) {
   switch (ut) {
     case pq::INT64:
     case pq::INT32: return std::to_string(iv);
-    case pq::FLOAT: return java_float_text(fv);
-    default: return java_float_text(dv);
+    case pq::FLOAT: return java_text(fv);
+    default: return java_text(dv);
   }
 }
 

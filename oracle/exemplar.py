@@ -12,11 +12,12 @@ PushDownAggregatorStage (exemplarsOnly, PushDownAggregatorStage.scala:42,66-68),
 with Akka mergeSorted under pushDownResponseOrdering (Commons.scala:116-132, 391-392).
 
 Choices where the reference is unspecified (same in the GPU path): rows tied on the timestamp keep file order
-(segment position in the glob, then row) -- DuckDB's ORDER BY leaves tie order open; DOUBLE / FLOAT text is
-Java's Double.toString / Float.toString over the shortest round-trip digits (JDK >= 19; JDK 17 differs in rare
-non-shortest cases).  Parity pinned by the restatement only (the reference holds no exemplar result vectors).
+(segment position in the glob, then row) -- DuckDB's ORDER BY leaves tie order open.  DOUBLE / FLOAT text is
+Java 17's Double.toString / Float.toString (the reference's runtime: query-worker/Dockerfile:20, eclipse-temurin:17),
+restated below.  Parity pinned by the restatement only (the reference holds no exemplar result vectors).
 """
-from decimal import Decimal
+import math
+import struct
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -28,58 +29,173 @@ SPAN_NAME = "span.name"           # Commons.scala:71
 SPAN_KIND = "span.kind"           # Commons.scala:72
 
 
-def _java_layout(neg: bool, digits: str, exp: int, mag: float) -> str:
-    """Double.toString layout: digits d1d2... with value d1.d2... x 10^exp."""
+# ----------------------------------------------------------------------------------------------
+# JDK 17 java.lang.Double.toString / Float.toString: sun.misc.FloatingDecimal's BinaryToASCIIBuffer.dtoa +
+# getChars (the reference runs on Java 17, query-worker/Dockerfile:20; JDK 19 replaced this algorithm by a
+# shortest-digit one, which differs for rare values: 2e23 prints 1.9999999999999998E23 here, 2.0E23 on JDK 19).  Restated from the algorithm (Steele & White / dtoa digit generation with a
+# symmetric half-ulp stopping test, an estimated decimal exponent, the "easy" long-integer case, and the int / long /
+# big-integer branches with their own `high` comparisons); Python integers make the big-integer branch exact.
+# No JDK in this image and the reference holds no printed vectors: pinned by the JDK's documented outputs
+# (tests/test_oracle_exemplar.py: Javadoc constants such as Float.MIN_NORMAL = 1.17549435E-38, and the JDK-4511638
+# examples that JDK 17 prints with non-shortest digits).
+# ----------------------------------------------------------------------------------------------
+_N_5_BITS = [0, 3, 5, 7, 10, 12, 14, 17, 19, 21, 24, 26, 28, 31, 33, 35, 38, 40, 42, 45, 47, 49, 52, 54, 56, 59, 61]
+_INSIGNIFICANT = [0, 0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3, 3, 4, 4, 4, 5, 5, 5, 6, 6, 6, 6, 7, 7, 7, 8, 8, 8, 9, 9, 9,
+                  9, 10, 10, 10, 11, 11, 11, 12, 12, 12, 12, 13, 13, 13, 14, 14, 14, 15, 15, 15, 15, 16, 16, 16, 17,
+                  17, 17, 18, 18, 18, 19]
+_EXP_SHIFT = 52
+
+
+def _estimate_dec_exp(fract_bits: int, bin_exp: int) -> int:
+    """FloatingDecimal.estimateDecExp: floor((d2 - 1.5) * 0.289529654 + 0.176091259 + binExp * log10(2))."""
+    d2 = struct.unpack("<d", struct.pack("<Q", (0x3ff << 52) | (fract_bits & ((1 << 52) - 1))))[0]
+    d = (d2 - 1.5) * 0.289529654 + 0.176091259 + float(bin_exp) * 0.301029995663981
+    return math.floor(d)
+
+
+def _dtoa(bin_exp: int, fract_bits: int, n_sig: int):
+    """BinaryToASCIIBuffer.dtoa (isCompatibleFormat = true): (digits, decExponent)."""
+    tail_zeros = (fract_bits & -fract_bits).bit_length() - 1
+    n_fract_bits = _EXP_SHIFT + 1 - tail_zeros
+    n_tiny_bits = max(0, n_fract_bits - bin_exp - 1)
+    if -21 <= bin_exp <= 62 and n_tiny_bits < 27 and n_fract_bits + _N_5_BITS[n_tiny_bits] < 64 and n_tiny_bits == 0:
+        # the easy case: an integer value that fits a long (developLongDigits)
+        insignificant = _INSIGNIFICANT[bin_exp - n_sig - 1] if bin_exp > n_sig and 1 < bin_exp - n_sig - 1 < 64 else 0
+        lvalue = fract_bits << (bin_exp - _EXP_SHIFT) if bin_exp >= _EXP_SHIFT else fract_bits >> (_EXP_SHIFT - bin_exp)
+        dec_exp = 0
+        if insignificant:
+            pow10 = 10 ** insignificant
+            residue = lvalue % pow10
+            lvalue //= pow10
+            dec_exp += insignificant
+            if residue >= (pow10 >> 1):
+                lvalue += 1
+        s = str(lvalue)
+        stripped = s.rstrip("0")
+        dec_exp += len(s) - 1
+        return list(stripped), dec_exp + 1
+    dec_exp = _estimate_dec_exp(fract_bits, bin_exp)
+    b5 = max(0, -dec_exp)
+    b2 = b5 + n_tiny_bits + bin_exp
+    s5 = max(0, dec_exp)
+    s2 = s5 + n_tiny_bits
+    m5 = b5
+    m2 = b2 - n_sig
+    fract_bits >>= tail_zeros
+    b2 -= n_fract_bits - 1
+    common = min(b2, s2)
+    b2 -= common
+    s2 -= common
+    m2 -= common
+    if n_fract_bits == 1:
+        m2 -= 1
+    if m2 < 0:
+        b2 -= m2
+        s2 -= m2
+        m2 = 0
+    b_bits = n_fract_bits + b2 + (_N_5_BITS[b5] if b5 < len(_N_5_BITS) else b5 * 3)
+    ten_s_bits = s2 + 1 + (_N_5_BITS[s5 + 1] if s5 + 1 < len(_N_5_BITS) else (s5 + 1) * 3)
+    small = b_bits < 64 and ten_s_bits < 64        # int / long branches: high = b + m > tens
+    b = fract_bits * 5 ** b5 << b2
+    s = 5 ** s5 << s2
+    m = 5 ** m5 << m2
+    tens = s * 10
+    digits = []
+
+    def is_high(b, m):
+        return b + m > tens if small else b + m >= tens   # FDBigInteger.addAndCmp(B, M) <= 0 in the big branch
+
+    q, b = divmod(b, s)
+    b *= 10
+    m *= 10
+    low, high = b < m, is_high(b, m)
+    if q == 0 and not high:
+        dec_exp -= 1
+    else:
+        digits.append(chr(48 + q))
+    if dec_exp < -3 or dec_exp >= 8:
+        low = high = False
+    while not low and not high:
+        q, b = divmod(b, s)
+        b *= 10
+        m *= 10
+        low, high = b < m, is_high(b, m)
+        digits.append(chr(48 + q))
+    low_diff = 2 * b - tens
+    dec_exponent = dec_exp + 1
+    if high and (not low or low_diff > 0 or (low_diff == 0 and (ord(digits[-1]) & 1))):
+        i = len(digits) - 1
+        while digits[i] == "9" and i > 0:   # roundup()
+            digits[i] = "0"
+            i -= 1
+        if digits[i] == "9":
+            dec_exponent += 1
+            digits[0] = "1"
+        else:
+            digits[i] = chr(ord(digits[i]) + 1)
+    return digits, dec_exponent
+
+
+def _java_chars(neg: bool, digits, dec_exponent: int) -> str:
+    """BinaryToASCIIBuffer.getChars."""
     out = "-" if neg else ""
-    if 1e-3 <= mag < 1e7:
-        if exp >= 0:
-            ip = digits[:exp + 1].ljust(exp + 1, "0")
-            fp = digits[exp + 1:] or "0"
-            return out + ip + "." + fp
-        return out + "0." + "0" * (-exp - 1) + digits
-    return out + digits[0] + "." + (digits[1:] or "0") + "E" + str(exp)
+    nd = len(digits)
+    if 0 < dec_exponent < 8:
+        n = min(nd, dec_exponent)
+        out += "".join(digits[:n])
+        if n < dec_exponent:
+            return out + "0" * (dec_exponent - n) + ".0"
+        return out + "." + ("".join(digits[n:]) if n < nd else "0")
+    if -3 < dec_exponent <= 0:
+        return out + "0." + "0" * (-dec_exponent) + "".join(digits)
+    out += digits[0] + "." + ("".join(digits[1:]) if nd > 1 else "0") + "E"
+    return out + ("-" + str(-dec_exponent + 1) if dec_exponent <= 0 else str(dec_exponent - 1))
 
 
 def java_double_text(x: float) -> str:
-    """java.lang.Double.toString (shortest round-trip digits)."""
-    if x != x:
-        return "NaN"
-    if x in (float("inf"), float("-inf")):
-        return "Infinity" if x > 0 else "-Infinity"
-    if x == 0:
-        return "-0.0" if str(x).startswith("-") else "0.0"
-    t = Decimal(repr(x)).as_tuple()
-    digits = "".join(map(str, t.digits)).rstrip("0") or "0"
-    exp = len(t.digits) - 1 + t.exponent
-    if len(digits) == 1:   # Java prints >= 2 significant digits: the 2-digit decimal closest to the exact value
-        digits, exp = _two_digits(Decimal(x))
-    return _java_layout(bool(t.sign), digits, exp, abs(x))
-
-
-def _two_digits(exact: Decimal):
-    from decimal import Context, ROUND_HALF_EVEN
-    q = Context(prec=2, rounding=ROUND_HALF_EVEN).plus(abs(exact)).as_tuple()
-    d = "".join(map(str, q.digits))
-    return (d.rstrip("0") or "0"), len(q.digits) - 1 + q.exponent
+    """java.lang.Double.toString on JDK 17 (FloatingDecimal.toJavaFormatString)."""
+    bits = struct.unpack("<Q", struct.pack("<d", x))[0]
+    neg = bits >> 63 != 0
+    fract = bits & ((1 << 52) - 1)
+    bexp = (bits >> 52) & 0x7ff
+    if bexp == 0x7ff:
+        return "NaN" if fract else ("-Infinity" if neg else "Infinity")
+    if bexp == 0:
+        if fract == 0:
+            return "-0.0" if neg else "0.0"
+        lz = 64 - fract.bit_length()
+        shift = lz - (63 - _EXP_SHIFT)
+        fract <<= shift
+        bexp = 1 - shift
+        nsig = 64 - lz
+    else:
+        fract |= 1 << 52
+        nsig = 53
+    digits, dexp = _dtoa(bexp - 1023, fract, nsig)
+    return _java_chars(neg, digits, dexp)
 
 
 def java_float_text(x: float) -> str:
-    """java.lang.Float.toString of a float32 value (shortest digits that round-trip as float32)."""
-    f = np.float32(x)
-    if f != f:
-        return "NaN"
-    if np.isinf(f):
-        return "Infinity" if f > 0 else "-Infinity"
-    if f == 0:
-        return "-0.0" if np.signbit(f) else "0.0"
-    sci = np.format_float_scientific(f, unique=True, trim="-")   # e.g. '1.5e-04', '1e+07'
-    mant, e = sci.split("e")
-    neg = mant.startswith("-")
-    digits = mant.lstrip("-").replace(".", "").rstrip("0") or "0"
-    exp = int(e)
-    if len(digits) == 1:
-        digits, exp = _two_digits(Decimal(float(f)))
-    return _java_layout(neg, digits, exp, abs(float(f)))
+    """java.lang.Float.toString on JDK 17 (the same dtoa over the float's 24 significant bits)."""
+    bits = struct.unpack("<I", struct.pack("<f", x))[0]
+    neg = bits >> 31 != 0
+    fract = bits & ((1 << 23) - 1)
+    bexp = (bits >> 23) & 0xff
+    if bexp == 0xff:
+        return "NaN" if fract else ("-Infinity" if neg else "Infinity")
+    if bexp == 0:
+        if fract == 0:
+            return "-0.0" if neg else "0.0"
+        lz = 32 - fract.bit_length()
+        shift = lz - (31 - 23)
+        fract <<= shift
+        bexp = 1 - shift
+        nsig = 32 - lz
+    else:
+        fract |= 1 << 23
+        nsig = 24
+    digits, dexp = _dtoa(bexp - 127, fract << (_EXP_SHIFT - 23), nsig)
+    return _java_chars(neg, digits, dexp)
 
 
 _RANK = {"int32": 1, "int64": 2, "float": 3, "double": 4}
