@@ -31,6 +31,7 @@ __device__ __forceinline__ unsigned long long dbl_order(double d) {
   return (u >> 63) ? ~u : (u | 0x8000000000000000ull);
 }
 __device__ __forceinline__ double order_dbl(unsigned long long o) {
+  if (o == MIN_NAN_ORDER) return __longlong_as_double(0x7ff8000000000000ll);
   unsigned long long u = (o >> 63) ? (o & 0x7fffffffffffffffull) : ~o;
   return __longlong_as_double((long long)u);
 }
@@ -101,6 +102,14 @@ __device__ __forceinline__ void acc_add(Acc& a, bool vvalid, double v) {
     unsigned long long o = dbl_order(v);
     a.ext = o > a.ext ? o : a.ext;
   }
+}
+
+// MIN over a NaN row: flagged so the host can keep cells apart whose sharing would hide an all-NaN DuckDB group from
+// query-api's NaN-absorbing math.min (eval.cpp, REDO_MIN_APART).  NULL-like group values share a cell row by row,
+// so the test is per row (a rarely taken branch; MIN queries only).
+template <int AGG>
+__device__ __forceinline__ void min_nan_check(const QParams& P, bool vvalid, double v) {
+  if (AGG == AGG_MIN && vvalid && v != v) atomicOr(P.flags, FLAG_MIN_NAN);
 }
 
 template <int AGG>
@@ -177,6 +186,7 @@ __device__ __forceinline__ void global_merge(const QParams& P, unsigned long lon
     const double c = lo + e;
     if (c != 0.0) atomicAdd(&P.lo[cell], c);
   } else if (AGG == AGG_MIN) {
+    if (ext == NAN_ORDER) atomicOr(P.flags, FLAG_MIN_NAN);   // the general row scan's rows (see min_nan_check)
     atomicMin(&P.ext[cell], ext);
   } else if (AGG == AGG_MAX) {
     atomicMax(&P.ext[cell], ext);

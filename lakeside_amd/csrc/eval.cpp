@@ -231,10 +231,13 @@ bool noisy_tag(const std::string& t) {
 namespace {
 // Metrics timestamps off the step grid: the scan is re-run at millisecond granularity (see below).
 struct MetricsUnaligned {};
+// Merged MIN with an all-NaN partial cell: the scan is re-run with per-glob cells (see below).
+struct MinNanApart {};
+enum Redo : unsigned { REDO_METRICS_RAW = 1u, REDO_MIN_APART = 2u };
 }  // namespace
 
 static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
-                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, bool metrics_raw);
+                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo);
 
 // Metrics: the worker groups by the raw timestamp (`GROUP BY "_cardinalhq.timestamp"`, BaseExpr.scala:376-394); the
 // segment index picks segments whose frequency equals the step (`metric_seg.frequency_ms = ?`,
@@ -243,15 +246,24 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
 // one bucket per millisecond: the cell key is then the raw timestamp (a sparse key space: the hash table).
 int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
              unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
-  try {
-    return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, false);
-  } catch (const MetricsUnaligned&) {   // thrown before anything is written to *res
-    return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, true);
+  // Both re-runs are thrown before anything is written to *res, and every rank throws them together (agreed flags).
+  unsigned redo = 0;
+  for (;;) {
+    try {
+      return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, redo);
+    } catch (const MetricsUnaligned&) {
+      if (redo & REDO_METRICS_RAW) throw PlanError(LK_ERR_DEVICE, "internal: metrics re-run flagged again");
+      redo |= REDO_METRICS_RAW;
+    } catch (const MinNanApart&) {
+      if (redo & REDO_MIN_APART) throw PlanError(LK_ERR_DEVICE, "internal: min re-run flagged again");
+      redo |= REDO_MIN_APART;
+    }
   }
 }
 
 static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
-                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, bool metrics_raw) {
+                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo) {
+  const bool metrics_raw = (redo & REDO_METRICS_RAW) != 0;
   auto t_start = std::chrono::steady_clock::now();
   // Distributed calls issue collectives: one at a time per engine, in the same order on every rank.  Every call
   // runs on its own context (stream, workspaces), so local calls from several threads overlap.
@@ -567,7 +579,11 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // Merged min/max over values that can be NULL: NULL, "null" and "" group values stay apart in the table
   // (each is its own DuckDB group, and an all-NULL group reads back 0.0); they collapse after per-glob
   // finalization (rekey_minmax).  Everywhere else they can share a cell.
-  const bool min_max_nulls = (agg == AGG_MIN || agg == AGG_MAX) && value_nulls;
+  // MIN re-run (REDO_MIN_APART): a DuckDB group whose values are all NaN has MIN = NaN, and query-api's math.min of
+  // the globs' rows (TimeGroupedSketchAggregator.scala:79-88) -- or of a glob's NULL / "null" / "" groups, which share
+  // an output key -- is then NaN; cells shared in the table would lose it (NaN orders above every number), so they stay
+  // apart exactly as for NULL values.
+  const bool min_max_nulls = (agg == AGG_MIN || agg == AGG_MAX) && (value_nulls || (redo & REDO_MIN_APART));
   const bool collapse_in_table = merged && !min_max_nulls;
   double dims_ms = 0;      // distributed group-dim agreement (stats)
   int dims_rebuilt = 0;
@@ -1182,6 +1198,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (step == 1) throw PlanError(LK_ERR_DEVICE, "internal: metrics timestamp off a 1 ms grid");
     throw MetricsUnaligned{};
   }
+  if ((hflags & FLAG_MIN_NAN) && agg == AGG_MIN && merged && !min_max_nulls) throw MinNanApart{};
   if (hflags & FLAG_CELL_RANGE) throw PlanError(LK_ERR_DEVICE, "internal: bucket outside the table");
   if (hflags & FLAG_HASH_FULL) throw PlanError(LK_ERR_MEMORY, "aggregation hash table full at its bound");
   // DDSketch.accept on NaN / a magnitude beyond the mapping's range throws in the worker's stream stage: the
@@ -1729,6 +1746,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
            dims_rebuilt, emit_mode);
   res->stats = buf;
   if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
+  if (redo) res->stats += ",\"redo\":" + std::to_string(redo);   // 1: metrics at 1 ms, 2: MIN cells kept per glob
   res->stats += "}";
   return LK_OK;
 }

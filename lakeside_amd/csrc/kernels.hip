@@ -235,7 +235,8 @@ __global__ __launch_bounds__(256) void merge_tables(TableRef T, const unsigned l
 // Merged min/max when values can be NULL: per-glob cells keep NULL, "null" and "" group values apart (DuckDB
 // groups them separately and a group whose values are all NULL reads back 0.0, Commons.scala:427); the
 // query-api then merges rows whose tag maps are equal (the three drop to the same map, Commons.scala:433).
-// Re-key every per-glob cell to its collapsed group and fold its SQL value in with exact min/max.
+// Re-key every per-glob cell to its collapsed group and fold its SQL value in with math.min / math.max (order bits;
+// for MIN a NaN value re-orders below everything, MIN_NAN_ORDER, so it absorbs like java.lang.Math.min).
 __global__ __launch_bounds__(256) void rekey_minmax(RParams R) {
   size_t i = size_t(blockIdx.x) * 256 + threadIdx.x;
   if (i >= R.ncells_in) return;
@@ -251,6 +252,7 @@ __global__ __launch_bounds__(256) void rekey_minmax(RParams R) {
   }
   unsigned long long o = b * R.ngroups + cg;
   unsigned long long v = R.in_cnt[i] ? R.in_ext[i] : dbl_order(0.0);
+  if (R.agg == AGG_MIN && v == NAN_ORDER) v = MIN_NAN_ORDER;   // math.min: a NaN row absorbs the merge
   atomicAdd(&R.out_rows[o], rows);
   atomicMax(&R.out_cnt[o], 1ull);
   if (R.agg == AGG_MIN) atomicMin(&R.out_ext[o], v);
@@ -379,7 +381,8 @@ __global__ __launch_bounds__(SB) void runs_write(SParams S, const unsigned long 
           lo += e2 + S.lo[c];
         } else if (S.agg == AGG_MIN || S.agg == AGG_MAX) {
           if (S.rekey) {   // per-glob SQL value: NULL cell -> 0.0 (Commons.scala:427), exact min/max on order bits
-            const unsigned long long v = cc ? S.ext[c] : dbl_order(0.0);
+            unsigned long long v = cc ? S.ext[c] : dbl_order(0.0);
+            if (S.agg == AGG_MIN && v == NAN_ORDER) v = MIN_NAN_ORDER;   // math.min: NaN absorbs
             oext = (S.agg == AGG_MIN) ? (v < oext ? v : oext) : (v > oext ? v : oext);
           } else {
             const double v = cc ? order_dbl(S.ext[c]) : 0.0;

@@ -175,8 +175,12 @@ struct QParams {
 
 enum Flag : uint32_t {
   FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u,
-  FLAG_HASH_GROW = 16u   // host only: this rank's hash table was full below its bound (agreed re-run)
+  FLAG_HASH_GROW = 16u,  // host only: this rank's hash table was full below its bound (agreed re-run)
+  FLAG_MIN_NAN = 32u     // MIN over a NaN value (eval.cpp: merged tables re-run with per-glob cells)
 };
+constexpr unsigned long long NAN_ORDER = 0xfff8000000000000ull;   // dbl_order(NaN)
+// NaN re-ordered below -inf (0: no dbl_order value) where MIN merges rows with math.min semantics (rekey_minmax)
+constexpr unsigned long long MIN_NAN_ORDER = 0ull;
 
 // DDSketch bins (sketches-java LogarithmicMapping, relative accuracy 0.01): bin 0 = zero, 1 + DD_BIAS + i = positive
 // index i, 1 + DD_HALF + DD_BIAS + i = negative index i (|i| < DD_BIAS covers every finite double).

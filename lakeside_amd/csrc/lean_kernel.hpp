@@ -350,6 +350,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       lds_merge<AGG, HASH, false>(L, P, acc);
       acc_reset<AGG>(acc, cell);
     }
+    min_nan_check<AGG>(P, true, v);
     acc_add<AGG>(acc, true, v);
   };
 

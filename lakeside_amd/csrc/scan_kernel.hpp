@@ -672,6 +672,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
         lds_merge<AGG, HASH, SLIM>(L, P, acc);
         acc_reset<AGG>(acc, cell);
       }
+      min_nan_check<AGG>(P, vvalid, v);
       acc_add<AGG>(acc, vvalid, v);
     }
   };

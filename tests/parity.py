@@ -9,7 +9,8 @@ SUM_LIKE = ("sum", "avg")
 
 
 def _key(r):
-    return (r[0], sorted(r[2].items()), r[1])
+    v = r[1]
+    return (r[0], sorted(r[2].items()), (1, 0.0) if v != v else (0, v))   # NaN last: a total order
 
 
 def assert_rows_equal(got, want, agg, label=""):

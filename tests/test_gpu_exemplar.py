@@ -176,3 +176,40 @@ def test_exemplar_errors(engine, tmp_path):
         with pytest.raises(LakesideError):
             engine.eval_pushdown(req, paths, 10, LK_PER_GLOB_ROWS)
         assert evaluate_push_down_request(engine, "q", True, req, paths) == [[]]
+
+
+def test_exemplar_java17_number_text(engine, tmp_path):
+    """DOUBLE / FLOAT tag text is Java 17's Double.toString / Float.toString (the reference runs on
+    eclipse-temurin:17): values whose JDK 17 digits are not the shortest round-trip ones (2e23, 2.82879384806159E17,
+    Float.MIN_NORMAL, integers below 2^63 with noise digits) print as JDK 17 prints them, next to random bit patterns;
+    every row is checked against the oracle and the pinned values against the JDK's documented strings."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    from tests.test_jdtoa import PINNED_DOUBLE, PINNED_FLOAT
+    rng = np.random.default_rng(17)
+    n = 4000
+    dv = rng.integers(0, 2 ** 64, n, dtype=np.uint64).view(np.float64).copy()
+    fv = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32).view(np.float32).copy()
+    dv[: len(PINNED_DOUBLE)] = [v for v, _ in PINNED_DOUBLE]
+    fv[: len(PINNED_FLOAT)] = [v for v, _ in PINNED_FLOAT]
+    dv[len(PINNED_DOUBLE): 200] = rng.integers(1, 2 ** 62, 200 - len(PINNED_DOUBLE)).astype(np.float64)
+    dv[np.isnan(dv)] = 1.5
+    fv[np.isnan(fv)] = 2.5
+    ts = synth.T0 + np.arange(n, dtype=np.int64) * 10
+    t = pa.table({dx.TIMESTAMP: pa.array(ts), dx.VALUE: pa.array(dv),
+                  dx.NAME: pa.array(["m"] * n, pa.string()), "attr.d": pa.array(dv), "attr.f": pa.array(fv)})
+    path = str(tmp_path / "jdk17.parquet")
+    pq.write_table(t, path, compression="NONE", use_dictionary=[dx.NAME],
+                   column_encoding={c: "PLAIN" for c in t.column_names if c != dx.NAME})
+    blobs = [open(path, "rb").read()]
+    req = _request(synth.leaf(dx.NAME, "eq", "m"), 1, limit=n, order="asc", hour=0)
+    got = _check(engine, req, [path], blobs, 1, "jdk17 text")
+    assert len(got) == n
+    texts_d = {got.tags[r]["attr.d"] for r in range(len(got))}
+    texts_f = {got.tags[r]["attr.f"] for r in range(len(got))}
+    for _, s in PINNED_DOUBLE:
+        assert s in texts_d, s
+    for _, s in PINNED_FLOAT:
+        assert s in texts_f, s

@@ -211,3 +211,50 @@ def test_worker_entry_local_and_sealed_streams(engine, glob_files):
         assert_rows_equal(rows, want, agg, f"worker entry {agg}")
         frames = list(parse_sse("".join(worker_sse(rows, agg))))
         assert len(frames) == len(rows) and all(fr["message"]["sketchType"] == "map" for fr in frames)
+
+
+def _write_nan(path, rng, nan_names=(), nan_services=(), n=40_000):
+    """Hour-0 rows with no NULL value; rows of `nan_names` / `nan_services` hold NaN.  The service column mixes NULL,
+    "null" and "" (distinct DuckDB groups that share one output key once their tags are dropped)."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    ts = np.sort(rng.integers(synth.T0, synth.T0 + synth.HOUR, n))
+    names = np.array([f"metric_{k:02d}" for k in rng.integers(0, 3, n)])
+    svc_pool = np.array(["svc-000", "svc-001", "null", ""], dtype=object)
+    svc = svc_pool[rng.integers(0, 4, n)]
+    svc_mask = rng.random(n) < 0.2
+    val = rng.lognormal(0, 2, n)
+    nan_rows = np.isin(names, list(nan_names)) | (np.isin(svc, list(nan_services)) & ~svc_mask)
+    val[nan_rows] = np.nan
+    t = pa.table({dx.TIMESTAMP: pa.array(ts), dx.VALUE: pa.array(val, pa.float64()),
+                  synth.NAME: pa.array(names.tolist(), pa.string()),
+                  synth.SERVICE: pa.array(svc.tolist(), pa.string(), mask=svc_mask)})
+    pq.write_table(t, path, compression="NONE", use_dictionary=[synth.NAME, synth.SERVICE],
+                   column_encoding={dx.TIMESTAMP: "PLAIN", dx.VALUE: "PLAIN"}, row_group_size=20_000)
+    return path
+
+
+def test_merged_min_absorbs_all_nan_glob(engine, tmp_path):
+    """a glob whose group is all NaN has DuckDB MIN = NaN, and query-api's math.min over the globs'
+    rows (TimeGroupedSketchAggregator.scala:79-88) is then NaN.  The merged table would keep only the other glob's
+    number (NaN orders above every number): the kernel flags the all-NaN partial and the query re-runs with per-glob
+    cells (stats redo = 2).  Also inside one glob: the "null" service group all NaN, the NULL group numeric -- one
+    output key once tags drop."""
+    from lakeside_amd import LK_MERGED, synth
+    rng = np.random.default_rng(11)
+    pa_ = _write_nan(str(tmp_path / "nan_a.parquet"), rng, nan_names=("metric_01",))
+    pb = _write_nan(str(tmp_path / "nan_b.parquet"), rng)
+    pc = _write_nan(str(tmp_path / "nan_c.parquet"), rng, nan_services=("null",))
+    for paths, gbs in (([pa_, pb], []), ([pa_, pb], [synth.SERVICE]), ([pc], [synth.SERVICE])):
+        req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(len(paths)), "min", gbs)
+        cells, _ = _compare(engine, req, paths, 1, "min", f"min nan {len(paths)} by {gbs}")
+        merged = engine.eval_pushdown(json.dumps(req), paths, 1, LK_MERGED)
+        vals = [float(merged.values[r]) for r in range(len(merged))]
+        assert any(v != v for v in vals), "expected NaN rows in the merged min"
+        assert merged.stats.get("redo") == 2, merged.stats
+    # max: NaN is DuckDB's greatest value and math.max's absorbing one -- the shared cell already agrees, no re-run
+    req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(2), "max", [])
+    _compare(engine, req, [pa_, pb], 1, "max", "max nan")
+    assert "redo" not in engine.eval_pushdown(json.dumps(req), [pa_, pb], 1, LK_MERGED).stats
