@@ -167,7 +167,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
-    launch_ms, sync_ms, alloc_ms, copy_ms = [], [], [], []
+    launch_ms, sync_ms, alloc_ms, copy_ms, dims_ms = [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -179,6 +179,7 @@ def main():
         sync_ms.append(res.stats.get("sync_ms", 0.0))
         alloc_ms.append(res.stats.get("alloc_ms", 0.0))
         copy_ms.append(res.stats.get("copy_ms", 0.0))
+        dims_ms.append(res.stats.get("dims_ms", 0.0))
         alg_bytes = res.stats.get("algorithmic_bytes", 0)
         out_rows = len(res)
     torch.cuda.synchronize()
@@ -204,7 +205,9 @@ def main():
         f"plan bytes {pbytes / 1e9:.2f} GB/launch -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.3f} of peak); "
         f"SURVEY algorithmic {alg_bytes / 1e9:.2f} GB -> {alg_gbs:.0f} GB/s; {out_rows} output rows; in the call: "
         f"plan {sum(plan_ms) / len(plan_ms):.2f} ms, device {sum(device_ms) / len(device_ms):.2f} ms, "
-        f"total {sum(total_ms) / len(total_ms):.2f} ms")
+        f"total {sum(total_ms) / len(total_ms):.2f} ms" +
+        (f"; group-dim agreement {sum(dims_ms) / len(dims_ms):.2f} ms, reduce {res.stats.get('reduce')}, "
+         f"emit {res.stats.get('emit')}" if world > 1 else ""))
 
     # measured device-to-device copy rate on this GPU (a stream-copy peak beside the spec peak)
     copy_gbs = None
@@ -275,6 +278,9 @@ def main():
             "validated": validated,
             "cpu_baseline": cpu,
         }
+        if world > 1:   # the distributed call's own stages (rank 0): group-dim agreement, table reduce, row emission
+            line["dist"] = {"dims_ms": sum(dims_ms) / len(dims_ms), "reduce": res.stats.get("reduce"),
+                            "emit": res.stats.get("emit"), "comm": args.comm}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

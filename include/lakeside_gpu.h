@@ -47,10 +47,13 @@ enum {
 #define LK_PLAN_BYTES 4u      /* optional, with either: the scan kernel counts the bytes its plan reads
                                  (lk_result_stats "plan_bytes"; measurement only, costs ~5% of scan time) */
 
-/* options_json: {"device": 0, "hbm_budget_bytes": N, "max_calls": 4}; NULL = defaults.
+/* options_json: {"device": 0, "hbm_budget_bytes": N, "max_calls": 4, "dict_compact_min_dead": 1024}; NULL = defaults.
  * hbm_budget_bytes: weight bound of the HBM segment cache (the worker's Caffeine cache weight,
  * query-worker/.../WorkerApi.scala:53-64): inserting past it evicts least-recently-used segments; 0 (default) = no
  * bound, eviction only when HBM runs out.  max_calls: evaluations in flight (one stream each).
+ * dict_compact_min_dead: engine dictionaries (one per column, value -> id) count the cached segments' references to
+ * every id; once evictions leave at least max(live ids, this) ids unreferenced, the next load or evaluation renumbers
+ * the live ids densely first, so group-dim spaces track the cached segments (results keep their strings).
  * Replaces DuckDbConnectionFactory (core/.../utils/DuckDbConnectionFactory.scala:76-114). */
 int lk_engine_create(const char* options_json, lk_engine** out);
 void lk_engine_destroy(lk_engine* e);
@@ -65,6 +68,9 @@ int lk_segment_evict(lk_engine* e, const char* key);
 size_t lk_segment_count(const lk_engine* e);
 /* HBM bytes held by the cache. */
 size_t lk_segment_bytes(const lk_engine* e);
+/* Engine counters as JSON: {"segments", "segment_bytes", "evictions", "dict_compactions",
+ * "dictionaries": {column: {"size", "live", "generation"}}}; valid until the calling thread's next call. */
+const char* lk_engine_stats(lk_engine* e);
 
 /* Mirrors one Commons.evaluatePushDownRequest call (Commons.scala:343-397).
  * push_down_json: PushDownRequest.toJson wire format (core/.../model/SegmentRequest.scala:30-60).

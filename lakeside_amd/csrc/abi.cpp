@@ -2,6 +2,7 @@
 #include <cstring>
 #include <exception>
 #include <new>
+#include <shared_mutex>
 #include <string>
 
 #include "../../include/lakeside_gpu.h"
@@ -64,6 +65,8 @@ int lk_engine_create(const char* options_json, lk_engine** out) {
         lk::Json o = lk::Json::parse(options_json);
         if (const lk::Json* b = o.get("hbm_budget_bytes")) e->e->hbm_budget = size_t(b->as_i64());
         if (const lk::Json* c = o.get("max_calls")) e->e->max_calls = size_t(std::max<int64_t>(1, c->as_i64()));
+        if (const lk::Json* d = o.get("dict_compact_min_dead"))
+          e->e->compact_min_dead = size_t(std::max<int64_t>(1, d->as_i64()));
       }
     } catch (...) {
       delete e;
@@ -76,14 +79,22 @@ int lk_engine_create(const char* options_json, lk_engine** out) {
 
 void lk_engine_destroy(lk_engine* e) { delete e; }
 
+// Loads, evictions and evaluations hold the engine's dictionary generation shared (a compaction renumbers ids only
+// between them); each first compacts dictionaries that evictions have left mostly dead.
 int lk_segment_put(lk_engine* e, const char* key, const uint8_t* data, size_t size) {
   if (!e || !key || (!data && size)) return LK_ERR_ARG;
-  return guarded([&] { return e->e->put_segment(key, data, size); });
+  return guarded([&] {
+    e->e->maybe_compact();
+    std::shared_lock<std::shared_mutex> gen(e->e->gen_mu);
+    return e->e->put_segment(key, data, size);
+  });
 }
 
 int lk_segment_load(lk_engine* e, const char* path) {
   if (!e || !path) return LK_ERR_ARG;
   return guarded([&] {
+    e->e->maybe_compact();
+    std::shared_lock<std::shared_mutex> gen(e->e->gen_mu);
     e->e->get_segment(path, true);
     return LK_OK;
   });
@@ -91,12 +102,52 @@ int lk_segment_load(lk_engine* e, const char* path) {
 
 int lk_segment_evict(lk_engine* e, const char* key) {
   if (!e || !key) return LK_ERR_ARG;
-  std::lock_guard<std::mutex> g(e->e->cache_mu);
-  auto it = e->e->cache.find(key);
-  if (it == e->e->cache.end()) return LK_ERR_ARG;
-  e->e->cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
-  e->e->cache.erase(it);
-  return LK_OK;
+  return guarded([&] {
+    std::shared_lock<std::shared_mutex> gen(e->e->gen_mu);
+    std::shared_ptr<lk::Segment> victim;   // released after cache_mu (~Segment returns its dictionary references)
+    {
+      std::lock_guard<std::mutex> g(e->e->cache_mu);
+      auto it = e->e->cache.find(key);
+      if (it == e->e->cache.end()) return int(LK_ERR_ARG);
+      e->e->cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
+      victim = std::move(it->second);
+      e->e->cache.erase(it);
+    }
+    return int(LK_OK);
+  });
+}
+
+const char* lk_engine_stats(lk_engine* e) {
+  if (!e) return nullptr;
+  lk::Engine& E = *e->e;
+  std::string o = "{";
+  {
+    std::lock_guard<std::mutex> g(E.cache_mu);
+    o += "\"segments\":" + std::to_string(E.cache.size()) + ",\"segment_bytes\":" + std::to_string(E.cache_bytes) +
+         ",\"evictions\":" + std::to_string(E.evictions);
+  }
+  o += ",\"dict_compactions\":" + std::to_string(E.compactions) + ",\"dictionaries\":{";
+  {
+    std::lock_guard<std::mutex> g(E.dict_mu);
+    bool first = true;
+    for (auto& kv : E.dicts) {
+      std::lock_guard<std::mutex> dg(kv.second->mu);
+      if (!first) o += ",";
+      first = false;
+      std::string name;
+      for (char c : kv.first) {
+        if (c == '"' || c == '\\') name += '\\';
+        if (static_cast<unsigned char>(c) >= 0x20) name += c;
+      }
+      o += "\"" + name + "\":{\"size\":" + std::to_string(kv.second->size()) + ",\"live\":" +
+           std::to_string(kv.second->live) + ",\"generation\":" + std::to_string(kv.second->gen) + "}";
+    }
+  }
+  o += "}}";
+  t_err.clear();
+  static thread_local std::string t_stats;
+  t_stats = o;
+  return t_stats.c_str();
 }
 
 size_t lk_segment_count(const lk_engine* e) {
@@ -115,6 +166,8 @@ static int eval_common(lk_engine* e, const char* json, const char* const* paths,
   if (!e || !json || !out || (n_paths && !paths)) return LK_ERR_ARG;
   *out = nullptr;
   return guarded([&] {
+    e->e->maybe_compact();
+    std::shared_lock<std::shared_mutex> gen(e->e->gen_mu);
     auto* r = new lk_result();
     try {
       lk::evaluate(*e->e, json, paths, n_paths, glob_size, flags, shard, dist, r);

@@ -115,7 +115,8 @@ std::shared_ptr<DimUnion> agree_dim_union(Engine& E, CallCtx& X, const std::stri
   std::vector<const std::string*> own(dict_n);
   {
     std::lock_guard<std::mutex> g(gd.mu);
-    for (uint32_t i = 0; i < dict_n; i++) own[i] = &gd.vals[i];   // stable addresses
+    for (uint32_t i = 0; i < dict_n; i++) own[i] = &gd[i];   // stable addresses
+    u->strs = gd.vals;   // `text` points into this block: it outlives a dictionary compaction with the union
   }
   auto text_of = [](const std::string* s) -> const char* {
     return (s->empty() || *s == "null") ? nullptr : s->c_str();

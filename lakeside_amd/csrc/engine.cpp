@@ -72,9 +72,10 @@ static inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) 
 uint32_t GlobalDict::intern(const std::string& s) {
   auto it = ids.find(s);
   if (it != ids.end()) return it->second;
-  uint32_t id = uint32_t(vals.size());
-  vals.push_back(s);
-  ids.emplace(vals.back(), id);
+  uint32_t id = uint32_t(vals->size());
+  vals->push_back(s);
+  refs.push_back(0);
+  ids.emplace(vals->back(), id);
   return id;
 }
 
@@ -177,7 +178,7 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   std::vector<const std::string*> v(n);
   {
     std::lock_guard<std::mutex> dg(gd.mu);
-    for (size_t i = 0; i < n; i++) v[i] = &gd.vals[i];   // stable addresses (StableStrs)
+    for (size_t i = 0; i < n; i++) v[i] = &gd[i];   // stable addresses (StableStrs)
   }
   auto o = std::make_shared<DictOrder>();
   o->n = n;
@@ -217,28 +218,24 @@ DimUnion::~DimUnion() {
   }
 }
 
-std::shared_ptr<const std::vector<const char*>> Engine::dict_ptrs(const std::string& col, size_t n) {
+std::shared_ptr<const std::vector<const char*>> Engine::dict_ptrs(const std::string& col, size_t n,
+                                                                  const std::shared_ptr<StableStrs>& strs) {
   std::lock_guard<std::mutex> g(ptrs_mu);
-  auto& slot = ptrs[col];
-  if (slot && slot->size() == n + 1) return slot;
+  PtrTable& slot = ptrs[col];
+  if (slot.strs != strs) slot = PtrTable{strs, nullptr};   // another generation of the dictionary: start over
+  if (slot.tab && slot.tab->size() == n + 1) return slot.tab;
   auto v = std::make_shared<std::vector<const char*>>(n + 1, nullptr);
   size_t from = 0;
-  if (slot && slot->size() <= n + 1) {   // the dictionary grew: values [0, old n) are unchanged (StableStrs)
-    from = slot->size() - 1;
-    memcpy(v->data(), slot->data(), from * sizeof(const char*));
+  if (slot.tab && slot.tab->size() <= n + 1) {   // the dictionary grew: values [0, old n) are unchanged (StableStrs)
+    from = slot.tab->size() - 1;
+    memcpy(v->data(), slot.tab->data(), from * sizeof(const char*));
   }
-  GlobalDict& gd = dict(col);
-  std::vector<const std::string*> s(n - from);
-  {
-    std::lock_guard<std::mutex> dg(gd.mu);
-    for (size_t i = from; i < n; i++) s[i - from] = &gd.vals[i];   // stable addresses
-  }
-  for (size_t i = from; i < n; i++) {
-    const std::string& x = *s[i - from];
+  for (size_t i = from; i < n; i++) {   // values [0, n) of one block never change (stable addresses)
+    const std::string& x = (*strs)[i];
     (*v)[i] = (x.empty() || x == "null") ? nullptr : x.c_str();
   }
-  slot = v;
-  return slot;
+  if (!slot.tab || slot.tab->size() < v->size()) slot.tab = v;
+  return v;
 }
 
 }  // namespace lk
@@ -253,8 +250,9 @@ const std::vector<const char*>* lk_result::tag_dictionary(size_t c) const {
     bulk[c] = t.shared;
     return bulk[c].get();
   }
-  if (t.local.empty() && !t.order && t.engine && !t.null_value && t.dim_null == t.dict_n && t.ndim == t.dict_n + 1) {
-    bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n);   // dim id = engine global id: the engine's shared table
+  if (t.local.empty() && !t.order && t.engine && t.dict_keep && !t.null_value && t.dim_null == t.dict_n &&
+      t.ndim == t.dict_n + 1) {
+    bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n, t.dict_keep);   // dim id = engine global id: the shared table
     return bulk[c].get();
   }
   auto v = std::make_shared<std::vector<const char*>>(size_t(t.ndim), nullptr);
@@ -281,6 +279,104 @@ GlobalDict& Engine::dict(const std::string& col) {
   auto& p = dicts[col];
   if (!p) p = std::make_unique<GlobalDict>();
   return *p;
+}
+
+void Engine::dict_ref(const std::string& col, const uint32_t* ids, size_t n, int delta) {
+  GlobalDict& gd = dict(col);
+  std::lock_guard<std::mutex> g(gd.mu);
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t id = ids[i];
+    if (id >= gd.refs.size()) continue;
+    if (delta > 0) {
+      if (gd.refs[id]++ == 0) gd.live++;
+    } else if (gd.refs[id] > 0 && --gd.refs[id] == 0) {
+      gd.live--;
+    }
+  }
+}
+
+// Columns whose dead ids (no cached segment references them) are at least as many as the live ones get renumbered.
+// Called at the C ABI before a load or an evaluation takes gen_mu shared.
+void Engine::maybe_compact() {
+  std::vector<std::string> cols;
+  {
+    std::lock_guard<std::mutex> g(dict_mu);
+    for (auto& kv : dicts) {
+      GlobalDict& gd = *kv.second;
+      std::lock_guard<std::mutex> dg(gd.mu);
+      const size_t dead = gd.size() - gd.live;
+      if (dead > 0 && dead >= std::max(gd.live, compact_min_dead)) cols.push_back(kv.first);
+    }
+  }
+  if (cols.empty()) return;
+  std::unique_lock<std::shared_mutex> g(gen_mu);
+  for (auto& c : cols) compact_locked(c);
+}
+
+void Engine::compact_locked(const std::string& col) {
+  GlobalDict& gd = dict(col);
+  std::vector<uint32_t> map;
+  auto nv = std::make_shared<StableStrs>();
+  std::unordered_map<std::string, uint32_t> ids;
+  std::vector<uint32_t> refs;
+  {
+    std::lock_guard<std::mutex> dg(gd.mu);
+    const size_t n = gd.size();
+    if (n - gd.live == 0 || n - gd.live < std::max(gd.live, compact_min_dead)) return;
+    map.assign(n, UINT32_MAX);
+    ids.reserve(gd.live);
+    refs.reserve(gd.live);
+    for (size_t i = 0; i < n; i++) {
+      if (gd.refs[i] == 0) continue;
+      map[i] = uint32_t(nv->size());
+      nv->push_back(gd[i]);
+      ids.emplace(nv->back(), map[i]);
+      refs.push_back(gd.refs[i]);
+    }
+  }
+  // every cached segment's remap of this column: old id -> new id, on the GPU
+  std::vector<std::pair<uint32_t*, size_t>> remaps;
+  {
+    std::lock_guard<std::mutex> g(cache_mu);
+    for (auto& kv : cache) {
+      const int c = kv.second->col_index(col);
+      if (c < 0) continue;
+      const HostCol& hc = kv.second->cols[size_t(c)];
+      if (hc.is_string && hc.nremap) remaps.emplace_back(hc.d_remap, hc.nremap);
+    }
+  }
+  if (!remaps.empty()) {
+    CtxLease X(*this);
+    uint32_t* d_map = static_cast<uint32_t*>(X->workspace("compact_map", map.size() * sizeof(uint32_t)));
+    HIP_CHECK(hipMemcpyAsync(d_map, map.data(), map.size() * sizeof(uint32_t), hipMemcpyHostToDevice, X->stream));
+    for (auto& r : remaps) HIP_CHECK(launch_remap_ids(r.first, r.second, d_map, X->stream));
+    HIP_CHECK(hipStreamSynchronize(X->stream));
+  }
+  {
+    std::lock_guard<std::mutex> dg(gd.mu);
+    gd.live = refs.size();
+    gd.vals = nv;          // results built before keep the old block (lk_result::TagCol::dict_keep / keep)
+    gd.ids.swap(ids);
+    gd.refs.swap(refs);
+    gd.gen++;
+  }
+  // caches keyed by the old ids
+  {
+    std::lock_guard<std::mutex> g(leaf_mu);
+    const std::string pre = col + '\x1f';
+    for (auto it = leaf_cache.begin(); it != leaf_cache.end();)
+      it = it->first.compare(0, pre.size(), pre) == 0 ? leaf_cache.erase(it) : std::next(it);
+  }
+  {
+    std::lock_guard<std::mutex> g(order_mu);
+    orders.erase(col);
+  }
+  {
+    std::lock_guard<std::mutex> g(ptrs_mu);
+    ptrs.erase(col);
+  }
+  unions.erase(col);   // (used under comm_mu by distributed evaluations, none of which runs now)
+  compactions++;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -697,6 +793,18 @@ int Segment::col_index(const std::string& name) const {
 }
 
 Segment::~Segment() {
+  // release this segment's references to dictionary ids (read back from its remaps: the host copy is dropped after
+  // upload), so a later compaction can reclaim ids no cached segment uses any more
+  if (engine && d_meta)
+    for (const HostCol& c : cols) {
+      if (!c.is_string || c.nremap == 0 || !c.d_remap) continue;
+      std::vector<uint32_t> ids(c.nremap);
+      if (hipMemcpy(ids.data(), c.d_remap, c.nremap * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess) {
+        (void)hipGetLastError();
+        continue;   // the ids stay referenced (never reclaimed): safe
+      }
+      engine->dict_ref(c.name, ids.data(), ids.size(), -1);
+    }
   if (d_data) (void)hipFree(d_data);
   if (d_meta) (void)hipFree(d_meta);
 }
@@ -800,6 +908,13 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     for (auto& p : c.pages) c.any_nulls |= p.has_nulls != 0;
   }
   HIP_CHECK(hipMemcpy(S->d_meta, blob.data(), off, hipMemcpyHostToDevice));
+  // the segment now references its chunk dictionaries' ids (released by ~Segment)
+  S->engine = this;
+  for (auto& c : S->cols)
+    if (c.is_string && !c.remap.empty()) {
+      dict_ref(c.name, c.remap.data(), c.remap.size(), +1);
+      c.nremap = c.remap.size();
+    }
   // host copies no longer needed except what the planner reads
   for (auto& c : S->cols) {
     std::vector<RunDesc>().swap(c.runs);
@@ -809,7 +924,7 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
   return S;
 }
 
-size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep) {
+size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep, std::vector<std::shared_ptr<Segment>>* out) {
   size_t freed = 0;
   while (cache_bytes > target_bytes) {
     auto victim = cache.end();
@@ -820,6 +935,7 @@ size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep) {
     cache_bytes -= b;
     freed += b;
     evictions++;
+    if (out) out->push_back(std::move(victim->second));   // destroyed by the caller after cache_mu
     cache.erase(victim);
   }
   return freed;
@@ -851,20 +967,26 @@ int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size
     // The failed hipMalloc left HIP's thread-local last error set: clear it, or the next launch on this thread
     // would report it.
     (void)hipGetLastError();
+    std::vector<std::shared_ptr<Segment>> dead;
     {
       std::lock_guard<std::mutex> g(cache_mu);
       const size_t want = 2 * size + (64u << 20);
-      if (evict_lru_locked(cache_bytes > want ? cache_bytes - want : 0, key) == 0) throw;
+      if (evict_lru_locked(cache_bytes > want ? cache_bytes - want : 0, key, &dead) == 0) throw;
     }
+    dead.clear();   // their HBM is freed (and dictionary references returned) before the retry
     S = build_checked(*this, key, data, size);
   }
   S->last_use = ++use_clock;
+  std::vector<std::shared_ptr<Segment>> dead;   // replaced / evicted segments, destroyed after cache_mu
   std::lock_guard<std::mutex> g(cache_mu);
   auto it = cache.find(key);
-  if (it != cache.end()) cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
+  if (it != cache.end()) {
+    cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
+    dead.push_back(std::move(it->second));
+  }
   cache_bytes += S->data_bytes + S->meta_bytes;
   cache[key] = S;
-  if (hbm_budget) evict_lru_locked(hbm_budget, key);
+  if (hbm_budget) evict_lru_locked(hbm_budget, key, &dead);
   return LK_OK;
 }
 

@@ -9,6 +9,7 @@
 #include <memory>
 #include <mutex>
 #include <set>
+#include <shared_mutex>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -44,12 +45,21 @@ class StableStrs {
 };
 
 // Engine-global dictionary of one column name.  Values get dense ids in first-seen order, at stable
-// addresses (result tag values point into it).
+// addresses (result tag values point into it).  Every id counts the chunk-dictionary entries of cached segments
+// that map to it (`refs`); when evictions have left as many dead ids as live ones, Engine::maybe_compact renumbers
+// the live values densely (old order kept), rewrites the cached segments' remaps and starts a new `vals` block --
+// results keep the block they were built from (shared ownership), so the group-dim space of a long-lived worker
+// tracks its cached segments, as the worker's bounded disk cache does (WorkerApi.scala:53-64).
 struct GlobalDict {
   std::mutex mu;
   std::unordered_map<std::string, uint32_t> ids;
-  StableStrs vals;
+  std::shared_ptr<StableStrs> vals = std::make_shared<StableStrs>();
+  std::vector<uint32_t> refs;              // per id: cached chunk-dictionary entries mapping to it
+  size_t live = 0;                         // ids with refs > 0
+  uint64_t gen = 0;                        // compactions so far (ids are renumbered by each)
   uint32_t intern(const std::string& s);   // caller holds mu
+  size_t size() const { return vals->size(); }
+  const std::string& operator[](size_t i) const { return (*vals)[i]; }
 };
 
 struct HostCol {
@@ -64,6 +74,7 @@ struct HostCol {
   std::vector<RunDesc> runs;              // load-time only
   std::vector<TileCol> tcols;             // load-time only
   std::vector<uint32_t> remap;            // load-time only
+  size_t nremap = 0;                      // entries of d_remap counted in the column dictionary's refs
   PageDesc* d_pages = nullptr;
   RunDesc* d_runs = nullptr;
   TileCol* d_tcols = nullptr;
@@ -85,6 +96,7 @@ struct Segment {
   void* d_meta = nullptr;
   size_t meta_bytes = 0;
   std::atomic<uint64_t> last_use{0};             // LRU clock value of the last lookup (cache eviction)
+  struct Engine* engine = nullptr;               // whose dictionaries its remaps reference (refs released at ~Segment)
   int col_index(const std::string& name) const;
   ~Segment();
 };
@@ -143,6 +155,7 @@ struct DimUnion {
                                                              // [size] = nullptr (NULL); complete on rank 0
   std::deque<std::string> owned;              // values this rank received from the ranks that hold them
   std::shared_ptr<const DictOrder> order;
+  std::shared_ptr<StableStrs> strs;           // the dictionary block `text` points into
   uint32_t* d_dim_of_gid = nullptr;           // device copy (the scan's lookup table for this dim)
   int device = 0;
   ~DimUnion();
@@ -186,9 +199,17 @@ struct Engine {
   std::atomic<uint64_t> use_clock{0};
   size_t evictions = 0;
   // evict LRU segments (never `keep`) until cache_bytes + extra <= budget; caller holds cache_mu
-  size_t evict_lru_locked(size_t target_bytes, const std::string& keep);
+  size_t evict_lru_locked(size_t target_bytes, const std::string& keep, std::vector<std::shared_ptr<Segment>>* out);
   std::mutex dict_mu;
   std::unordered_map<std::string, std::unique_ptr<GlobalDict>> dicts;
+  // Dictionary generations: loads and evaluations hold gen_mu shared (at the C ABI); a compaction holds it exclusive,
+  // so no evaluation or load sees ids change under it.
+  std::shared_mutex gen_mu;
+  size_t compact_min_dead = 1024;                // compact a column once dead ids >= max(live ids, this)
+  size_t compactions = 0;
+  void maybe_compact();                          // caller holds no engine lock
+  void compact_locked(const std::string& col);   // caller holds gen_mu exclusive
+  void dict_ref(const std::string& col, const uint32_t* ids, size_t n, int delta);
   std::mutex leaf_mu;
   std::map<std::string, std::shared_ptr<LeafBits>> leaf_cache;   // key: column \x1f op \x1f values
   std::shared_ptr<LeafBits> leaf_bits(const std::string& key);
@@ -200,8 +221,13 @@ struct Engine {
   // null-like "" / "null", which drop the tag) plus a trailing nullptr (the dim id of NULL).  Cached per column and
   // rebuilt (prefix copied) only when the dictionary has grown, so in steady state a result's dictionary costs O(1).
   std::mutex ptrs_mu;
-  std::unordered_map<std::string, std::shared_ptr<const std::vector<const char*>>> ptrs;
-  std::shared_ptr<const std::vector<const char*>> dict_ptrs(const std::string& col, size_t n);
+  struct PtrTable {
+    std::shared_ptr<StableStrs> strs;              // the dictionary block the pointers point into
+    std::shared_ptr<const std::vector<const char*>> tab;
+  };
+  std::unordered_map<std::string, PtrTable> ptrs;
+  std::shared_ptr<const std::vector<const char*>> dict_ptrs(const std::string& col, size_t n,
+                                                           const std::shared_ptr<StableStrs>& strs);
   // distributed group-dim unions, latest per column (DimUnion); used under comm_mu
   std::unordered_map<std::string, std::shared_ptr<DimUnion>> unions;
 
@@ -253,6 +279,7 @@ struct lk_result {
     std::shared_ptr<const std::vector<const char*>> shared;   // distributed union dim: dim id -> string (DimUnion)
     std::shared_ptr<const void> keep;            // keeps the strings `shared` points to alive
     const lk::StableStrs* dict = nullptr;        // the engine dictionary (dim id = global id, or perm[dim id])
+    std::shared_ptr<lk::StableStrs> dict_keep;   // ... kept alive across dictionary compactions
     std::shared_ptr<const lk::DictOrder> order;  // distributed dims agreed by fingerprint: dim id -> global id
     bool hidden = false;                         // tag name dropped by NoisyTagsDropper (tag queries)
     const char* null_value = nullptr;            // the tag's value for dim_null (nullptr: tag dropped)
@@ -272,6 +299,7 @@ struct lk_result {
   int count_col = -1;                            // tag queries: the "count" tag column
   std::vector<std::string> count_str;            //   and its per-row value (COUNT(*) as text)
   std::deque<std::string> owned;                 // strings not owned by a dictionary
+  std::vector<std::shared_ptr<const void>> keep; // dictionary blocks tag pointers point into
   std::string stats;
   std::vector<std::string> sketches;             // percentile rows: the serialized DDSketch of each row
 

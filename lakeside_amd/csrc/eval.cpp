@@ -62,7 +62,7 @@ struct StrCol {
   // dim's null-like values read as "" (their tag drops either way).
   std::string_view dim_value(uint32_t d, const GlobalDict& gd) const {
     if (restricted) return cand[d];
-    if (!exchanged) return gd.vals[d];
+    if (!exchanged) return gd[d];
     const char* t = (*uni->text)[d];
     return t ? std::string_view(t) : std::string_view();
   }
@@ -593,7 +593,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     GlobalDict& gd = E.dict(sc.name);
     {
       std::lock_guard<std::mutex> g(gd.mu);
-      sc.dict_n = uint32_t(gd.vals.size());
+      sc.dict_n = uint32_t(gd.size());
     }
     if (!sc.is_dim) continue;
     if (restricted_values(R.filter.get(), sc.name, sc.cand)) {
@@ -679,7 +679,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       lb_guard = std::unique_lock<std::mutex>(lb->mu);
       lb->hit.reserve(sc.dict_n);
       for (uint32_t gid = uint32_t(lb->hit.size()); gid < sc.dict_n; gid++) {
-        const std::string& v = gd.vals[gid];
+        const std::string& v = gd[gid];
         uint8_t bits = 0;
         for (size_t j = 0; j < sc.leaves.size(); j++)
           if (!skip_leaf[j] && leaf_eval(*sc.leaves[j], v, res[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
@@ -689,7 +689,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     auto& tab = tabs[s];
     tab.resize(std::max<uint32_t>(sc.dict_n, 1));
     for (uint32_t gid = 0; gid < sc.dict_n; gid++) {
-      const std::string& v = gd.vals[gid];
+      const std::string& v = gd[gid];
       const uint32_t bits = lb ? lb->hit[gid] : 0u;
       uint32_t dim = 0;
       if (sc.is_dim) {
@@ -1050,6 +1050,18 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   P.lean_split = (lean_shape && P.truth && agg != AGG_ROWS && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric) P.lean = 0;   // the general row scan accumulates every table field
+  // scan_lean: a dense table whose group space fits LDS for the few buckets a tile spans is aggregated in the tile's
+  // direct table (lean_kernel.hpp) instead of the LDS hash table: ring_w = the most buckets it holds
+  if (P.lean_split && !hash_mode && !getenv("LK_NO_RING")) {
+    const uint64_t words = lean_ring_words(P.nstr - 1);
+    const bool rows_plane = kagg != AGG_COUNT && !(P.lean & (LEAN_SUM_EXISTS | LEAN_NO_ROWS));
+    const uint32_t cw = (kagg == AGG_SUM ? 2u : 1u) + (rows_plane ? 1u : 0u);
+    const uint64_t w = std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * std::max<uint64_t>(ngroups, 1)));
+    if (w >= 1) {
+      P.ring_w = uint32_t(w);
+      P.ring_cw = cw;
+    }
+  }
   if (sketch) {
     P.sketch = 1;
     P.dd_mult = dd::mapping().multiplier;
@@ -1676,7 +1688,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     tc.stride = sc.stride ? sc.stride : 1;
     tc.ndim = sc.ndim;
     tc.dim_null = sc.dim_null;
-    tc.dict = &E.dict(sc.name).vals;
+    {
+      GlobalDict& gd = E.dict(sc.name);
+      std::lock_guard<std::mutex> g(gd.mu);
+      tc.dict_keep = gd.vals;   // this generation's block stays alive with the result
+      tc.dict = tc.dict_keep.get();
+    }
     tc.engine = &E;
     tc.col = sc.name;
     tc.dict_n = sc.dict_n;

@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <set>
 #include <string>
 #include <unordered_set>
 #include <vector>
@@ -305,7 +306,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     XStr& sc = strs[s];
     GlobalDict& gd = E.dict(sc.name);
     std::lock_guard<std::mutex> dg(gd.mu);
-    sc.dict_n = uint32_t(gd.vals.size());
+    sc.dict_n = uint32_t(gd.size());
     std::string key = sc.name;
     for (const FilterNode* l : sc.leaves) {
       key += '\x1f';
@@ -328,7 +329,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     for (uint32_t gid = uint32_t(lb->hit.size()); gid < sc.dict_n; gid++) {
       uint8_t bits = 0;
       for (size_t j = 0; j < sc.leaves.size(); j++)
-        if (leaf_eval(*sc.leaves[j], gd.vals[gid], rxs[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
+        if (leaf_eval(*sc.leaves[j], gd[gid], rxs[j].get(), sets[j].get())) bits |= uint8_t(1u << j);
       lb->hit.push_back(bits);
     }
     tabs[s].resize(std::max<uint32_t>(sc.dict_n, 1));
@@ -707,6 +708,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   res->tag_names = out_cols;
   res->ex_tags.assign(nsel * ncols, nullptr);
   const size_t vcol = size_t(std::find(out_cols.begin(), out_cols.end(), std::string(kValue)) - out_cols.begin());
+  std::set<const void*> kept;   // dictionary blocks already held by the result
   for (size_t i = 0; i < nsel; i++) {
     const Cand& c = *stream[i];
     const XGlob& g = globs[qseg_glob[c.qseg]];
@@ -728,7 +730,8 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
         if (utype != pq::BYTE_ARRAY) throw PlanError(LK_ERR_UNSUPPORTED, "union_by_name over string and numeric " + name);
         GlobalDict& gd = E.dict(name);
         std::lock_guard<std::mutex> dg(gd.mu);
-        const std::string& s = gd.vals[size_t(raw)];
+        if (kept.insert(gd.vals.get()).second) res->keep.push_back(gd.vals);   // tag text outlives a compaction
+        const std::string& s = gd[size_t(raw)];
         if (!null_like(s)) res->ex_tags[i * ncols + k] = s.c_str();   // Commons.scala:433
       } else {
         res->owned.push_back(value_text(raw, hc.ptype, utype));

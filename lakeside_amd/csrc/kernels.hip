@@ -533,6 +533,19 @@ __global__ __launch_bounds__(256) void fill_u64(unsigned long long* p, unsigned 
     p[i] = v;
 }
 
+// Dictionary compaction (Engine::compact_locked): a segment's chunk remap, old engine id -> new id.
+__global__ __launch_bounds__(256) void remap_ids(uint32_t* p, unsigned long long n, const uint32_t* map) {
+  for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (unsigned long long)gridDim.x * 256)
+    p[i] = map[p[i]];
+}
+
+hipError_t launch_remap_ids(uint32_t* p, unsigned long long n, const uint32_t* map, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  const unsigned long long blocks = std::min<unsigned long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(remap_ids, dim3(uint32_t(blocks)), dim3(256), 0, st, p, n, map);
+  return hipGetLastError();
+}
+
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long n, unsigned long long v, hipStream_t st) {
   if (n == 0) return hipSuccess;
   const unsigned long long blocks = std::min<unsigned long long>((n + 255) / 256, 8192);

@@ -176,6 +176,7 @@ hipError_t launch_merge_tables(const TableRef& T, const unsigned long long* part
                                hipStream_t stream);
 hipError_t launch_scan(const QParams& P, int agg, hipStream_t stream);
 // lean tables: restore the rows / cnt fields the scan did not accumulate (LEAN_* in layout.hpp)
+hipError_t launch_remap_ids(uint32_t* p, unsigned long long n, const uint32_t* map, hipStream_t stream);
 hipError_t launch_fixup_table(const QParams& P, unsigned long long nc, int agg, hipStream_t stream);
 // p[0 .. n) = v (64-bit pattern fill: LEAN_SUM_EXISTS's -0.0)
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long n, unsigned long long v, hipStream_t stream);

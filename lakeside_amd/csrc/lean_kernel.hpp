@@ -25,12 +25,17 @@
 
 namespace lk {
 
-constexpr int LEAN_H = HCAP / 2;                                 // LDS cells (a tile touches few)
+constexpr int LEAN_H = HCAP / 2;                                 // LDS hash cells (hash mode)
 constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a tile, upper bound
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
 constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
 
 constexpr uint32_t LEAN_LIST = 512;                                    // per-wave list of passing rows (late columns)
+#ifndef LK_LEAN_ROWS
+#define LK_LEAN_ROWS 2
+#endif
+constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
+constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -42,14 +47,8 @@ struct LeanRun {            // one run of the name column over the tile (24 B)
   uint32_t cbk;             // chunk index of the run's chunk k = 0 (so k = q - cbk)
 };
 
-template <int NL>
-struct LeanLds {
+struct LeanHash {           // hash mode: the LDS hash table (lds_merge's layout)
   static constexpr int H = LEAN_H;
-  static constexpr int NLA = NL > 0 ? NL : 1;
-  LeanRun runs[RUN_CAP];
-  uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
-  uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
-  uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
   unsigned long long hkey[H];
   uint32_t hrows[H];
   uint32_t hcnt[H];
@@ -57,6 +56,22 @@ struct LeanLds {
   double hlo[H];
   unsigned long long hval[1];
   uint32_t hfull;
+};
+
+template <int NL>
+struct LeanLds {
+  static constexpr int NLA = NL > 0 ? NL : 1;
+  static constexpr uint32_t RW = lean_ring_words(NL);
+  LeanRun runs[RUN_CAP];
+  uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
+  uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
+  uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
+  // The tile's aggregation table: the hash table, or the direct table (the tile's buckets x ngroups cells, P.ring_cw
+  // u64 planes: value (SUM: hi), SUM: lo, rows when the table keeps them)
+  union {
+    LeanHash hs;
+    unsigned long long ring[RW];
+  } agg;
   uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
   // late columns (NL > 0): value runs (+ sentinel), run-block tables, lookup values, the late conjuncts' table
   LRun lruns[NLA][NL > 0 ? RUN_CAP + 1 : 1];
@@ -110,7 +125,7 @@ __device__ __forceinline__ uint32_t lean_code(uint32_t w0, uint32_t w1, uint32_t
 }
 
 template <int AGG, bool HASH, int NL>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void scan_lean(QParams P) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ? 5 : 4))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
   __shared__ LT L;
   const int tid = threadIdx.x;
@@ -129,9 +144,58 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   const uint32_t nr = tc2->nruns, dict_n = tc2->dict_n, bw = tc2->bw;
   const uint32_t vb2 = tc2->vbase, vend = vb2 + nrows;
   const bool count_plan = P.plan_bytes != nullptr;
+  const unsigned long long glob_base = (unsigned long long)Sp->glob_slot * P.nbuckets;
   uint64_t pbytes = 0;
 
-  // ---- prologue: code lookup values, LDS table ----
+  // ---- the tile's aggregation table ----
+  // Direct table (P.ring_w > 0: a dense table whose group space fits LDS, and the tile's buckets -- zone map clipped
+  // to the window -- number at most ring_w): cell (bucket - tbl) * ngroups + group, indexed without key or probe.
+  // Otherwise the LDS hash table (lds_merge).
+  int64_t tbl = 0;
+  uint32_t tspan = 0;   // buckets of the direct table (0: hash table)
+  if (!HASH && P.ring_w) {
+    auto bucket_of = [&](int64_t ts) __attribute__((always_inline)) -> int64_t {   // monotone in ts
+      if (P.metrics) return (ts - P.bucket_base) / P.step;
+      return ((ts - ts % P.step) - P.bucket_base) / P.step;
+    };
+    const int64_t lo_ts = tdp->ts_min > win_lo ? tdp->ts_min : win_lo;
+    const int64_t hi_ts = tdp->ts_max < win_hi - 1 ? tdp->ts_max : win_hi - 1;
+    int64_t bl = bucket_of(lo_ts), bh = bucket_of(hi_ts);
+    bl = bl < 0 ? 0 : bl;
+    bh = bh >= int64_t(P.nbuckets) ? int64_t(P.nbuckets) - 1 : bh;
+    if (bl <= bh && bh - bl < int64_t(P.ring_w)) {
+      tbl = bl;
+      tspan = uint32_t(bh - bl + 1);
+    }
+  }
+  const uint32_t ngr = tspan ? uint32_t(P.ngroups) : 0u;
+  const uint32_t ndir = tspan * ngr;                                // direct cells
+  unsigned long long* const rv = L.agg.ring;                         // value plane (SUM: hi)
+  unsigned long long* const rlo = L.agg.ring + ndir;                 // SUM: lo plane
+  const bool rrows_on = P.ring_cw > (AGG == AGG_SUM ? 2u : 1u);      // the table keeps rows: a rows plane
+  unsigned long long* const rrows = L.agg.ring + (P.ring_cw - 1u) * ndir;
+  // empty value: SUM's -0.0 marker (no rows plane: LEAN_SUM_EXISTS), the MIN / MAX identity, COUNT 0
+  const unsigned long long rident = AGG == AGG_SUM ? (rrows_on ? 0ull : NEG_ZERO_BITS) : (AGG == AGG_MIN ? ~0ull : 0ull);
+  constexpr unsigned long long GBIT = 1ull << 63;                   // register-cell key: a global cell, not a direct one
+  if (tspan) {
+    for (uint32_t x = tid; x < ndir; x += BLOCK) {
+      rv[x] = rident;
+      if (AGG == AGG_SUM) rlo[x] = 0ull;
+      if (rrows_on) rrows[x] = 0ull;
+    }
+  } else {
+    for (int i = tid; i < LeanHash::H; i += BLOCK) {
+      L.agg.hs.hkey[i] = EMPTY;
+      L.agg.hs.hrows[i] = 0;
+      L.agg.hs.hcnt[i] = 0;
+      L.agg.hs.hlo[i] = 0.0;
+      if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.agg.hs.hhi)[i] = ~0ull;
+      else L.agg.hs.hhi[i] = 0.0;
+    }
+    if (tid == 0) L.agg.hs.hfull = 0u;
+  }
+
+  // ---- prologue: code lookup values ----
   {
     const uint32_t* remap = Sp->cols[2].remap + tc2->remap;
     const uint32_t* tab = P.strp[0].strtab;
@@ -140,21 +204,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       L.lut[tid] = tab ? tab[g] : g;
     }
   }
-  for (int i = tid; i < LT::H; i += BLOCK) {
-    L.hkey[i] = EMPTY;
-    L.hrows[i] = 0;
-    L.hcnt[i] = 0;
-    L.hlo[i] = 0.0;
-    if (AGG == AGG_MIN) reinterpret_cast<unsigned long long*>(L.hhi)[i] = ~0ull;
-    else L.hhi[i] = 0.0;
-  }
   if (count_plan) {
     for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) L.lines_t[i] = L.lines_v[i] = 0u;
 #pragma unroll
     for (int k = 0; k < NL; k++)
       for (uint32_t i = tid; i < LEAN_LLINES; i += BLOCK) L.lines_l[k][i] = 0u;
   }
-  if (tid == 0) L.hfull = 0u;
   __syncthreads();
 
   // passing codes: one ballot per wave over the chunk dictionary (Kleene: the leaves' T/F bits of the code)
@@ -281,7 +336,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
   const __amdgpu_buffer_rsrc_t rs1 = make_rsrc(Sp->base + tc1->vals, tc1->vals_len);
   const __amdgpu_buffer_rsrc_t rs2 = make_rsrc(Sp->base + tc2->vals, tc2->vals_len + 16u);
   const uint32_t line_t0 = (vb0 * 8u) >> 7, line_v0 = (vb1 * 8u) >> 7;
-  const unsigned long long glob_base = (unsigned long long)Sp->glob_slot * P.nbuckets;
   const uint32_t stride = P.strp[0].dim_stride;
   const uint32_t npass = uint32_t(__popcll(emask));
   const uint32_t code0 = uint32_t(__builtin_ctzll(emask));
@@ -310,6 +364,33 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
+  // a register cell into the workgroup's table: its ring cell (LDS atomics), HBM (a bucket beyond the tile's ring
+  // slots), or the LDS hash table
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (acc.rows == 0) return;
+    if (!tspan) {
+      lds_merge<AGG, HASH, false>(L.agg.hs, P, acc);
+    } else if (acc.key & GBIT) {
+      global_merge<AGG, HASH>(P, acc.key & ~GBIT, acc.rows, acc.cnt, acc.hi, acc.lo, acc.ext);
+    } else {
+      const uint32_t x = uint32_t(acc.key);
+      if (AGG == AGG_SUM) {
+        const double h = acc.hi + 0.0;   // never -0.0 (the empty marker)
+        const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
+        double s, e;
+        two_sum(old, h, s, e);
+        const double c = acc.lo + e;
+        if (c != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), c);
+      } else if (AGG == AGG_MIN) {
+        atomicMin(rv + x, acc.ext);
+      } else if (AGG == AGG_MAX) {
+        atomicMax(rv + x, acc.ext);
+      } else {
+        atomicAdd(rv + x, (unsigned long long)acc.rows);
+      }
+      if (rrows_on) atomicAdd(rrows + x, (unsigned long long)acc.rows);
+    }
+  };
   // one passing row: bucket (BaseExpr.scala:159-165 window, 163-165 / 376-394 bucket), cell, register cell
   auto row = [&](int64_t ts, double v, uint32_t dim) __attribute__((always_inline)) {
     bool ok = true;
@@ -345,13 +426,155 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         return;
       }
     }
-    const unsigned long long cell = (glob_base + (unsigned long long)b) * P.ngroups + dim;
+    unsigned long long cell;
+    const uint64_t j = uint64_t(b - tbl);
+    if (tspan && j < tspan) {
+      cell = uint32_t(j) * ngr + dim;
+    } else {
+      cell = (glob_base + (unsigned long long)b) * P.ngroups + dim;
+      if (tspan) cell |= GBIT;
+    }
     if (cell != acc.key) {
-      lds_merge<AGG, HASH, false>(L, P, acc);
+      flush();
       acc_reset<AGG>(acc, cell);
     }
     min_nan_check<AGG>(P, true, v);
     acc_add<AGG>(acc, true, v);
+  };
+
+  // N rows per lane (rr[u] live when aa[u]) with group terms dd[u]: late columns (run lookup + packed word, all N
+  // rows' loads in flight together), late filter, timestamp / value gather, accumulate
+  auto rowsN = [&](auto ncst, const uint32_t* rr, const bool* aa, uint32_t* dd) __attribute__((always_inline)) {
+    constexpr int N = decltype(ncst)::value;
+    bool p[N];
+    v2u tt[N], xx[N];
+#pragma unroll
+    for (int u = 0; u < N; u++) {
+      p[u] = aa[u];
+      tt[u] = xx[u] = v2u{0u, 0u};
+    }
+    auto gather = [&]() __attribute__((always_inline)) {   // timestamps / values of the passing rows
+#pragma unroll
+      for (int u = 0; u < N; u++) {
+        if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, p[u] ? (vb0 + rr[u]) * 8u : OOB, 0, 0);
+        if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, p[u] ? (vb1 + rr[u]) * 8u : OOB, 0, 0);
+      }
+    };
+    if constexpr (NL > 0) {
+      // with no late filter leaf every row passes, so the timestamp / value loads go out with the late-column loads
+      v2u lw[N][LT::NLA];
+      uint32_t lm[N][LT::NLA];
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+          lw[u][k] = v2u{0u, 0u};
+          lm[u][k] = 0u;
+        }
+        if (!((lpres >> k) & 1u)) continue;   // uniform
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+          const uint32_t v = lvb[k] + rr[u];
+          const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
+          const LRun lr = L.lruns[k][ri];
+          const bool lt = (lr.off_lit & 0x80000000u) != 0u;
+          const uint32_t bit = (v - lr.start) * lbw[k];
+          const uint32_t byte = (lr.off_lit & 0x7fffffffu) + (bit >> 3);
+          lw[u][k] = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], (aa[u] && lt) ? (byte & ~3u) : OOB, 0, 0);
+          lm[u][k] = lt ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : lr.value;
+          if (count_plan && aa[u] && lt) {   // distinct 128-B lines of the late stream gathered
+            const uint32_t l = ((byte & ~3u) >> 7) - ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
+            if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
+          }
+        }
+      }
+      if (late_trivial) gather();
+      uint32_t T[N], F[N];
+#pragma unroll
+      for (int u = 0; u < N; u++) T[u] = F[u] = 0u;
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        const StrParam sp = P.strp[1 + k];
+        if (!((lpres >> k) & 1u)) {   // absent column: NULL in every row
+#pragma unroll
+          for (int u = 0; u < N; u++) {
+            dd[u] += sp.dim_null * sp.dim_stride;
+            F[u] |= sp.hmask;
+          }
+          continue;
+        }
+        const uint32_t bwk = lbw[k];
+        const uint32_t msk = bwk >= 32u ? ~0u : ((1u << bwk) - 1u);
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+          const uint64_t x = ((uint64_t)lw[u][k].y << 32) | lw[u][k].x;
+          const uint32_t meta = lm[u][k];
+          const uint32_t idx = (meta >> 31) ? uint32_t(x >> (meta & 63u)) & msk : meta;
+          uint32_t packed;
+          if ((llut_on >> k) & 1u) {
+            packed = L.llut[k][idx < LUT_CAP ? idx : 0u];
+          } else {
+            const uint32_t g = aa[u] ? lremap[k][idx] : 0u;
+            packed = sp.strtab ? sp.strtab[g] : g;
+          }
+          const uint32_t bits = (packed >> 24) << sp.lbase;
+          dd[u] += (packed & DIM_MASK) * sp.dim_stride;
+          T[u] |= bits & sp.lmask;
+          F[u] |= ~bits & sp.lmask;
+        }
+      }
+      if (!late_trivial) {
+        const uint32_t lf = Sp->leaf_false;
+#pragma unroll
+        for (int u = 0; u < N; u++) {
+          const uint32_t ix = (T[u] & ~lf) | ((F[u] | lf) << P.nleaves);
+          p[u] = aa[u] && ((L.ltruth[ix >> 5] >> (ix & 31)) & 1u);
+        }
+        gather();
+      }
+    } else {
+      gather();
+    }
+    if (count_plan) {
+      auto mark = [&](uint32_t* bm, uint32_t off, uint32_t line0) __attribute__((always_inline)) {
+        const uint32_t l = (off >> 7) - line0;
+        atomicOr(&bm[l >> 5], 1u << (l & 31u));
+      };
+#pragma unroll
+      for (int u = 0; u < N; u++) {
+        if (!p[u]) continue;
+        if (!one_bucket) mark(L.lines_t, (vb0 + rr[u]) * 8u, line_t0);
+        if (AGG != AGG_COUNT) mark(L.lines_v, (vb1 + rr[u]) * 8u, line_v0);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < N; u++)
+      if (p[u])
+        row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x)), dd[u]);
+  };
+  // Late columns: each wave's passing rows wait in its LDS list (a ring of LEAN_LIST entries, tile row | code << 16)
+  // until a full trip of LEAN_TRIP rows -- LEAN_ROWS per lane, every lane busy, all their late-column loads and then
+  // all their value loads in flight together -- is ready, across the tile's rounds; the rest drains at the tile's end.
+  uint32_t lhead = 0, ltail = 0;   // wave-uniform list positions (mod LEAN_LIST)
+  uint32_t* const wl = L.wlist[tid >> 6];
+  auto list_trip = [&](uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
+    uint32_t rr[LEAN_ROWS], dd[LEAN_ROWS];
+    bool aa[LEAN_ROWS];
+#pragma unroll
+    for (int u = 0; u < LEAN_ROWS; u++) {
+      const uint32_t i = uint32_t(lane) + 64u * uint32_t(u);
+      aa[u] = i < n;
+      const uint32_t x = aa[u] ? wl[(lhead + i) & (LEAN_LIST - 1u)] : 0u;
+      rr[u] = x & 0xffffu;
+      dd[u] = npass > 1 ? (L.lut[x >> 16] & DIM_MASK) * stride : dim_u;
+    }
+    rowsN(std::integral_constant<int, LEAN_ROWS>{}, rr, aa, dd);
+    lhead += n;
+  };
+  auto wave_sync = [&]() __attribute__((always_inline)) {   // the wave's list writes / reads are ordered
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
   auto body = [&](auto bwc) __attribute__((always_inline)) {
@@ -499,108 +722,6 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
           m = 0;
         }
       }
-      // two rows (r1 live when a1, r2 when two) with group terms d1, d2: late columns, gather, accumulate
-      auto rows2 = [&](uint32_t r1, uint32_t r2, bool a1, bool two, uint32_t d1, uint32_t d2) __attribute__((always_inline)) {
-        bool p1 = a1, p2 = two;
-        v2u t1 = v2u{0u, 0u}, t2 = v2u{0u, 0u}, x1 = v2u{0u, 0u}, x2 = v2u{0u, 0u};
-        auto gather = [&]() __attribute__((always_inline)) {   // timestamps / values of the passing rows
-          if (!one_bucket) {
-            t1 = __builtin_amdgcn_raw_buffer_load_b64(rs0, p1 ? (vb0 + r1) * 8u : OOB, 0, 0);
-            t2 = __builtin_amdgcn_raw_buffer_load_b64(rs0, p2 ? (vb0 + r2) * 8u : OOB, 0, 0);
-          }
-          if (AGG != AGG_COUNT) {
-            x1 = __builtin_amdgcn_raw_buffer_load_b64(rs1, p1 ? (vb1 + r1) * 8u : OOB, 0, 0);
-            x2 = __builtin_amdgcn_raw_buffer_load_b64(rs1, p2 ? (vb1 + r2) * 8u : OOB, 0, 0);
-          }
-        };
-        if constexpr (NL > 0) {
-          // late columns of both rows: run lookup + packed-word load (in flight together); with no late filter
-          // leaf every row passes, so the timestamp / value loads go out with them
-          v2u lw1[LT::NLA], lw2[LT::NLA];
-          uint32_t lm1[LT::NLA], lm2[LT::NLA];
-#pragma unroll
-          for (int k = 0; k < NL; k++) {
-            lw1[k] = lw2[k] = v2u{0u, 0u};
-            lm1[k] = lm2[k] = 0u;
-            if (!((lpres >> k) & 1u)) continue;   // uniform
-            auto issue = [&](uint32_t r, bool live, v2u& w, uint32_t& meta) __attribute__((always_inline)) {
-              const uint32_t v = lvb[k] + r;
-              const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
-              const LRun rr = L.lruns[k][ri];
-              const bool lt = (rr.off_lit & 0x80000000u) != 0u;
-              const uint32_t bit = (v - rr.start) * lbw[k];
-              const uint32_t byte = (rr.off_lit & 0x7fffffffu) + (bit >> 3);
-              w = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], (live && lt) ? (byte & ~3u) : OOB, 0, 0);
-              meta = lt ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : rr.value;
-              if (count_plan && live && lt) {   // distinct 128-B lines of the late stream gathered
-                const uint32_t l = ((byte & ~3u) >> 7) - ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
-                if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
-              }
-            };
-            issue(r1, a1, lw1[k], lm1[k]);
-            issue(r2, two, lw2[k], lm2[k]);
-          }
-          if (late_trivial) gather();
-          uint32_t T1 = 0, F1 = 0, T2 = 0, F2 = 0;
-#pragma unroll
-          for (int k = 0; k < NL; k++) {
-            const StrParam sp = P.strp[1 + k];
-            if (!((lpres >> k) & 1u)) {   // absent column: NULL in every row
-              d1 += sp.dim_null * sp.dim_stride;
-              d2 += sp.dim_null * sp.dim_stride;
-              F1 |= sp.hmask;
-              F2 |= sp.hmask;
-              continue;
-            }
-            const uint32_t bwk = lbw[k];
-            const uint32_t msk = bwk >= 32u ? ~0u : ((1u << bwk) - 1u);
-            auto look = [&](v2u w, uint32_t meta, uint32_t& d, uint32_t& T, uint32_t& F) __attribute__((always_inline)) {
-              const uint64_t x = ((uint64_t)w.y << 32) | w.x;
-              const uint32_t idx = (meta >> 31) ? uint32_t(x >> (meta & 63u)) & msk : meta;
-              uint32_t packed;
-              if ((llut_on >> k) & 1u) {
-                packed = L.llut[k][idx < LUT_CAP ? idx : 0u];
-              } else {
-                const uint32_t g = lremap[k][idx];
-                packed = sp.strtab ? sp.strtab[g] : g;
-              }
-              const uint32_t bits = (packed >> 24) << sp.lbase;
-              d += (packed & DIM_MASK) * sp.dim_stride;
-              T |= bits & sp.lmask;
-              F |= ~bits & sp.lmask;
-            };
-            look(lw1[k], lm1[k], d1, T1, F1);
-            look(lw2[k], lm2[k], d2, T2, F2);
-          }
-          if (!late_trivial) {
-            const uint32_t lf = Sp->leaf_false;
-            const uint32_t ix1 = (T1 & ~lf) | ((F1 | lf) << P.nleaves), ix2 = (T2 & ~lf) | ((F2 | lf) << P.nleaves);
-            p1 = a1 && ((L.ltruth[ix1 >> 5] >> (ix1 & 31)) & 1u);
-            p2 = two && ((L.ltruth[ix2 >> 5] >> (ix2 & 31)) & 1u);
-            gather();
-          }
-        } else {
-          gather();
-        }
-        if (count_plan) {
-          auto mark = [&](uint32_t* bm, uint32_t off, uint32_t line0) __attribute__((always_inline)) {
-            const uint32_t l = (off >> 7) - line0;
-            atomicOr(&bm[l >> 5], 1u << (l & 31u));
-          };
-          if (!one_bucket) {
-            if (p1) mark(L.lines_t, (vb0 + r1) * 8u, line_t0);
-            if (p2) mark(L.lines_t, (vb0 + r2) * 8u, line_t0);
-          }
-          if (AGG != AGG_COUNT) {
-            if (p1) mark(L.lines_v, (vb1 + r1) * 8u, line_v0);
-            if (p2) mark(L.lines_v, (vb1 + r2) * 8u, line_v0);
-          }
-        }
-        if (p1)
-          row((int64_t)(((uint64_t)t1.y << 32) | t1.x), __longlong_as_double((long long)(((uint64_t)x1.y << 32) | x1.x)), d1);
-        if (p2)
-          row((int64_t)(((uint64_t)t2.y << 32) | t2.x), __longlong_as_double((long long)(((uint64_t)x2.y << 32) | x2.x)), d2);
-      };
       if constexpr (NL == 0) {
         // passing rows: two per trip (their loads in flight together)
         while (m) {
@@ -614,12 +735,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
             d1 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e1) : rval] & DIM_MASK) * stride;
             d2 = (L.lut[lit ? lean_code<BW>(w0, w1, w2, e2) : rval] & DIM_MASK) * stride;
           }
-          rows2(rbase + e1, rbase + e2, true, two, d1, d2);
+          const uint32_t rr[2] = {rbase + e1, rbase + e2};
+          const bool aa[2] = {true, two};
+          uint32_t dd[2] = {d1, d2};
+          rowsN(std::integral_constant<int, 2>{}, rr, aa, dd);
         }
       } else {
-        // Late columns: the wave's passing rows are compacted into its LDS list (tile row | code << 16, lane-major)
-        // and processed 128 per trip, every lane busy -- a per-lane loop would run as many trips as the lane with
-        // the most passing rows, each a chain of dependent late-column and value loads.
+        // Late columns: the wave's passing rows are appended to its LDS list (lane-major) and processed LEAN_TRIP at
+        // a time (list_trip) -- a per-lane loop would run as many trips as the lane with the most passing rows, each
+        // a chain of dependent late-column and value loads.
         uint32_t f16 = uint32_t(m);
         if (swar) {
           f16 = 0;
@@ -635,36 +759,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
         }
         const uint32_t wtotal = uni(uint32_t(__shfl(int(inc), 63)));
         const uint32_t pos0 = inc - cnt;
-        uint32_t* wl = L.wlist[tid >> 6];
-        for (uint32_t b0 = 0; b0 < wtotal; b0 += LEAN_LIST) {   // uniform
+        for (uint32_t done = 0; done < wtotal;) {   // uniform
+          const uint32_t take = min(LEAN_LIST - (ltail - lhead), wtotal - done);
           uint32_t f = f16, pos = pos0;
           while (f) {
             const uint32_t e = uint32_t(__builtin_ctz(f));
             f &= f - 1u;
-            if (pos >= b0 && pos < b0 + LEAN_LIST)
-              wl[pos - b0] = (rbase + e) | ((lit ? lean_code<BW>(w0, w1, w2, e) : rval) << 16);
+            if (pos >= done && pos < done + take)
+              wl[(ltail + pos - done) & (LEAN_LIST - 1u)] = (rbase + e) | ((lit ? lean_code<BW>(w0, w1, w2, e) : rval) << 16);
             pos++;
           }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          const uint32_t nb = min(LEAN_LIST, wtotal - b0);
-          for (uint32_t j = 0; j < nb; j += 128) {   // uniform
-            const uint32_t i1 = j + uint32_t(lane), i2 = i1 + 64u;
-            const bool a1 = i1 < nb, a2 = i2 < nb;
-            const uint32_t x1 = a1 ? wl[i1] : 0u, x2 = a2 ? wl[i2] : 0u;
-            uint32_t d1 = dim_u, d2 = dim_u;
-            if (npass > 1) {
-              d1 = (L.lut[x1 >> 16] & DIM_MASK) * stride;
-              d2 = (L.lut[x2 >> 16] & DIM_MASK) * stride;
-            }
-            rows2(x1 & 0xffffu, x2 & 0xffffu, a1, a2, d1, d2);
-          }
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // the list is rewritten by the next batch
-          __builtin_amdgcn_wave_barrier();
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          ltail += take;
+          done += take;
+          wave_sync();
+          while (ltail - lhead >= LEAN_TRIP) list_trip(LEAN_TRIP);   // uniform
+          wave_sync();   // the trips' entries are rewritten by later appends
         }
       }
+    }
+    if constexpr (NL > 0) {
+      while (ltail != lhead) list_trip(min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
+      wave_sync();
     }
   };
   switch (bw) {   // uniform
@@ -676,7 +791,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
     default: body(std::integral_constant<uint32_t, 6>{}); break;
   }
 
-  lds_merge<AGG, HASH, false>(L, P, acc);
+  flush();
   __syncthreads();
   if (count_plan) {
     if (tid == 0) {
@@ -688,10 +803,23 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(4))) void
       for (uint32_t i = tid; i < LEAN_LLINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_l[k][i]));
     if (pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
   }
-  for (int i = tid; i < LT::H; i += BLOCK) {
-    if (L.hkey[i] == EMPTY) continue;
-    global_merge<AGG, HASH>(P, L.hkey[i], L.hrows[i], L.hcnt[i], L.hhi[i], L.hlo[i],
-                            reinterpret_cast<unsigned long long*>(L.hhi)[i]);
+  // ---- the table's cells -> the global table (device atomics) ----
+  if (tspan) {
+    for (uint32_t x = tid; x < ndir; x += BLOCK) {
+      const unsigned long long v = rv[x];
+      const unsigned long long r = rrows_on ? rrows[x] : (AGG == AGG_COUNT ? v : (v != rident ? 1ull : 0ull));
+      if (r == 0ull) continue;
+      const uint32_t j = x / ngr, g = x - j * ngr;
+      global_merge<AGG, HASH>(P, (glob_base + (unsigned long long)(tbl + j)) * P.ngroups + g, uint32_t(r), uint32_t(r),
+                              __longlong_as_double((long long)v),
+                              AGG == AGG_SUM ? __longlong_as_double((long long)rlo[x]) : 0.0, v);
+    }
+  } else {
+    for (int i = tid; i < LeanHash::H; i += BLOCK) {
+      if (L.agg.hs.hkey[i] == EMPTY) continue;
+      global_merge<AGG, HASH>(P, L.agg.hs.hkey[i], L.agg.hs.hrows[i], L.agg.hs.hcnt[i], L.agg.hs.hhi[i], L.agg.hs.hlo[i],
+                              reinterpret_cast<unsigned long long*>(L.agg.hs.hhi)[i]);
+    }
   }
 }
 

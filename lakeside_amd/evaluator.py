@@ -132,10 +132,12 @@ class Result:
 class Engine:
     """One per process per GPU: HIP device, stream, HBM segment cache, optional RCCL communicator."""
 
-    def __init__(self, device: int = 0, hbm_budget_bytes: int = 0, max_calls: int = 4):
+    def __init__(self, device: int = 0, hbm_budget_bytes: int = 0, max_calls: int = 4, dict_compact_min_dead: int = 0):
         L = _lib.lib()
         h = ctypes.c_void_p()
         opts = {"device": device, "hbm_budget_bytes": int(hbm_budget_bytes), "max_calls": int(max_calls)}
+        if dict_compact_min_dead:
+            opts["dict_compact_min_dead"] = int(dict_compact_min_dead)
         check(L.lk_engine_create(json.dumps(opts).encode(), ctypes.byref(h)))
         self._h = h
         self.device = device
@@ -172,6 +174,11 @@ class Engine:
     @property
     def segment_bytes(self) -> int:
         return int(_lib.lib().lk_segment_bytes(self._h))
+
+    @property
+    def stats(self) -> dict:
+        """Engine counters: cached segments, evictions, dictionary sizes / live ids / compactions."""
+        return json.loads(_lib.lib().lk_engine_stats(self._h).decode())
 
     # ---- evaluation ----
     def eval_pushdown(self, request_json: str, paths: Sequence[str], glob_size: int = 10,

@@ -199,10 +199,13 @@ def test_exemplar_java17_number_text(engine, tmp_path):
     fv[np.isnan(fv)] = 2.5
     ts = synth.T0 + np.arange(n, dtype=np.int64) * 10
     t = pa.table({dx.TIMESTAMP: pa.array(ts), dx.VALUE: pa.array(dv),
-                  dx.NAME: pa.array(["m"] * n, pa.string()), "attr.d": pa.array(dv), "attr.f": pa.array(fv)})
+                  dx.NAME: pa.array(["m"] * n, pa.string()), "_cardinalhq.message": pa.array(["msg"] * n, pa.string()),
+                  "attr.d": pa.array(dv), "attr.f": pa.array(fv)})
     path = str(tmp_path / "jdk17.parquet")
-    pq.write_table(t, path, compression="NONE", use_dictionary=[dx.NAME],
-                   column_encoding={c: "PLAIN" for c in t.column_names if c != dx.NAME})
+    strings = [dx.NAME, "_cardinalhq.message"]   # the logs projection needs the message column (a Binder Error without)
+    pq.write_table(t, path, compression="NONE", use_dictionary=strings,
+                   column_encoding={c: "PLAIN" for c in t.column_names if c not in strings})
+    engine.load_segment(path)
     blobs = [open(path, "rb").read()]
     req = _request(synth.leaf(dx.NAME, "eq", "m"), 1, limit=n, order="asc", hour=0)
     got = _check(engine, req, [path], blobs, 1, "jdk17 text")
