@@ -78,6 +78,8 @@ def lib():
             raise ImportError(f"{LIB_PATH} is missing: build it with `make` (no CPU fallback exists)")
         L = ctypes.CDLL(LIB_PATH)
         for name, res, args in SIGNATURES:
+            if os.environ.get("LK_LIB_PATH") and not hasattr(L, name):
+                continue   # an A/B build from before this symbol existed (experiments only)
             f = getattr(L, name)
             f.restype = res
             f.argtypes = args

@@ -124,6 +124,21 @@ __device__ __forceinline__ uint32_t lean_code(uint32_t w0, uint32_t w1, uint32_t
   return __builtin_amdgcn_alignbit(hi, lo, off) & ((1u << BW) - 1u);
 }
 
+// An RLE chunk's code v as 16 BW-bit fields in (w0, w1, w2) (the layout lean_code reads).
+template <uint32_t BW>
+__device__ __forceinline__ void lean_rep(uint32_t v, uint32_t& w0, uint32_t& w1, uint32_t& w2) {
+  uint32_t w[3] = {0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t e = 0; e < 16; e++) {
+    const uint32_t bit = e * BW, wi = bit >> 5, off = bit & 31u;
+    w[wi] |= v << off;
+    if (off + BW > 32u) w[wi + 1] |= v >> (32u - off);
+  }
+  w0 = w[0];
+  w1 = w[1];
+  w2 = w[2];
+}
+
 template <int AGG, bool HASH, int NL>
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ? 5 : 4))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
@@ -679,7 +694,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
         const bool contig = live && valid == 0xffffu && v0 == v0l + 16u * uint32_t(lane);
         if (__ballot(contig) == ~0ull && __popcll(__ballot(__popc(f16) >= 2u)) >= 48) {
           const uint32_t rb0 = uni(rbase);
-          const uint32_t litv = lit ? 1u : 0u;
+          // The owner lane's 16 codes as 16 BW-bit fields in (c0, c1, c2) -- an RLE chunk's code replicated -- with
+          // the pass bits in the spare high bits (BW <= 5), so a reader takes its code and pass bit with 1-3 cross-lane
+          // reads instead of six.
+          uint32_t c0 = w0, c1 = w1, c2 = w2;
+          if (!lit) lean_rep<BW>(rval, c0, c1, c2);
+          constexpr uint32_t FSH = BW <= 4 ? 0u : 16u;   // f16's place in c2 (BW == 6: no room, its own read)
+          if constexpr (BW <= 5) c2 = (BW <= 4 ? 0u : (c2 & 0xffffu)) | (f16 << FSH);
 #pragma unroll 1
           for (int j0 = 0; j0 < 16; j0 += 4) {
             v2u tt[4], xx[4];
@@ -689,7 +710,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
             for (int u = 0; u < 4; u++) {   // issue the 4 trips' loads before any use
               const int src = 4 * (j0 + u) + (lane >> 4);
               const uint32_t e = uint32_t(lane) & 15u;
-              pp[u] = (uint32_t(__shfl(int(f16), src)) >> e) & 1u;
+              const uint32_t a2 = BW <= 5 ? uint32_t(__shfl(int(c2), src)) : 0u;
+              pp[u] = ((BW <= 5 ? a2 >> FSH : uint32_t(__shfl(int(f16), src))) >> e) & 1u;
               const uint32_t r = rb0 + 64u * uint32_t(j0 + u) + uint32_t(lane);
               tt[u] = v2u{0u, 0u};
               xx[u] = v2u{0u, 0u};
@@ -697,10 +719,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
               if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, pp[u] ? (vb1 + r) * 8u : OOB, 0, 0);
               dd[u] = dim_u;
               if (npass > 1) {   // uniform
-                const uint32_t a0 = uint32_t(__shfl(int(w0), src)), a1 = uint32_t(__shfl(int(w1), src));
-                const uint32_t a2 = uint32_t(__shfl(int(w2), src));
-                const uint32_t sl = uint32_t(__shfl(int(litv), src)), sv = uint32_t(__shfl(int(rval), src));
-                dd[u] = (L.lut[sl ? lean_code<BW>(a0, a1, a2, e) : sv] & DIM_MASK) * stride;
+                const uint32_t a0 = uint32_t(__shfl(int(c0), src));
+                const uint32_t a1 = BW > 2 ? uint32_t(__shfl(int(c1), src)) : 0u;
+                const uint32_t a2c = BW == 6 ? uint32_t(__shfl(int(c2), src)) : a2;
+                dd[u] = (L.lut[lean_code<BW>(a0, a1, a2c, e)] & DIM_MASK) * stride;
               }
               if (count_plan && pp[u]) {
                 if (!one_bucket) {
