@@ -134,7 +134,7 @@ def main():
                 kept[i] = seg
             else:
                 seg.free()
-            if n % 8 == 7:
+            if n % 8 == 7 or S <= 16:
                 log(f"rank {rank}: {n + 1}/{S} segments generated + loaded to HBM ({time.time() - t0:.0f}s)")
     log(f"rank {rank}: {S} segments ({bytes_loaded / 1e9:.1f} GB Parquet) resident, HBM cache "
         f"{eng.segment_bytes / 1e9:.1f} GB; Parquet -> HBM load {load_s:.2f} s ({bytes_loaded / load_s / 1e9:.2f} GB/s, "

@@ -169,6 +169,7 @@ template <int AGG, bool HASH = false>
 __device__ __forceinline__ void global_merge(const QParams& P, unsigned long long cell, uint32_t rows,
                                              uint32_t cnt, double hi, double lo, unsigned long long ext) {
   if (rows == 0) return;
+  if (P.ablate & 4u) return;   // diagnostics only (LK_ABLATE=4): no device atomics (wrong results; the atomics' cost)
   if (HASH) {
     cell = hash_slot(P.hkeys, P.hmask, P.flags, cell);
     if (cell == EMPTY) return;

@@ -905,7 +905,12 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     c.d_tcols = reinterpret_cast<TileCol*>(base + place(c.tcols.data(), c.tcols.size() * sizeof(TileCol)));
     c.d_remap = reinterpret_cast<uint32_t*>(base + place(c.remap.data(), c.remap.size() * sizeof(uint32_t)));
     c.any_nulls = false;
-    for (auto& p : c.pages) c.any_nulls |= p.has_nulls != 0;
+    c.pages_lean_name = c.pages_lean_late = !c.pages.empty();
+    for (auto& p : c.pages) {
+      c.any_nulls |= p.has_nulls != 0;
+      if (p.kind != PAGE_DICT || p.dict_n > 64 || p.bw < 1 || p.bw > 6) c.pages_lean_name = false;
+      if (p.kind != PAGE_DICT || p.bw > 32) c.pages_lean_late = false;
+    }
   }
   HIP_CHECK(hipMemcpy(S->d_meta, blob.data(), off, hipMemcpyHostToDevice));
   // the segment now references its chunk dictionaries' ids (released by ~Segment)

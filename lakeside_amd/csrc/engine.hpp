@@ -69,6 +69,9 @@ struct HostCol {
   bool is_string = false;
   bool unsupported = false;
   bool any_nulls = false;
+  // page summaries (load time), so a query's lean-tile test costs O(1) per column instead of a walk over its pages:
+  bool pages_lean_name = false;           // every page: dictionary indices, chunk dictionary <= 64 values, 1..6 bits
+  bool pages_lean_late = false;           // every page: dictionary indices of <= 32 bits
   uint64_t compressed_bytes = 0;          // Σ ColumnMetaData.total_compressed_size (algorithmic bytes)
   std::vector<PageDesc> pages;            // host copy (planner reads dict sizes / null flags)
   std::vector<RunDesc> runs;              // load-time only
@@ -310,6 +313,8 @@ struct lk_result {
   // with_glob = false (merged rows: every glob index is 0): the glob column is a shared read-only block of
   // zeros, so the device writes 20 instead of 24 bytes per row over the host link.
   void alloc_rows(size_t n, bool with_glob = true) {
+    lk::pinned_release(blk);   // a re-run evaluation (metrics / MIN re-runs) allocates again
+    blk = lk::HostBlock{};
     blk = lk::pinned_acquire(n * (with_glob ? 24 : 20) + 64);
     nrows = n;
     auto* b = static_cast<uint8_t*>(blk.p);

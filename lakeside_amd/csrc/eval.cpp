@@ -270,7 +270,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::unique_lock<std::mutex> comm_lock;
   if (dist) comm_lock = std::unique_lock<std::mutex>(E.comm_mu);
   CtxLease X(E);
+  static const bool plan_timing = getenv("LK_PLAN_TIMING") != nullptr;   // diagnostics: host planning stages
+  auto stage = [&](const char* what) {
+    if (plan_timing) fprintf(stderr, "[lk plan] %-10s %.3f ms\n", what, ms_since(t_start));
+  };
   Request R = parse_request(json);
+  stage("parse");
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
   if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
   if (glob_size <= 0) glob_size = 10;
@@ -463,6 +468,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     load_msg = msg;
   }
 
+  stage("segments");
   // ---- globs ----
   const std::set<std::string> fset = field_set(R);
   std::vector<std::string> probe_cols(fset.begin(), fset.end());   // columns whose existence matters
@@ -574,6 +580,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // metrics off the step grid: one bucket per millisecond, i.e. the raw timestamp (see evaluate())
   if (metrics_raw && R.dataset == "metrics" && !tagq) step = 1;
 
+  stage("globs");
   // ---- group dimensions ----
   const bool merged = !per_glob_rows;
   // Merged min/max over values that can be NULL: NULL, "null" and "" group values stay apart in the table
@@ -630,6 +637,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (ngroups > 0xffffffffull) throw PlanError(LK_ERR_UNSUPPORTED, "group space beyond 2^32 groups");
   }
 
+  stage("dims");
   // ---- lookup tables: global id -> leaf bits << 24 | dim id ----
   std::vector<std::vector<uint32_t>> tabs(strs.size());
   std::vector<char> need_tab(strs.size(), 0);
@@ -705,6 +713,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
   }
 
+  stage("tables");
   // ---- bucket space ----
   int64_t min_lo = INT64_MAX, max_hi = INT64_MIN;
   for (auto& g : globs) {
@@ -820,13 +829,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         for (size_t s2 = 1; s2 < strs.size() && all_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
           const int cl = S.col_index(strs[s2].name);
           if (cl < 0) continue;
-          if (S.cols[cl].any_nulls) all_lean = false;
-          for (const PageDesc& pg : S.cols[cl].pages)
-            if (pg.kind != PAGE_DICT || pg.bw > 32) { all_lean = false; break; }
+          if (S.cols[cl].any_nulls || !S.cols[cl].pages_lean_late) all_lean = false;
         }
-        if (all_lean)
-          for (const PageDesc& pg : S.cols[cn].pages)
-            if (pg.kind != PAGE_DICT || pg.dict_n > 64 || pg.bw < 1 || pg.bw > 6) { all_lean = false; break; }
+        if (all_lean && !S.cols[cn].pages_lean_name) all_lean = false;
       }
       q.tile_begin = total_tiles;
       seg_begin.push_back(total_tiles);
@@ -845,6 +850,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     gsegs.clear();
     total_tiles = 0;
   }
+  stage("qsegs");
   uint32_t max_tiles = 0, gmax_tiles = 0;
   for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
   for (auto& q : gsegs) gmax_tiles = std::max(gmax_tiles, q.ntiles);
@@ -929,6 +935,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     cap = std::min<uint64_t>(cap_max, pow2(std::max<uint64_t>(64, uint64_t(atoll(getenv("LK_HASH_INIT_SLOTS"))))));
 
   // ---- device: upload, zero table, scan ----
+  stage("truth");
   const double plan_ms = ms_since(t_start);
   HIP_TRY(hipSetDevice(E.device));
   hipStream_t st = X->stream;
@@ -1069,6 +1076,29 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     P.dd_max = dd::mapping().max_indexable;
   }
 
+  // Single-GPU dense tables with a bounded output: the finalize is enqueued right behind the scan -- rows written by
+  // the kernel into the (pinned) result block sized for every output key -- so the flags, the row count and the rows
+  // come back with one stream synchronization instead of three (scan flags, row count, rows).  A re-run (metrics off
+  // the step grid, MIN over NaN) discards the speculative rows.
+  const uint64_t out_keys = ncells == 0 ? 0 : (per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups));
+  const bool fast_final = !dist && !hash_mode && !sketch && !ces && !rekey && ncells && out_keys <= (uint64_t(1) << 20) &&
+                          !getenv("LK_NO_FAST_FINAL");
+  auto setup_final = [&](FParams& Fp, uint32_t fslots) {
+    Fp.ngroups = ngroups;
+    Fp.nbuckets = nbuckets;
+    Fp.nglob_slots = fslots;
+    Fp.agg = agg;
+    Fp.per_glob = per_glob_rows ? 1 : 0;
+    Fp.collapse = collapse ? 1 : 0;
+    Fp.name_stride = strs[0].stride ? strs[0].stride : 1;
+    Fp.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
+    Fp.bucket_base = bucket_base;
+    Fp.step = P.step;
+    Fp.nkeys = out_keys;
+  };
+  bool fast_done = false;         // rows already written by the speculative finalize
+  uint32_t fast_rows = 0;
+
   // Zero the table (SoA [rows | cnt | hi | lo | ext (| keys)]) and scan; returns the kernel's flags.
   size_t nc = 0;
   double launch_ms = 0;
@@ -1149,6 +1179,24 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       }
     }
     uint32_t fl[4] = {0, 0, 0, 0};
+    if (fast_final && !fast_done) {
+      res->alloc_rows(size_t(out_keys), per_glob_rows);
+      if (res->blk.pinned) {
+        FParams Fs{};
+        Fs.rows = P.rows;
+        Fs.cnt = P.cnt;
+        Fs.hi = P.hi;
+        Fs.lo = P.lo;
+        Fs.ext = P.ext;
+        setup_final(Fs, nslots);
+        const uint32_t nb = finalize_blocks(Fs.nkeys);
+        uint32_t* cnts = static_cast<uint32_t*>(X->workspace("counts", (size_t(nb) + 2) * 4));
+        HIP_TRY(launch_finalize_count(Fs, cnts, st));
+        HIP_TRY(launch_finalize_write(Fs, cnts, res->ts, res->val, res->gid, per_glob_rows ? res->glob : nullptr, st));
+        HIP_TRY(hipMemcpyAsync(&fast_rows, cnts + nb, 4, hipMemcpyDeviceToHost, st));
+        fast_done = true;
+      }
+    }
     HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     memcpy(&plan_bytes, fl + 2, 8);
@@ -1556,20 +1604,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
 
     // ---- finalize + compaction ----
-    F.ngroups = ngroups;
-    F.nbuckets = nbuckets;
-    F.nglob_slots = fslots;
-    F.agg = agg;
-    F.per_glob = per_glob_rows ? 1 : 0;
-    F.collapse = collapse ? 1 : 0;
-    F.name_stride = strs[0].stride ? strs[0].stride : 1;
-    F.name_rank = name_rank.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_rank);
-    F.bucket_base = bucket_base;
-    F.step = P.step;
-    F.nkeys = ncells == 0 ? 0 : (per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups));
+    setup_final(F, fslots);
     nfb = finalize_blocks(F.nkeys);
     d_counts = static_cast<uint32_t*>(X->workspace("counts", (size_t(nfb) + 2) * 4));
-    if (emit && F.nkeys) {
+    if (fast_done) {
+      nrows_out = fast_rows;   // rows already in the result block (speculative finalize behind the scan)
+    } else if (emit && F.nkeys) {
       HIP_TRY(launch_finalize_count(F, d_counts, st));
       HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
     }
@@ -1616,9 +1656,10 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     HIP_TRY(launch_sparse_sort(S, occ, nocc, end_bit, sws, &d_nrows, st));
     HIP_TRY(hipMemcpyAsync(&nrows_out, d_nrows, 4, hipMemcpyDeviceToHost, st));
   }
-  HIP_TRY(hipStreamSynchronize(st));
+  if (!fast_done) HIP_TRY(hipStreamSynchronize(st));
   const double sync_ms = ms_since(t_start);     // scan + merge + finalize done
-  if (!rows_done) res->alloc_rows(nrows_out, per_glob_rows);
+  if (fast_done) res->nrows = nrows_out;       // the block holds out_keys rows' room; nrows_out of them are written
+  else if (!rows_done) res->alloc_rows(nrows_out, per_glob_rows);
   const double alloc_ms = ms_since(t_start);
   if (ces) {
     for (size_t r = 0; r < nrows_out; r++) {
@@ -1637,7 +1678,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (per_glob_rows) res->glob[r] = k.glob;
       res->sketches.push_back(k.sk.serialize());
     }
-  } else if (nrows_out && !rows_done) {
+  } else if (nrows_out && !rows_done && !fast_done) {
     // Rows written by the kernel straight into the mapped pinned result block when it is pinned: no device->host
     // copies (small async D2H copies cost ~1 ms of completion latency each call on this stack, measured in C4).
     const bool direct = res->blk.pinned;

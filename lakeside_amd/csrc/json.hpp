@@ -82,8 +82,14 @@ class Json {
     i++;
     std::string o;
     while (i < s.size() && s[i] != '"') {
-      char c = s[i++];
-      if (c != '\\') { o += c; continue; }
+      if (s[i] != '\\') {   // a run of plain characters: appended at once
+        size_t j = i + 1;
+        while (j < s.size() && s[j] != '"' && s[j] != '\\') j++;
+        o.append(s, i, j - i);
+        i = j;
+        continue;
+      }
+      i++;
       if (i >= s.size()) throw JsonError("json: bad escape");
       char e = s[i++];
       switch (e) {

@@ -165,7 +165,8 @@ struct QParams {
                                     // 2: every tile is lean (scan_tiles is not launched)
   uint32_t lean;                    // LEAN_* bits: table fields the scan leaves to the fix-up pass (fewer atomics)
   uint32_t* flags;                  // error / diagnostic flags
-  uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode
+  uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode,
+                                    // 4 no global-table atomics
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
   // Plan bytes (the roofline numerator): bytes the late-materialized plan must read from HBM, counted
   // by the kernel: tile metadata + staged runs + dictionary lookups, every fully decoded stream of a tile, and the

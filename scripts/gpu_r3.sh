@@ -12,7 +12,7 @@ if [[ $STEPS == *tests* ]]; then
 fi
 if [[ $STEPS == *bench* ]]; then
   for q in ${QUERIES:-c2 c3 c4 c5 dense}; do
-    cs=0; [ "$q" = c2 ] && cs=${CPU_SAMPLE_C2:--1}
+    cs=0; [ "$q" = c2 ] && cs=${CPU_SAMPLE_C2:--1}; [ -n "$CPU_ALL" ] && [ "$q" != dense ] && [ "$q" != exemplar ] && [ "$q" != tag ] && cs=-1; [ -n "$CPU_ALL" ] && [ "$q" = c5 ] && cs=1
     timeout -k 10 400 python3 bench.py --query $q --steps ${NSTEPS:-10} --warmup 3 --cpu-sample $cs $BENCH_ARGS > gpurun_out/bench/$q.json 2> gpurun_out/bench/$q.log
     rc=$?; grep -h "scan kernel" gpurun_out/bench/$q.log | sed 's/; in the call.*//'; [ $rc -eq 0 ] || exit $rc
   done
