@@ -6,6 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/prof
 export TMPDIR=/tmp
 Q=${QUERY:-c2}
+rm -rf gpurun_out/prof/bench_kt gpurun_out/prof/bench_fetch gpurun_out/prof/bench_write gpurun_out/prof/dense_fetch
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof/bench_kt -o kt --output-format csv -- python3 bench.py --query $Q --steps 10 --warmup 3 --cpu-sample 0 > gpurun_out/prof/bench_kt.json 2> gpurun_out/prof/bench_kt.log || exit $?
 timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d gpurun_out/prof/bench_fetch -o pmc --output-format csv -- python3 bench.py --query $Q --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/prof/bench_fetch.json 2> gpurun_out/prof/bench_fetch.log || exit $?
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d gpurun_out/prof/bench_write -o pmc --output-format csv -- python3 bench.py --query $Q --steps 3 --warmup 1 --cpu-sample 0 > gpurun_out/prof/bench_write.json 2> gpurun_out/prof/bench_write.log || exit $?
