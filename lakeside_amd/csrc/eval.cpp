@@ -1063,10 +1063,18 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     const uint64_t words = lean_ring_words(P.nstr - 1);
     const bool rows_plane = kagg != AGG_COUNT && !(P.lean & (LEAN_SUM_EXISTS | LEAN_NO_ROWS));
     const uint32_t cw = (kagg == AGG_SUM ? 2u : 1u) + (rows_plane ? 1u : 0u);
-    const uint64_t w = std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * std::max<uint64_t>(ngroups, 1)));
-    if (w >= 1) {
-      P.ring_w = uint32_t(w);
-      P.ring_cw = cw;
+    // the most replicas per cell (spreading lanes that add into the same cells over more LDS addresses) that still
+    // leave room for a tile spanning two buckets
+    for (uint32_t rep = 4; rep >= 1; rep /= 2) {
+      const uint64_t w = std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * rep * std::max<uint64_t>(ngroups, 1)));
+      if (w >= 2 || (rep == 1 && w >= 1)) {
+        P.ring_w = uint32_t(w);
+        P.ring_cw = cw;
+        P.ring_rep = getenv("LK_RING_REP1") ? 1u : rep;   // env: A/B only
+        if (P.ring_rep == 1u && rep != 1u)
+          P.ring_w = uint32_t(std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * std::max<uint64_t>(ngroups, 1))));
+        break;
+      }
     }
   }
   if (sketch) {

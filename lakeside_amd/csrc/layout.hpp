@@ -176,6 +176,7 @@ struct QParams {
   // cell (0: the LDS hash table instead)
   uint32_t ring_w;
   uint32_t ring_cw;
+  uint32_t ring_rep;                  // replicas per direct-table cell (1, 2 or 4)
 };
 // scan_lean's direct table: LDS words by late-column count NL (the hash table's 8 KB for NL >= 1, so the kernels keep
 // their occupancy), at most LEAN_RING_MAXW buckets

@@ -30,10 +30,17 @@ constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a 
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
 constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
 
-constexpr uint32_t LEAN_LIST = 512;                                    // per-wave list of passing rows (late columns)
+#ifndef LK_LEAN_LIST
+#define LK_LEAN_LIST 512
+#endif
+constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wave list of passing rows (late columns)
 #ifndef LK_LEAN_ROWS
 #define LK_LEAN_ROWS 2
 #endif
+#ifndef LK_LEAN_WAVES2
+#define LK_LEAN_WAVES2 4
+#endif
+#define LEAN_WAVES(NL) ((NL) <= 1 ? 5 : LK_LEAN_WAVES2)   // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 
@@ -140,7 +147,7 @@ __device__ __forceinline__ void lean_rep(uint32_t v, uint32_t& w0, uint32_t& w1,
 }
 
 template <int AGG, bool HASH, int NL>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ? 5 : 4))) void scan_lean(QParams P) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVES(NL)))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
   __shared__ LT L;
   const int tid = threadIdx.x;
@@ -184,7 +191,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
     }
   }
   const uint32_t ngr = tspan ? uint32_t(P.ngroups) : 0u;
-  const uint32_t ndir = tspan * ngr;                                // direct cells
+  // P.ring_rep replicas of every cell (a lane adds into replica lane % rep): lanes adding into the same few cells (the
+  // dense query: 64 rows over 16 names) spread over rep times as many LDS addresses; combined at the flush
+  const uint32_t rep = P.ring_rep ? P.ring_rep : 1u;
+  const uint32_t myrep = uint32_t(lane) & (rep - 1u);
+  const uint32_t ndir = tspan * ngr * rep;                          // direct cells (replicas included)
   unsigned long long* const rv = L.agg.ring;                         // value plane (SUM: hi)
   unsigned long long* const rlo = L.agg.ring + ndir;                 // SUM: lo plane
   const bool rrows_on = P.ring_cw > (AGG == AGG_SUM ? 2u : 1u);      // the table keeps rows: a rows plane
@@ -444,7 +455,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
     unsigned long long cell;
     const uint64_t j = uint64_t(b - tbl);
     if (tspan && j < tspan) {
-      cell = uint32_t(j) * ngr + dim;
+      cell = (uint32_t(j) * ngr + dim) * rep + myrep;
     } else {
       cell = (glob_base + (unsigned long long)b) * P.ngroups + dim;
       if (tspan) cell |= GBIT;
@@ -827,14 +838,33 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NL <= 1 ?
   }
   // ---- the table's cells -> the global table (device atomics) ----
   if (tspan) {
-    for (uint32_t x = tid; x < ndir; x += BLOCK) {
-      const unsigned long long v = rv[x];
-      const unsigned long long r = rrows_on ? rrows[x] : (AGG == AGG_COUNT ? v : (v != rident ? 1ull : 0ull));
+    for (uint32_t c = tid; c < tspan * ngr; c += BLOCK) {   // a cell's replicas, combined
+      unsigned long long v = rident, r = 0;
+      double hi = 0.0, lo = 0.0;
+      for (uint32_t k = 0; k < rep; k++) {
+        const uint32_t x = c * rep + k;
+        const unsigned long long vk = rv[x];
+        const unsigned long long rk = rrows_on ? rrows[x] : (AGG == AGG_COUNT ? vk : (vk != rident ? 1ull : 0ull));
+        if (rk == 0ull) continue;
+        r += rk;
+        if (AGG == AGG_SUM) {
+          double s2, e;
+          two_sum(hi, __longlong_as_double((long long)vk), s2, e);
+          hi = s2;
+          lo += e + __longlong_as_double((long long)rlo[x]);
+        } else if (AGG == AGG_MIN) {
+          v = vk < v ? vk : v;
+        } else if (AGG == AGG_MAX) {
+          v = vk > v ? vk : v;
+        } else {
+          v = (v == rident ? 0ull : v) + vk;
+        }
+      }
       if (r == 0ull) continue;
-      const uint32_t j = x / ngr, g = x - j * ngr;
+      const uint32_t j = c / ngr, g = c - j * ngr;
+      if (AGG == AGG_SUM) v = (unsigned long long)__double_as_longlong(hi);
       global_merge<AGG, HASH>(P, (glob_base + (unsigned long long)(tbl + j)) * P.ngroups + g, uint32_t(r), uint32_t(r),
-                              __longlong_as_double((long long)v),
-                              AGG == AGG_SUM ? __longlong_as_double((long long)rlo[x]) : 0.0, v);
+                              hi, lo, v);
     }
   } else {
     for (int i = tid; i < LeanHash::H; i += BLOCK) {
