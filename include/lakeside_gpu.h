@@ -13,7 +13,8 @@
  * library until lk_result_free.  Calls on one engine are thread-safe and re-entrant: each evaluation leases its
  * own context (HIP stream, workspaces; up to "max_calls" in flight), so calls from several threads run
  * concurrently, as the worker's glob queries do (Commons.scala:371-372); only distributed calls
- * (lk_eval_pushdown_dist) are serialised, to keep every rank's collectives in one order.
+ * (lk_eval_pushdown_dist) are serialised, to keep every rank's collectives in one order, and a dictionary
+ * compaction (see lk_engine_create) runs between loads / evaluations, never under one.
  *
  * Errors: a failure that belongs to one glob's DuckDB query in the reference -- a missing or unreadable segment,
  * corrupt Parquet, a column type the query cannot bind, a regex RE2 rejects -- empties that glob only
