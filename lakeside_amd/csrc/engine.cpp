@@ -281,6 +281,19 @@ GlobalDict& Engine::dict(const std::string& col) {
   return *p;
 }
 
+std::shared_ptr<const Request> Engine::parse_cached(const std::string& json) {
+  {
+    std::lock_guard<std::mutex> g(parsed_mu);
+    auto it = parsed.find(json);
+    if (it != parsed.end()) return it->second;
+  }
+  auto r = std::make_shared<const Request>(parse_request(json));   // throws on a malformed request: nothing cached
+  std::lock_guard<std::mutex> g(parsed_mu);
+  if (parsed.size() >= 64) parsed.clear();
+  parsed.emplace(json, r);
+  return r;
+}
+
 void Engine::dict_ref(const std::string& col, const uint32_t* ids, size_t n, int delta) {
   GlobalDict& gd = dict(col);
   std::lock_guard<std::mutex> g(gd.mu);

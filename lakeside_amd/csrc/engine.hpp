@@ -231,6 +231,11 @@ struct Engine {
   std::unordered_map<std::string, PtrTable> ptrs;
   std::shared_ptr<const std::vector<const char*>> dict_ptrs(const std::string& col, size_t n,
                                                            const std::shared_ptr<StableStrs>& strs);
+  // Parsed requests by their JSON text (a dashboard re-issues the same pushdown every refresh): parsing a 64-segment
+  // request is a third of the host planning.  Bounded; a parsed Request is immutable.
+  std::mutex parsed_mu;
+  std::unordered_map<std::string, std::shared_ptr<const Request>> parsed;
+  std::shared_ptr<const Request> parse_cached(const std::string& json);
   // distributed group-dim unions, latest per column (DimUnion); used under comm_mu
   std::unordered_map<std::string, std::shared_ptr<DimUnion>> unions;
 

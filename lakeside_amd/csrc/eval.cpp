@@ -274,7 +274,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   auto stage = [&](const char* what) {
     if (plan_timing) fprintf(stderr, "[lk plan] %-10s %.3f ms\n", what, ms_since(t_start));
   };
-  Request R = parse_request(json);
+  const std::shared_ptr<const Request> Rp = E.parse_cached(json);
+  const Request& R = *Rp;
   stage("parse");
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
   if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
@@ -1058,21 +1059,21 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric) P.lean = 0;   // the general row scan accumulates every table field
   // scan_lean: a dense table whose group space fits LDS for the few buckets a tile spans is aggregated in the tile's
-  // direct table (lean_kernel.hpp) instead of the LDS hash table: ring_w = the most buckets it holds
-  if (P.lean_split && !hash_mode && !getenv("LK_NO_RING")) {
-    const uint64_t words = lean_ring_words(P.nstr - 1);
+  // direct table (lean_kernel.hpp) instead of the LDS hash table: dir_span = the most buckets it holds
+  if (P.lean_split && !hash_mode && !getenv("LK_NO_DIRECT")) {
+    const uint64_t words = lean_dir_words(P.nstr - 1);
     const bool rows_plane = kagg != AGG_COUNT && !(P.lean & (LEAN_SUM_EXISTS | LEAN_NO_ROWS));
     const uint32_t cw = (kagg == AGG_SUM ? 2u : 1u) + (rows_plane ? 1u : 0u);
     // the most replicas per cell (spreading lanes that add into the same cells over more LDS addresses) that still
     // leave room for a tile spanning two buckets
     for (uint32_t rep = 4; rep >= 1; rep /= 2) {
-      const uint64_t w = std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * rep * std::max<uint64_t>(ngroups, 1)));
+      const uint64_t w = std::min<uint64_t>(LEAN_DIR_MAXSPAN, words / (uint64_t(cw) * rep * std::max<uint64_t>(ngroups, 1)));
       if (w >= 2 || (rep == 1 && w >= 1)) {
-        P.ring_w = uint32_t(w);
-        P.ring_cw = cw;
-        P.ring_rep = getenv("LK_RING_REP1") ? 1u : rep;   // env: A/B only
-        if (P.ring_rep == 1u && rep != 1u)
-          P.ring_w = uint32_t(std::min<uint64_t>(LEAN_RING_MAXW, words / (uint64_t(cw) * std::max<uint64_t>(ngroups, 1))));
+        P.dir_span = uint32_t(w);
+        P.dir_planes = cw;
+        P.dir_rep = getenv("LK_DIRECT_REP1") ? 1u : rep;   // env: A/B only
+        if (P.dir_rep == 1u && rep != 1u)
+          P.dir_span = uint32_t(std::min<uint64_t>(LEAN_DIR_MAXSPAN, words / (uint64_t(cw) * std::max<uint64_t>(ngroups, 1))));
         break;
       }
     }

@@ -172,18 +172,18 @@ struct QParams {
   // by the kernel: tile metadata + staged runs + dictionary lookups, every fully decoded stream of a tile, and the
   // distinct 128-B lines touched by the per-row gathers (timestamps, values, late columns).
   unsigned long long* plan_bytes;
-  // scan_lean (lean_kernel.hpp): the direct table holds up to ring_w buckets of ngroups cells, ring_cw u64 planes per
+  // scan_lean (lean_kernel.hpp): the direct table holds up to dir_span buckets of ngroups cells, dir_planes u64 planes per
   // cell (0: the LDS hash table instead)
-  uint32_t ring_w;
-  uint32_t ring_cw;
-  uint32_t ring_rep;                  // replicas per direct-table cell (1, 2 or 4)
+  uint32_t dir_span;
+  uint32_t dir_planes;
+  uint32_t dir_rep;                  // replicas per direct-table cell (1, 2 or 4)
 };
 // scan_lean's direct table: LDS words by late-column count NL (the hash table's 8 KB for NL >= 1, so the kernels keep
-// their occupancy), at most LEAN_RING_MAXW buckets
-constexpr uint32_t LEAN_RING_WORDS0 = 1536;
-constexpr uint32_t LEAN_RING_WORDS1 = 1024;
-constexpr uint32_t LEAN_RING_MAXW = 8;
-constexpr uint32_t lean_ring_words(uint32_t nl) { return nl == 0 ? LEAN_RING_WORDS0 : LEAN_RING_WORDS1; }
+// their occupancy), at most LEAN_DIR_MAXSPAN buckets
+constexpr uint32_t LEAN_DIR_WORDS0 = 1536;
+constexpr uint32_t LEAN_DIR_WORDS1 = 1024;
+constexpr uint32_t LEAN_DIR_MAXSPAN = 8;
+constexpr uint32_t lean_dir_words(uint32_t nl) { return nl == 0 ? LEAN_DIR_WORDS0 : LEAN_DIR_WORDS1; }
 
 enum Flag : uint32_t {
   FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u,

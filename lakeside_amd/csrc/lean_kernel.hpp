@@ -68,16 +68,16 @@ struct LeanHash {           // hash mode: the LDS hash table (lds_merge's layout
 template <int NL>
 struct LeanLds {
   static constexpr int NLA = NL > 0 ? NL : 1;
-  static constexpr uint32_t RW = lean_ring_words(NL);
+  static constexpr uint32_t RW = lean_dir_words(NL);
   LeanRun runs[RUN_CAP];
   uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
   uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
   uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
-  // The tile's aggregation table: the hash table, or the direct table (the tile's buckets x ngroups cells, P.ring_cw
+  // The tile's aggregation table: the hash table, or the direct table (the tile's buckets x ngroups cells, P.dir_planes
   // u64 planes: value (SUM: hi), SUM: lo, rows when the table keeps them)
   union {
     LeanHash hs;
-    unsigned long long ring[RW];
+    unsigned long long dir[RW];
   } agg;
   uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
   // late columns (NL > 0): value runs (+ sentinel), run-block tables, lookup values, the late conjuncts' table
@@ -170,12 +170,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
   uint64_t pbytes = 0;
 
   // ---- the tile's aggregation table ----
-  // Direct table (P.ring_w > 0: a dense table whose group space fits LDS, and the tile's buckets -- zone map clipped
-  // to the window -- number at most ring_w): cell (bucket - tbl) * ngroups + group, indexed without key or probe.
+  // Direct table (P.dir_span > 0: a dense table whose group space fits LDS, and the tile's buckets -- zone map clipped
+  // to the window -- number at most dir_span): cell (bucket - tbl) * ngroups + group, indexed without key or probe.
   // Otherwise the LDS hash table (lds_merge).
   int64_t tbl = 0;
   uint32_t tspan = 0;   // buckets of the direct table (0: hash table)
-  if (!HASH && P.ring_w) {
+  if (!HASH && P.dir_span) {
     auto bucket_of = [&](int64_t ts) __attribute__((always_inline)) -> int64_t {   // monotone in ts
       if (P.metrics) return (ts - P.bucket_base) / P.step;
       return ((ts - ts % P.step) - P.bucket_base) / P.step;
@@ -185,21 +185,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
     int64_t bl = bucket_of(lo_ts), bh = bucket_of(hi_ts);
     bl = bl < 0 ? 0 : bl;
     bh = bh >= int64_t(P.nbuckets) ? int64_t(P.nbuckets) - 1 : bh;
-    if (bl <= bh && bh - bl < int64_t(P.ring_w)) {
+    if (bl <= bh && bh - bl < int64_t(P.dir_span)) {
       tbl = bl;
       tspan = uint32_t(bh - bl + 1);
     }
   }
   const uint32_t ngr = tspan ? uint32_t(P.ngroups) : 0u;
-  // P.ring_rep replicas of every cell (a lane adds into replica lane % rep): lanes adding into the same few cells (the
+  // P.dir_rep replicas of every cell (a lane adds into replica lane % rep): lanes adding into the same few cells (the
   // dense query: 64 rows over 16 names) spread over rep times as many LDS addresses; combined at the flush
-  const uint32_t rep = P.ring_rep ? P.ring_rep : 1u;
+  const uint32_t rep = P.dir_rep ? P.dir_rep : 1u;
   const uint32_t myrep = uint32_t(lane) & (rep - 1u);
   const uint32_t ndir = tspan * ngr * rep;                          // direct cells (replicas included)
-  unsigned long long* const rv = L.agg.ring;                         // value plane (SUM: hi)
-  unsigned long long* const rlo = L.agg.ring + ndir;                 // SUM: lo plane
-  const bool rrows_on = P.ring_cw > (AGG == AGG_SUM ? 2u : 1u);      // the table keeps rows: a rows plane
-  unsigned long long* const rrows = L.agg.ring + (P.ring_cw - 1u) * ndir;
+  unsigned long long* const rv = L.agg.dir;                         // value plane (SUM: hi)
+  unsigned long long* const rlo = L.agg.dir + ndir;                 // SUM: lo plane
+  const bool rrows_on = P.dir_planes > (AGG == AGG_SUM ? 2u : 1u);      // the table keeps rows: a rows plane
+  unsigned long long* const rrows = L.agg.dir + (P.dir_planes - 1u) * ndir;
   // empty value: SUM's -0.0 marker (no rows plane: LEAN_SUM_EXISTS), the MIN / MAX identity, COUNT 0
   const unsigned long long rident = AGG == AGG_SUM ? (rrows_on ? 0ull : NEG_ZERO_BITS) : (AGG == AGG_MIN ? ~0ull : 0ull);
   constexpr unsigned long long GBIT = 1ull << 63;                   // register-cell key: a global cell, not a direct one
