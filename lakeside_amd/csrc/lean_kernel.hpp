@@ -390,8 +390,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
-  // a register cell into the workgroup's table: its ring cell (LDS atomics), HBM (a bucket beyond the tile's ring
-  // slots), or the LDS hash table
+  // a register cell into the tile's table: its direct cell (LDS atomics), HBM (a bucket beyond the direct table's
+  // span), or the LDS hash table
   auto flush = [&]() __attribute__((always_inline)) {
     if (acc.rows == 0) return;
     if (!tspan) {
