@@ -147,6 +147,18 @@ struct Cand {
 
 }  // namespace
 
+namespace {
+// A pinned host block from the engine's pool for the length of a transfer (returned to the pool on scope exit).
+struct PinnedTmp {
+  HostBlock b;
+  explicit PinnedTmp(size_t n) : b(pinned_acquire(n)) {}
+  ~PinnedTmp() { pinned_release(b); }
+  PinnedTmp(const PinnedTmp&) = delete;
+  PinnedTmp& operator=(const PinnedTmp&) = delete;
+  void* p() const { return b.p; }
+};
+}  // namespace
+
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
                       int glob_size, unsigned flags, bool dist, lk_result* res) {
   const auto t_start = std::chrono::steady_clock::now();
@@ -608,11 +620,14 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     XHIP_TRY(hipEventRecord(e0, st));
     XHIP_TRY(launch_ex_scan(P, st));
     XHIP_TRY(hipEventRecord(e1, st));
-    std::vector<unsigned long long> h_out(total * 2);
-    uint32_t got = 0;
-    XHIP_TRY(hipMemcpyAsync(h_out.data(), d_out, total * 16, hipMemcpyDeviceToHost, st));
-    XHIP_TRY(hipMemcpyAsync(&got, dbuf + o_n, 4, hipMemcpyDeviceToHost, st));
+    // pinned destinations: a device-to-host copy into pageable memory goes through the runtime's staging buffers
+    PinnedTmp eo(total * 16 + 64);
+    const unsigned long long* h_out = static_cast<const unsigned long long*>(eo.p());
+    XHIP_TRY(hipMemcpyAsync(eo.p(), d_out, total * 16, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipMemcpyAsync(static_cast<uint8_t*>(eo.p()) + total * 16, dbuf + o_n, 4, hipMemcpyDeviceToHost, st));
     XHIP_TRY(hipStreamSynchronize(st));
+    uint32_t got = 0;
+    memcpy(&got, static_cast<const uint8_t*>(eo.p()) + total * 16, 4);
     float ms = 0.f;
     XHIP_TRY(hipEventElapsedTime(&ms, e0, e1));
     scan_ms += ms;
@@ -684,12 +699,13 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
         gc = GCol{S.d_data, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, 0u};
       }
     }
-    std::vector<unsigned long long> sel(nsel);
-    for (size_t i = 0; i < nsel; i++) sel[i] = stream[i]->ref;
     const size_t gb = gcols.size() * sizeof(GCol), sb = nsel * 8, vb = nsel * ncols * 8, ob = nsel * ncols;
+    PinnedTmp gio(gb + sb + vb + ob + 64);   // pinned staging both ways: [columns | selected refs | values | ok]
+    uint8_t* hg = static_cast<uint8_t*>(gio.p());
+    memcpy(hg, gcols.data(), gb);
+    for (size_t i = 0; i < nsel; i++) reinterpret_cast<unsigned long long*>(hg + gb)[i] = stream[i]->ref;
     uint8_t* dg = static_cast<uint8_t*>(X.workspace("xgather", gb + sb + vb + ob + 1024));
-    XHIP_TRY(hipMemcpyAsync(dg, gcols.data(), gb, hipMemcpyHostToDevice, st));
-    XHIP_TRY(hipMemcpyAsync(dg + gb, sel.data(), sb, hipMemcpyHostToDevice, st));
+    XHIP_TRY(hipMemcpyAsync(dg, hg, gb + sb, hipMemcpyHostToDevice, st));
     GParams G{};
     G.cols = reinterpret_cast<const GCol*>(dg);
     G.sel = reinterpret_cast<const unsigned long long*>(dg + gb);
@@ -698,9 +714,10 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     G.val = reinterpret_cast<unsigned long long*>(dg + gb + sb);
     G.ok = dg + gb + sb + vb;
     XHIP_TRY(launch_ex_gather(G, st));
-    XHIP_TRY(hipMemcpyAsync(gval.data(), G.val, vb, hipMemcpyDeviceToHost, st));
-    XHIP_TRY(hipMemcpyAsync(gok.data(), G.ok, ob, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipMemcpyAsync(hg + gb + sb, G.val, vb + ob, hipMemcpyDeviceToHost, st));   // values and ok flags
     XHIP_TRY(hipStreamSynchronize(st));
+    memcpy(gval.data(), hg + gb + sb, vb);
+    memcpy(gok.data(), hg + gb + sb + vb, ob);
   }
 
   // ---- rows: timestamp, getDouble(value) (SQL NULL -> 0.0), tags as JDBC getString text ----
