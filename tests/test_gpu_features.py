@@ -344,3 +344,49 @@ def test_sums_subnormal_and_cancelling(engine, tmp_path):
             assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"{agg} glob {gi}")
         merged = engine.eval_pushdown(req, paths, 2, LK_MERGED).rows()
         assert_rows_equal(merged, dx.merge_glob_cells(pr, cells), agg, f"{agg} merged")
+
+
+def test_lean_direct_table_planes(engine):
+    """scan_lean's per-tile direct table in every layout: segments with NULL values next to NULL-free ones (the table
+    keeps a rows plane: no lean bits), NULL-free sets (SUM's -0.0 marker, MIN/MAX existence by the extreme), replicas
+    per cell, per-glob rows and merged rows, the dense path (every name passes), and LK_NO_DIRECT (the LDS hash) giving
+    the same rows."""
+    import os
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    sets = {}
+    for label, nulls in (("clean", [0.0, 0.0, 0.0]), ("mixed", [0.0, 0.05, 0.0])):
+        keys, blobs, segs = [], [], []
+        for i, nf in enumerate(nulls):
+            s = synth.make_segment(synth.segment_spec(40 + i, rows=1 << 19, null_frac=nf, rg_rows=1 << 18,
+                                                      page_rows=1 << 15, value_mode=1, hour=0))
+            key = f"dt/{label}/{i}"
+            engine.put_segment_ptr(key, s.ptr, s.size)
+            blobs.append(s.bytes())
+            s.free()
+            keys.append(key)
+            segs.append(synth.segment_request(40 + i, hour=0))
+        sets[label] = (keys, blobs, segs)
+    for label, (keys, blobs, segs) in sets.items():
+        for filt, agg, gbs in [(synth.leaf(synth.NAME, "eq", "metric_07"), "sum", []),
+                               (synth.leaf(synth.NAME, "in", *[f"metric_{k:02d}" for k in range(16)]), "sum", []),
+                               (synth.leaf(synth.NAME, "in", *[f"metric_{k:02d}" for k in range(16)]), "max", []),
+                               (synth.leaf(synth.NAME, "in", "metric_01", "metric_05"), "min", [synth.SERVICE]),
+                               (synth.leaf(synth.NAME, "eq", "metric_03"), "avg", [synth.SERVICE]),
+                               (synth.leaf(synth.NAME, "in", "metric_02", "metric_09"), "count", [])]:
+            req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+            pr = dx.parse_pushdown(req)
+            cells = dx.evaluate_glob_cells(pr, 2, keys, sources=blobs)
+            got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+            for gi, (g, cs) in enumerate(zip(got.per_glob(len(cells)), cells)):
+                assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"{label} {agg} {gbs} glob {gi}")
+            merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+            assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, f"{label} {agg} {gbs} merged")
+            os.environ["LK_NO_DIRECT"] = "1"
+            try:
+                hashed = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+            finally:
+                del os.environ["LK_NO_DIRECT"]
+            assert list(hashed.ts) == list(merged.ts) and hashed.tags == merged.tags
+            if agg not in ("sum", "avg"):
+                assert np.array_equal(hashed.values.view(np.uint64), merged.values.view(np.uint64))
