@@ -756,6 +756,80 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     throw PlanError(LK_ERR_UNSUPPORTED, "cell key space beyond 64 bits");
   const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
 
+  // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
+  std::vector<uint32_t> truth, truth_early, truth_late;
+  uint32_t late_mask = 0;
+  int early = -1;   // the string column (strs index) of the single-column early conjuncts, when there is one
+  if (leaves.size() <= size_t(TT_MAX_LEAVES)) {
+    const uint32_t L = uint32_t(leaves.size());
+    truth = truth_table(prog, L);
+    // Predicate pushdown + late materialization.  filter = C_early AND C_late where C_early is the conjuncts
+    // over one "early" column (the name column when a conjunct constrains it alone).  The kernel decodes the
+    // early column for every row, lists the rows where C_early is TRUE, and decodes every other string column
+    // (late filter columns, group dims) only for listed rows, where it evaluates C_late.
+    std::vector<const FilterNode*> conj;
+    conjuncts(R.filter.get(), conj);
+    auto cols_of = [&](const FilterNode* n) {
+      std::vector<const FilterNode*> ls;
+      collect_leaves(n, ls);
+      uint32_t m = 0;
+      for (auto* l : ls) m |= numeric_op(l->op) ? (1u << 31) : (1u << str_index(l->k));   // no StrCol for numbers
+      return m;
+    };
+    // A conjunct of only `exists`/`has` leaves (IS NOT NULL: passes nearly every row, e.g. the one query-api adds
+    // to a tag query) is a poor early filter: it is chosen only when no other single-column conjunct exists.
+    auto weak = [&](const FilterNode* n) {
+      std::vector<const FilterNode*> ls;
+      collect_leaves(n, ls);
+      return std::all_of(ls.begin(), ls.end(), [](const FilterNode* l) { return l->op == "exists" || l->op == "has"; });
+    };
+    bool early_weak = true;
+    for (auto* c : conj) {
+      const uint32_t m = cols_of(c);
+      if (__builtin_popcount(m) != 1) continue;
+      const int col = __builtin_ctz(m);
+      const bool w = weak(c);
+      if (early < 0 || (early_weak && !w) || (w == early_weak && col == 0)) {
+        early = col;
+        early_weak = w;
+      }
+    }
+    // The late pass sees only the late columns' leaves: a conjunct mixing the early column with others keeps
+    // every column early (no late pass).
+    bool mixed = false;
+    for (auto* c : conj) {
+      const uint32_t m = cols_of(c);
+      if (early >= 0 && m != (1u << early) && ((m >> early) & 1u)) mixed = true;
+    }
+    if (early >= 0 && strs.size() >= 2 && !mixed && !numeric) {
+      std::vector<uint8_t> pe, pl;
+      for (auto* c : conj) {
+        std::vector<uint8_t>& dst = cols_of(c) == (1u << early) ? pe : pl;
+        const bool first = dst.empty();
+        postfix(c, leaves, dst);
+        if (!first) dst.push_back(OP_AND);
+      }
+      truth_early = truth_table(pe, L);
+      truth_late = truth_table(pl, L);
+      for (size_t sidx = 0; sidx < strs.size(); sidx++)
+        if (int(sidx) != early) late_mask |= 1u << sidx;
+    }
+  }
+  // Device order of the string columns (query column 2 + dev_of[s]): the early column first when the filter's late
+  // materialization lists every other column late, so scan_lean (whose early column is query column 2) takes the
+  // query even when the leading group dim -- a tag query's tag, a :by column -- is not the filter's early column.
+  std::vector<int> dev_of(strs.size());
+  for (size_t i = 0; i < strs.size(); i++) dev_of[i] = int(i);
+  // (opt-in until its GPU run: LK_EARLY_FIRST=1)
+  if (late_mask && early > 0 && strs.size() <= 3 && getenv("LK_EARLY_FIRST")) {
+    std::swap(dev_of[0], dev_of[size_t(early)]);
+    uint32_t m = 0;
+    for (size_t i = 0; i < strs.size(); i++)
+      if ((late_mask >> i) & 1u) m |= 1u << dev_of[i];
+    late_mask = m;
+  }
+  const int lead = dev_of[0] == 0 ? 0 : int(std::find(dev_of.begin(), dev_of.end(), 0) - dev_of.begin());   // strs index at device 0
+
   // ---- per-segment query descriptors ----
   // `qsegs` go to the fused kernels (scan_lean / scan_tiles: INT64 timestamps, DOUBLE values); `gsegs` to the general
   // row scan (ex_scan AGG mode): every segment of a numeric-leaf query, and segments whose timestamp or value column
@@ -811,7 +885,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
       if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
-      for (size_t s = 0; s < strs.size(); s++) bind(int(2 + s), strs[s].name, true);
+      for (size_t s = 0; s < strs.size(); s++) bind(2 + dev_of[s], strs[s].name, true);
       for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
       if (general) {
         q.tile_begin = total_tiles;
@@ -824,10 +898,11 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       // name page has a small dictionary (lean_tile's test at page granularity)
       if (all_lean) {
         const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
-        const int cn = strs.size() <= 3 ? S.col_index(strs[0].name) : -1;
-        all_lean = ct >= 0 && cv >= 0 && cn >= 0 && !S.cols[ct].any_nulls && !S.cols[cv].any_nulls &&
+        const int cn = strs.size() <= 3 ? S.col_index(strs[size_t(lead)].name) : -1;
+        all_lean = ct >= 0 && (cv >= 0 || tagq) && cn >= 0 && !S.cols[ct].any_nulls && (tagq || !S.cols[cv].any_nulls) &&
                    !S.cols[cn].any_nulls;
-        for (size_t s2 = 1; s2 < strs.size() && all_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
+        for (size_t s2 = 0; s2 < strs.size() && all_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
+          if (int(s2) == lead) continue;
           const int cl = S.col_index(strs[s2].name);
           if (cl < 0) continue;
           if (S.cols[cl].any_nulls || !S.cols[cl].pages_lean_late) all_lean = false;
@@ -855,65 +930,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   uint32_t max_tiles = 0, gmax_tiles = 0;
   for (auto& q : qsegs) max_tiles = std::max(max_tiles, q.ntiles);
   for (auto& q : gsegs) gmax_tiles = std::max(gmax_tiles, q.ntiles);
-  // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
-  std::vector<uint32_t> truth, truth_early, truth_late;
-  uint32_t late_mask = 0;
-  if (leaves.size() <= size_t(TT_MAX_LEAVES)) {
-    const uint32_t L = uint32_t(leaves.size());
-    truth = truth_table(prog, L);
-    // Predicate pushdown + late materialization.  filter = C_early AND C_late where C_early is the conjuncts
-    // over one "early" column (the name column when a conjunct constrains it alone).  The kernel decodes the
-    // early column for every row, lists the rows where C_early is TRUE, and decodes every other string column
-    // (late filter columns, group dims) only for listed rows, where it evaluates C_late.
-    std::vector<const FilterNode*> conj;
-    conjuncts(R.filter.get(), conj);
-    auto cols_of = [&](const FilterNode* n) {
-      std::vector<const FilterNode*> ls;
-      collect_leaves(n, ls);
-      uint32_t m = 0;
-      for (auto* l : ls) m |= numeric_op(l->op) ? (1u << 31) : (1u << str_index(l->k));   // no StrCol for numbers
-      return m;
-    };
-    // A conjunct of only `exists`/`has` leaves (IS NOT NULL: passes nearly every row, e.g. the one query-api adds
-    // to a tag query) is a poor early filter: it is chosen only when no other single-column conjunct exists.
-    auto weak = [&](const FilterNode* n) {
-      std::vector<const FilterNode*> ls;
-      collect_leaves(n, ls);
-      return std::all_of(ls.begin(), ls.end(), [](const FilterNode* l) { return l->op == "exists" || l->op == "has"; });
-    };
-    int early = -1;
-    bool early_weak = true;
-    for (auto* c : conj) {
-      const uint32_t m = cols_of(c);
-      if (__builtin_popcount(m) != 1) continue;
-      const int col = __builtin_ctz(m);
-      const bool w = weak(c);
-      if (early < 0 || (early_weak && !w) || (w == early_weak && col == 0)) {
-        early = col;
-        early_weak = w;
-      }
-    }
-    // The late pass sees only the late columns' leaves: a conjunct mixing the early column with others keeps
-    // every column early (no late pass).
-    bool mixed = false;
-    for (auto* c : conj) {
-      const uint32_t m = cols_of(c);
-      if (early >= 0 && m != (1u << early) && ((m >> early) & 1u)) mixed = true;
-    }
-    if (early >= 0 && strs.size() >= 2 && !mixed && !numeric) {
-      std::vector<uint8_t> pe, pl;
-      for (auto* c : conj) {
-        std::vector<uint8_t>& dst = cols_of(c) == (1u << early) ? pe : pl;
-        const bool first = dst.empty();
-        postfix(c, leaves, dst);
-        if (!first) dst.push_back(OP_AND);
-      }
-      truth_early = truth_table(pe, L);
-      truth_late = truth_table(pl, L);
-      for (size_t sidx = 0; sidx < strs.size(); sidx++)
-        if (int(sidx) != early) late_mask |= 1u << sidx;
-    }
-  }
   // ---- table mode ----
   // Dense: array index = cell key = (glob slot, bucket, group).  Hash (SURVEY §2.2 K4 spill, high cardinality):
   // an open-addressing table keyed by the cell key, first sized from a bound on the distinct cells and grown
@@ -958,11 +974,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   P.ncells = ncells;
   std::vector<StrParam> strp(strs.size());
   for (size_t s = 0; s < strs.size(); s++) {
-    strp[s].dim_null = strs[s].dim_null;
-    strp[s].dim_stride = strs[s].is_dim ? uint32_t(strs[s].stride) : 0u;
-    strp[s].lbase = strs[s].lbase;
-    strp[s].lmask = strs[s].lmask;
-    strp[s].hmask = strs[s].hmask;
+    StrParam& sp = strp[size_t(dev_of[s])];   // device order (query column 2 + dev_of[s])
+    sp.dim_null = strs[s].dim_null;
+    sp.dim_stride = strs[s].is_dim ? uint32_t(strs[s].stride) : 0u;
+    sp.lbase = strs[s].lbase;
+    sp.lmask = strs[s].lmask;
+    sp.hmask = strs[s].hmask;
   }
   memcpy(P.prog, prog.data(), prog.size());
   if (const char* ab = getenv("LK_ABLATE")) P.ablate = uint32_t(atoi(ab));   // diagnostics only
@@ -1025,9 +1042,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   for (size_t s = 0; s < strs.size(); s++)
     if (need_tab[s]) {
       memcpy(hbuf + o_tab[s], tabs[s].data(), tabs[s].size() * 4);
-      strp[s].strtab = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
+      strp[size_t(dev_of[s])].strtab = reinterpret_cast<const uint32_t*>(dbuf + o_tab[s]);
     } else if (strs[s].exchanged) {
-      strp[s].strtab = strs[s].uni->d_dim_of_gid;   // resident (dims.cpp)
+      strp[size_t(dev_of[s])].strtab = strs[s].uni->d_dim_of_gid;   // resident (dims.cpp)
     }
   memcpy(hbuf + o_strp, strp.data(), strp.size() * sizeof(StrParam));
   memset(hbuf + o_flags, 0, 16);
@@ -1055,7 +1072,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // (<= 2 of them): NULL-free tiles with a small name dictionary go to scan_lean (lean_kernel.hpp), the rest to
   // scan_tiles
   const bool lean_shape = P.nstr == 1 || (P.nstr <= 3 && P.late_mask == ((1u << P.nstr) - 2u));
-  P.lean_split = (lean_shape && P.truth && agg != AGG_ROWS && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
+  P.rows_only = tagq ? 1u : 0u;   // COUNT(*): no value column is bound (lean tiles need none)
+  P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric) P.lean = 0;   // the general row scan accumulates every table field
   // scan_lean: a dense table whose group space fits LDS for the few buckets a tile spans is aggregated in the tile's

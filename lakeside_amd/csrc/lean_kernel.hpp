@@ -92,12 +92,13 @@ struct LeanLds {
 // The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
 // same test to skip it.  Late columns (query columns 3 .. 2 + nl) must hold no NULL over the tile (value index =
 // row) or be absent from the segment.
-__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t, uint32_t nl) {
-  if (!Sp->cols[0].present || !Sp->cols[1].present || !Sp->cols[2].present) return false;
+__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t, uint32_t nl, uint32_t rows_only) {
+  if (!Sp->cols[0].present || !Sp->cols[2].present) return false;
+  if (!Sp->cols[1].present && !rows_only) return false;   // COUNT(*) reads no value column
   const TileCol* a = Sp->cols[0].tcols + t;
-  const TileCol* b = Sp->cols[1].tcols + t;
   const TileCol* c = Sp->cols[2].tcols + t;
-  if (a->has_nulls || b->has_nulls || c->has_nulls || c->kind != PAGE_DICT || c->dict_n > 64u || c->nruns == 0u ||
+  if (Sp->cols[1].present && Sp->cols[1].tcols[t].has_nulls) return false;
+  if (a->has_nulls || c->has_nulls || c->kind != PAGE_DICT || c->dict_n > 64u || c->nruns == 0u ||
       c->bw < 1u || c->bw > 6u)
     return false;
   for (uint32_t k = 0; k < nl; k++) {
@@ -158,9 +159,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
   const TileDesc* tdp = Sp->tiles + t;
   const int64_t win_lo = Sp->win_lo, win_hi = Sp->win_hi;
   if (tdp->ts_max < win_lo || tdp->ts_min >= win_hi) return;    // zone map: outside the glob window
-  if (!lean_tile(Sp, t, NL)) return;
+  if (!lean_tile(Sp, t, NL, P.rows_only)) return;
   const TileCol* tc0 = Sp->cols[0].tcols + t;
-  const TileCol* tc1 = Sp->cols[1].tcols + t;
+  const TileCol* tc1 = Sp->cols[1].present ? Sp->cols[1].tcols + t : tc0;   // COUNT(*): never read
   const TileCol* tc2 = Sp->cols[2].tcols + t;
   const uint32_t nrows = tdp->nrows;
   const uint32_t nr = tc2->nruns, dict_n = tc2->dict_n, bw = tc2->bw;

@@ -320,7 +320,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(NSTR == 1
   if (t >= Sp->ntiles) return;
   const TileDesc* tdp = Sp->tiles + t;
   if (tdp->ts_max < Sp->win_lo || tdp->ts_min >= Sp->win_hi) return;   // zone map: outside the glob window
-  if (P.lean_split && lean_tile(Sp, t, P.nstr - 1)) return;             // scan_lean's tile
+  if (P.lean_split && lean_tile(Sp, t, P.nstr - 1, P.rows_only)) return;             // scan_lean's tile
   const uint32_t tile_nrows = tdp->nrows;
 
   // ---- stage per-tile column state, run windows, lookup values, truth table; clear the LDS table ----
