@@ -1,0 +1,25 @@
+#!/bin/bash
+# GPU-box, round 4: the GPU suite (optionally under an env such as LK_EARLY_FIRST=1 via TEST_ENV), then bench lines
+# for $QUERIES under each env in $ENVS ("-" = none), then optional rocprofv3 kernel stats for $PROF_QUERIES.
+# Stops at the first failing step.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out/r4
+export TMPDIR=/tmp
+if [ -z "$NOTESTS" ]; then
+  env $TEST_ENV timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread ${TESTS:-} > gpurun_out/r4/tests.log 2>&1
+  rc=$?; tail -5 gpurun_out/r4/tests.log; [ $rc -eq 0 ] || exit $rc
+fi
+for e in ${ENVS:--}; do
+  ee=""; [ "$e" != "-" ] && ee="$e"
+  tag=$(echo "${e}" | tr '=,' '__')
+  for q in ${QUERIES:-}; do
+    cs=0; [ -n "$VALIDATE" ] && [ "$q" != tag ] && [ "$q" != dense ] && [ "$q" != c5 ] && [ "$q" != exemplar ] && cs=-1
+    env $ee timeout -k 10 ${PER:-400} python3 bench.py --query $q --steps ${STEPS:-10} --warmup 3 --cpu-sample $cs $BENCH_ARGS > gpurun_out/r4/${q}_${tag}.json 2> gpurun_out/r4/${q}_${tag}.log || exit $?
+    echo "== $q [$e]"; grep -h "scan kernel\|validation" gpurun_out/r4/${q}_${tag}.log | sed 's/; in the call.*//'
+  done
+done
+for q in ${PROF_QUERIES:-}; do
+  env $PROF_ENV timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/kt_$q -o kt --output-format csv -- python3 bench.py --query $q --steps 5 --warmup 2 --cpu-sample 0 > gpurun_out/r4/kt_$q.json 2> gpurun_out/r4/kt_$q.log || exit $?
+  head -6 gpurun_out/r4/kt_$q/kt_kernel_stats.csv
+done
+exit 0
