@@ -51,25 +51,39 @@ namespace lk {
 
 // Shared host result blocks (one node; comm_emit_begin): rank 0 owns a small pool of POSIX shared-memory blocks,
 // every rank maps and registers them with HIP once per block generation, and each rank's GPU writes its key range's
-// result rows straight into rank 0's result over its own PCIe link.
-struct ShmMap {
+// result rows straight into rank 0's result over its own PCIe link.  A mapping is its own reference-counted object:
+// the pool entry holds one reference and a result whose rows live in the block holds another (through its lease),
+// so a result outlives the engine and communicator that produced it.  The name is unlinked as soon as
+// every rank has mapped the generation, so a crashed process leaves nothing behind in /dev/shm.
+struct ShmBlock {
   std::string name;
-  uint64_t gen = 0;
   void* host = nullptr;
   void* dev = nullptr;
   size_t cap = 0;
-  bool owner = false;           // rank 0: created (and unlinks) it
-  std::weak_ptr<void> lease;    // rank 0: the result currently holding the block
-  void release() {
+  bool linked = false;          // rank 0: the name still exists in /dev/shm
+  ~ShmBlock() {
     if (host) {
       (void)hipHostUnregister(host);
       (void)hipGetLastError();
       munmap(host, cap);
     }
-    if (owner && !name.empty()) shm_unlink(name.c_str());
-    host = dev = nullptr;
-    cap = 0;
+    if (linked) shm_unlink(name.c_str());
   }
+  void unlink() {
+    if (linked) shm_unlink(name.c_str());
+    linked = false;
+  }
+};
+struct ShmMap {
+  std::shared_ptr<ShmBlock> blk;
+  uint64_t gen = 0;
+  std::weak_ptr<void> lease;    // rank 0: the result currently holding the block
+  size_t cap() const { return blk ? blk->cap : 0; }
+  void release() { blk.reset(); }
+};
+// A result's hold on a block: keeps the mapping alive and marks the pool entry busy.
+struct ShmLease {
+  std::shared_ptr<ShmBlock> blk;
 };
 
 struct Comm {
@@ -83,9 +97,7 @@ struct Comm {
   // (and checks) every RCCL data-path call the 8-GPU run makes.
   bool loopback = false;
   bool active() const { return world > 1 || loopback; }
-  virtual ~Comm() {
-    for (auto& kv : shm) kv.second.release();
-  }
+  virtual ~Comm() = default;   // mappings go with their last reference (pool entry or a live result)
   // host blobs of every rank, rank order
   virtual std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) = 0;
   // `bytes[r]` of device memory from every rank r into rank 0's `recv` at offsets `off[r]` (slot 0 is left
@@ -182,57 +194,90 @@ struct HostComm final : Comm {
   void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
                       const std::vector<size_t>& off) override {
     if (world == 1) return;
-    HIP_TRY2(hipSetDevice(E.device));
+    // each rank's block travels behind an 8-byte status: a rank whose device copy failed still takes part in the
+    // all-gather, and every rank then throws that failure (none is left inside the collective)
     size_t mx = 1;
     for (size_t b : bytes) mx = std::max(mx, b);
-    std::vector<uint8_t> mine(mx, 0), all(size_t(world) * mx);
-    if (bytes[size_t(rank)]) {
-      HIP_TRY2(hipMemcpyAsync(mine.data(), send, bytes[size_t(rank)], hipMemcpyDeviceToHost, X.stream));
-      HIP_TRY2(hipStreamSynchronize(X.stream));
+    std::vector<uint8_t> mine(8 + mx, 0), all(size_t(world) * (8 + mx));
+    uint64_t status = 0;
+    comm_local(X, [&] {
+      fault_point(E, "gather");
+      HIP_TRY2(hipSetDevice(E.device));
+      if (bytes[size_t(rank)]) {
+        HIP_TRY2(hipMemcpyAsync(mine.data() + 8, send, bytes[size_t(rank)], hipMemcpyDeviceToHost, X.stream));
+        HIP_TRY2(hipStreamSynchronize(X.stream));
+      }
+    });
+    if (X.pend_code) status = uint64_t(uint32_t(X.pend_code));
+    memcpy(mine.data(), &status, 8);
+    allgather(mine.data(), 8 + mx, all.data());
+    for (int r = 0; r < world; r++) {
+      uint64_t st;
+      memcpy(&st, all.data() + size_t(r) * (8 + mx), 8);
+      if (st) {
+        const std::string m = r == rank ? X.pend_msg : "rank " + std::to_string(r) + ": device copy of its table failed";
+        X.pend_code = 0;
+        X.pend_msg.clear();
+        throw PlanError(int(st), m);
+      }
     }
-    allgather(mine.data(), mx, all.data());
-    if (rank == 0) {
+    if (rank == 0) {   // the last step of the gather: rank 0 alone
       for (int r = 1; r < world; r++)
         if (bytes[size_t(r)])
-          HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * mx,
+          HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * (8 + mx) + 8,
                                   bytes[size_t(r)], hipMemcpyHostToDevice, X.stream));
       HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed on return
     }
   }
 
   void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) override {
-    HIP_TRY2(hipSetDevice(E.device));
     // one all-gather round per destination d: every rank contributes its pieces for d, concatenated (padded to
-    // the largest contribution); d unpacks each source's bytes into its receive pieces from that source, in order
+    // the largest contribution); d unpacks each source's bytes into its receive pieces from that source, in order.
+    // Each round's size all-gather carries every rank's status (a failed device copy -- of this round, or the
+    // previous round's unpacking -- fails every rank there); the last round's unpacking failure stays pending for
+    // the caller's next agreement point.
     for (int d = 0; d < world; d++) {
       size_t mine_n = 0;
       for (const Piece& p : sends)
         if (p.peer == d && d != rank) mine_n += p.bytes;
-      uint64_t n64 = mine_n;
-      std::vector<uint64_t> sz(static_cast<size_t>(world));
-      allgather(&n64, 8, sz.data());
-      size_t mx = 1;
-      for (uint64_t x : sz) mx = std::max(mx, size_t(x));
-      std::vector<uint8_t> buf(mx, 0), all(d == rank ? size_t(world) * mx : 0);
-      size_t o = 0;
-      for (const Piece& p : sends)
-        if (p.peer == d && d != rank && p.bytes) {
-          HIP_TRY2(hipMemcpyAsync(buf.data() + o, p.ptr, p.bytes, hipMemcpyDeviceToHost, X.stream));
-          o += p.bytes;
+      std::vector<uint8_t> buf(std::max<size_t>(mine_n, 1), 0);
+      comm_local(X, [&] {
+        HIP_TRY2(hipSetDevice(E.device));
+        size_t o = 0;
+        for (const Piece& p : sends)
+          if (p.peer == d && d != rank && p.bytes) {
+            HIP_TRY2(hipMemcpyAsync(buf.data() + o, p.ptr, p.bytes, hipMemcpyDeviceToHost, X.stream));
+            o += p.bytes;
+          }
+        HIP_TRY2(hipStreamSynchronize(X.stream));
+      });
+      uint64_t hdr[2] = {mine_n, uint64_t(uint32_t(X.pend_code))};
+      std::vector<uint64_t> sz2(size_t(world) * 2);
+      allgather(hdr, 16, sz2.data());
+      for (int r = 0; r < world; r++)
+        if (sz2[size_t(r) * 2 + 1]) {
+          const std::string m = r == rank ? X.pend_msg : "rank " + std::to_string(r) + ": device copy of its exchange pieces failed";
+          X.pend_code = 0;
+          X.pend_msg.clear();
+          throw PlanError(int(sz2[size_t(r) * 2 + 1]), m);
         }
-      HIP_TRY2(hipStreamSynchronize(X.stream));
-      std::vector<uint8_t> sink(d == rank ? 0 : size_t(world) * mx);
-      allgather(buf.data(), mx, d == rank ? all.data() : sink.data());
+      size_t mx = 1;
+      for (int r = 0; r < world; r++) mx = std::max(mx, size_t(sz2[size_t(r) * 2]));
+      buf.resize(mx, 0);
+      std::vector<uint8_t> all(size_t(world) * mx);
+      allgather(buf.data(), mx, all.data());
       if (d != rank) continue;
-      std::vector<size_t> cur(size_t(world), 0);
-      for (const Piece& p : recvs) {
-        if (p.peer == rank || !p.bytes) continue;
-        size_t& c = cur[size_t(p.peer)];
-        if (c + p.bytes > sz[size_t(p.peer)]) throw PlanError(LK_ERR_DEVICE, "host transport: exchange size mismatch");
-        HIP_TRY2(hipMemcpyAsync(p.ptr, all.data() + size_t(p.peer) * mx + c, p.bytes, hipMemcpyHostToDevice, X.stream));
-        c += p.bytes;
-      }
-      HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed at the end of the round
+      comm_local(X, [&] {
+        std::vector<size_t> cur(size_t(world), 0);
+        for (const Piece& p : recvs) {
+          if (p.peer == rank || !p.bytes) continue;
+          size_t& c = cur[size_t(p.peer)];
+          if (c + p.bytes > sz2[size_t(p.peer) * 2]) throw PlanError(LK_ERR_DEVICE, "host transport: exchange size mismatch");
+          HIP_TRY2(hipMemcpyAsync(p.ptr, all.data() + size_t(p.peer) * mx + c, p.bytes, hipMemcpyHostToDevice, X.stream));
+          c += p.bytes;
+        }
+        HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed at the end of the round
+      });
     }
   }
 };
@@ -253,37 +298,52 @@ static Comm& need_comm(Engine& E) {
   return *E.comm;
 }
 
-void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n) {
+std::vector<std::string> comm_allgather_status(Engine& E, CallCtx& X, int code, const std::string& msg,
+                                               const std::string& payload) {
   Comm& C = need_comm(E);
-  if (!C.active()) return;
-  std::vector<std::string> all = C.allgather_bytes(E, X, std::string(reinterpret_cast<const char*>(host), n));
+  std::string m = msg;
+  if (!code && X.pend_code) {   // a failure met after an earlier collective step travels with this agreement
+    code = X.pend_code;
+    m = X.pend_msg;
+  }
+  X.pend_code = 0;
+  X.pend_msg.clear();
+  if (!C.active()) {
+    if (code) throw PlanError(code, m);
+    return {payload};
+  }
+  // blob: status (4 B) | message length (4 B) | message | payload
+  std::string mine(8, '\0');
+  const uint32_t ml = code ? uint32_t(m.size()) : 0u;
+  memcpy(&mine[0], &code, 4);
+  memcpy(&mine[4], &ml, 4);
+  if (code) mine += m;
+  mine += payload;
+  std::vector<std::string> all = C.allgather_bytes(E, X, mine);
+  for (int r = 0; r < C.world; r++) {
+    const std::string& b = all[size_t(r)];
+    int c = 0;
+    uint32_t l = 0;
+    if (b.size() < 8) throw PlanError(LK_ERR_DEVICE, "internal: short status blob from rank " + std::to_string(r));
+    memcpy(&c, b.data(), 4);
+    memcpy(&l, b.data() + 4, 4);
+    if (c) throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(8, l));
+  }
+  for (auto& b : all) {
+    uint32_t l = 0;
+    memcpy(&l, b.data() + 4, 4);
+    b.erase(0, 8 + size_t(l));
+  }
+  return all;
+}
+
+void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n) {
+  const std::vector<std::string> all =
+      comm_allgather_status(E, X, code, msg, std::string(reinterpret_cast<const char*>(host), n));
   for (auto& b : all) {
     if (b.size() != n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
     for (size_t i = 0; i < n; i++) host[i] = std::max(host[i], uint8_t(b[i]));
   }
-}
-
-void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n) {
-  Comm& C = need_comm(E);
-  if (!C.active()) {
-    if (code) throw PlanError(code, msg);
-    return;
-  }
-  // blob: status (4 B) | n bytes | message
-  std::string mine(4 + n, '\0');
-  memcpy(&mine[0], &code, 4);
-  memcpy(&mine[4], host, n);
-  if (code) mine += msg;
-  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
-  for (int r = 0; r < C.world; r++) {
-    const std::string& b = all[size_t(r)];
-    if (b.size() < 4 + n) throw PlanError(LK_ERR_ARG, "ranks disagree on the request (glob column union size)");
-    int c;
-    memcpy(&c, b.data(), 4);
-    if (c) throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(4 + n));
-  }
-  for (auto& b : all)
-    for (size_t i = 0; i < n; i++) host[i] = std::max(host[i], uint8_t(b[4 + i]));
 }
 
 std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) {
@@ -291,25 +351,26 @@ std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::
 }
 
 void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg) {
-  Comm& C = need_comm(E);
-  std::string mine;
-  if (code != 0) {
-    mine.resize(4);
-    memcpy(&mine[0], &code, 4);
-    mine += msg;
-  }
-  if (!C.active()) {
-    if (code) throw PlanError(code, msg);
-    return;
-  }
-  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
-  for (int r = 0; r < C.world; r++) {
-    const std::string& b = all[size_t(r)];
-    if (b.size() < 4) continue;
-    int c;
-    memcpy(&c, b.data(), 4);
-    throw PlanError(c, (r == C.rank ? std::string() : "rank " + std::to_string(r) + ": ") + b.substr(4));
-  }
+  (void)comm_allgather_status(E, X, code, msg, std::string());
+}
+
+void comm_throw_pending(CallCtx& X) {
+  if (!X.pend_code) return;
+  const int c = X.pend_code;
+  const std::string m = X.pend_msg;
+  X.pend_code = 0;
+  X.pend_msg.clear();
+  throw PlanError(c, m);
+}
+
+void fault_point(const Engine& E, const char* stage) {
+  const char* f = getenv("LK_FAULT");
+  if (!f || !*f) return;
+  const std::string spec(f);
+  const size_t at = spec.find('@');
+  if (spec.substr(0, at) != stage) return;
+  if (at != std::string::npos && atoi(spec.c_str() + at + 1) != comm_rank(E)) return;
+  throw PlanError(LK_ERR_DEVICE, std::string("injected fault at stage '") + stage + "' (LK_FAULT)");
 }
 
 void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) {
@@ -330,20 +391,35 @@ void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const
   if (C.active()) C.exchange(E, X, sends, recvs);
 }
 
+void comm_reduce_prepare(Engine& E, CallCtx& X, size_t nc) {
+  Comm& C = need_comm(E);
+  if (!C.active() || C.rank != 0) return;
+  const size_t bytes = nc * 8 * 5;
+  void* parts = X.workspace("comm_parts", size_t(C.world) * bytes);
+  // loopback: rank 0's own table makes the round trip into slot 0 (poisoned first, so a transfer that did not
+  // happen cannot pass), and the table is rebuilt from what arrived
+  if (C.loopback) HIP_TRY2(hipMemsetAsync(parts, 0xA5, bytes, X.stream));
+}
+
 void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc) {
   Comm& C = need_comm(E);
   if (!C.active()) return;
-  // the table is one contiguous block [rows | cnt | hi | lo | ext] (eval.cpp)
+  // The table is one contiguous block [rows | cnt | hi | lo | ext] (eval.cpp).  Rank 0's receive buffer was placed
+  // by comm_reduce_prepare before the scan's agreement point, so nothing between that agreement and the gather can
+  // fail on one rank alone.
   const size_t bytes = nc * 8 * 5;
-  unsigned long long* parts =
-      C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_parts", size_t(C.world) * bytes)) : nullptr;
+  unsigned long long* parts = nullptr;
+  if (C.rank == 0) {
+    auto it = X.ws.find("comm_parts");
+    if (it == X.ws.end() || it->second.cap < size_t(C.world) * bytes)
+      throw PlanError(LK_ERR_DEVICE, "internal: comm_reduce_prepare was not called");
+    parts = static_cast<unsigned long long*>(it->second.p);
+  }
   std::vector<size_t> sz(size_t(C.world), bytes), off(size_t(C.world));
   for (int r = 0; r < C.world; r++) off[size_t(r)] = size_t(r) * bytes;
-  // loopback: rank 0's own table makes the round trip into slot 0 (poisoned first, so a transfer that did not
-  // happen cannot pass), and the table is rebuilt from what arrived
-  if (C.loopback && C.rank == 0) HIP_TRY2(hipMemsetAsync(parts, 0xA5, bytes, X.stream));
   C.gather_to_root(E, X, P.rows, parts, sz, off);
-  if (C.rank == 0) {
+  if (C.rank == 0) {   // after the last collective: rank 0 alone
+    fault_point(E, "merge");
     if (C.loopback) HIP_TRY2(hipMemcpyAsync(P.rows, parts, bytes, hipMemcpyDeviceToDevice, X.stream));
     TableRef T{P.rows, P.cnt, P.hi, P.lo, P.ext};
     HIP_TRY2(launch_merge_tables(T, parts, C.world, nc, agg, X.stream));
@@ -353,28 +429,33 @@ void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t 
 void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long long& cap) {
   Comm& C = need_comm(E);
   if (!C.active()) return;
-  // this rank's occupied slots -> compact records [key | rows | cnt | hi | lo | ext]
-  SParams S{};
-  S.keys = P.hkeys;
-  S.rows = P.rows;
-  S.cnt = P.cnt;
-  S.hi = P.hi;
-  S.lo = P.lo;
-  S.ext = P.ext;
-  S.cap = cap;
-  const uint32_t nb = sparse_blocks(cap);
-  uint32_t* counts = static_cast<uint32_t*>(X.workspace("comm_rec_counts", (size_t(nb) + 2) * 4));
-  HIP_TRY2(launch_sparse_count(S, counts, X.stream));
+  // this rank's occupied slots -> compact records [key | rows | cnt | hi | lo | ext]; a failure here travels with
+  // the record-count all-gather
   uint32_t n = 0;
-  HIP_TRY2(hipMemcpyAsync(&n, counts + nb, 4, hipMemcpyDeviceToHost, X.stream));
-  HIP_TRY2(hipStreamSynchronize(X.stream));
-  unsigned long long* recs = static_cast<unsigned long long*>(X.workspace("comm_recs", size_t(n) * 48 + 64));
-  HIP_TRY2(launch_table_records(P, cap, counts, recs, n, X.stream));
+  unsigned long long* recs = nullptr;
+  comm_local(X, [&] {
+    fault_point(E, "records");
+    SParams S{};
+    S.keys = P.hkeys;
+    S.rows = P.rows;
+    S.cnt = P.cnt;
+    S.hi = P.hi;
+    S.lo = P.lo;
+    S.ext = P.ext;
+    S.cap = cap;
+    const uint32_t nb = sparse_blocks(cap);
+    uint32_t* counts = static_cast<uint32_t*>(X.workspace("comm_rec_counts", (size_t(nb) + 2) * 4));
+    HIP_TRY2(launch_sparse_count(S, counts, X.stream));
+    HIP_TRY2(hipMemcpyAsync(&n, counts + nb, 4, hipMemcpyDeviceToHost, X.stream));
+    HIP_TRY2(hipStreamSynchronize(X.stream));
+    recs = static_cast<unsigned long long*>(X.workspace("comm_recs", size_t(n) * 48 + 64));
+    HIP_TRY2(launch_table_records(P, cap, counts, recs, n, X.stream));
+    HIP_TRY2(hipStreamSynchronize(X.stream));   // records complete before they are sent
+  });
   // record counts of every rank, then the records into rank 0 (rank order)
-  std::string mine(8, '\0');
   const uint64_t n64 = n;
-  memcpy(&mine[0], &n64, 8);
-  const std::vector<std::string> all = C.allgather_bytes(E, X, mine);
+  const std::vector<std::string> all =
+      comm_allgather_status(E, X, 0, std::string(), std::string(reinterpret_cast<const char*>(&n64), 8));
   std::vector<size_t> sz(size_t(C.world)), off(size_t(C.world));
   size_t total = 0, nrec = 0;
   for (int r = 0; r < C.world; r++) {
@@ -385,13 +466,17 @@ void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long 
     total += sz[size_t(r)];
     nrec += size_t(x);
   }
-  unsigned long long* parts =
-      C.rank == 0 ? static_cast<unsigned long long*>(X.workspace("comm_rec_parts", total + 64)) : nullptr;
-  if (C.loopback && C.rank == 0 && sz[0]) HIP_TRY2(hipMemsetAsync(parts, 0xA5, sz[0], X.stream));
-  HIP_TRY2(hipStreamSynchronize(X.stream));   // records complete before they are sent
+  // rank 0's receive buffer (sized only now): placed, then agreed on before the point-to-point gather
+  unsigned long long* parts = nullptr;
+  comm_local(X, [&] {
+    if (C.rank != 0) return;
+    parts = static_cast<unsigned long long*>(X.workspace("comm_rec_parts", total + 64));
+    if (C.loopback && sz[0]) HIP_TRY2(hipMemsetAsync(parts, 0xA5, sz[0], X.stream));
+  });
+  comm_agree(E, X, 0, std::string());
   C.gather_to_root(E, X, recs, parts, sz, off);
   if (C.rank != 0) return;
-  // rank 0: a fresh table for the union (at most nrec distinct keys, load factor <= 1/2)
+  // rank 0 (after the last collective): a fresh table for the union (at most nrec distinct keys, load factor <= 1/2)
   unsigned long long cap0 = 1 << 16;
   while (cap0 < 2 * nrec) cap0 <<= 1;
   uint8_t* tb = static_cast<uint8_t*>(X.workspace("table_merged", size_t(cap0) * 48 + 1024));
@@ -414,96 +499,103 @@ void comm_reduce_hash(Engine& E, CallCtx& X, QParams& P, int agg, unsigned long 
 
 // ---- shared host result blocks ----
 namespace {
-bool map_block(ShmMap& m, const std::string& name, size_t cap, bool create) {
+std::shared_ptr<ShmBlock> map_block(const std::string& name, size_t cap, bool create) {
   const int fd = shm_open(name.c_str(), create ? (O_CREAT | O_EXCL | O_RDWR) : O_RDWR, 0600);
-  if (fd < 0) return false;
+  if (fd < 0) return nullptr;
+  auto b = std::make_shared<ShmBlock>();
+  b->name = name;
+  b->linked = create;
   if (create && ftruncate(fd, off_t(cap)) != 0) {
     close(fd);
-    shm_unlink(name.c_str());
-    return false;
+    return nullptr;   // ~ShmBlock unlinks
   }
   void* p = mmap(nullptr, cap, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
-  if (p == MAP_FAILED) {
-    if (create) shm_unlink(name.c_str());
-    return false;
-  }
+  if (p == MAP_FAILED) return nullptr;
   void* d = nullptr;
   if (hipHostRegister(p, cap, hipHostRegisterMapped) != hipSuccess || hipHostGetDevicePointer(&d, p, 0) != hipSuccess) {
     (void)hipGetLastError();
     (void)hipHostUnregister(p);
     (void)hipGetLastError();
     munmap(p, cap);
-    if (create) shm_unlink(name.c_str());
-    return false;
+    return nullptr;
   }
-  m.name = name;
-  m.host = p;
-  m.dev = d;
-  m.cap = cap;
-  m.owner = create;
-  return true;
+  b->host = p;
+  b->dev = d;
+  b->cap = cap;
+  return b;
 }
 }  // namespace
 
 EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes) {
   Comm& C = need_comm(E);
-  HIP_TRY2(hipSetDevice(E.device));
   EmitTarget T;
-  // rank 0 picks a free block of >= bytes (growing or adding one) and announces (pid, block, generation, size)
+  // rank 0 picks a free block of >= bytes (growing or adding one) and announces (pid, block, generation, size); a
+  // pending failure of any rank travels with the announcement
   uint64_t hdr[5] = {0, 0, 0, 0, 0};   // ok, pid, block, gen, cap
   std::shared_ptr<void> lease;
   if (C.rank == 0) {
-    int pick = -1;
-    for (auto& kv : C.shm)
-      if (kv.second.lease.expired() && kv.second.cap >= bytes) { pick = kv.first; break; }
-    if (pick < 0)
+    comm_local(X, [&] {
+      int pick = -1;
       for (auto& kv : C.shm)
-        if (kv.second.lease.expired()) { pick = kv.first; break; }
-    if (pick < 0 && C.shm.size() < 8) pick = int(C.shm.size());
-    if (pick >= 0) {
+        if (kv.second.lease.expired() && kv.second.cap() >= bytes) { pick = kv.first; break; }
+      if (pick < 0)
+        for (auto& kv : C.shm)
+          if (kv.second.lease.expired()) { pick = kv.first; break; }
+      if (pick < 0 && C.shm.size() < 8) pick = int(C.shm.size());
+      if (pick < 0) return;
       ShmMap& m = C.shm[pick];
-      bool ok = m.host && m.cap >= bytes;
-      if (!ok) {
-        const size_t cap = std::max<size_t>((std::max(bytes, m.cap * 3 / 2) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1),
+      if (!m.blk || m.cap() < bytes) {
+        const size_t cap = std::max<size_t>((std::max(bytes, m.cap() * 3 / 2) + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1),
                                             size_t(2) << 20);
         m.release();
         const uint64_t gen = ++C.shm_gen;
         const std::string name = "/lakeside-" + std::to_string(getpid()) + "-" + std::to_string(pick) + "-" +
                                  std::to_string(gen);
-        ok = map_block(m, name, cap, true);
+        m.blk = map_block(name, cap, true);
         m.gen = gen;
       }
-      if (ok) {
-        lease = std::make_shared<int>(0);
-        m.lease = lease;
-        hdr[0] = 1;
-        hdr[1] = uint64_t(getpid());
-        hdr[2] = uint64_t(pick);
-        hdr[3] = m.gen;
-        hdr[4] = m.cap;
-      }
-    }
+      if (!m.blk) return;
+      auto l = std::make_shared<ShmLease>();
+      l->blk = m.blk;
+      lease = l;
+      m.lease = lease;
+      hdr[0] = 1;
+      hdr[1] = uint64_t(getpid());
+      hdr[2] = uint64_t(pick);
+      hdr[3] = m.gen;
+      hdr[4] = m.blk->cap;
+    });
   }
-  const std::vector<std::string> all = C.allgather_bytes(E, X, std::string(reinterpret_cast<const char*>(hdr), sizeof(hdr)));
+  const std::vector<std::string> all =
+      comm_allgather_status(E, X, 0, std::string(), std::string(reinterpret_cast<const char*>(hdr), sizeof(hdr)));
   if (all.empty() || all[0].size() < sizeof(hdr)) return T;
   memcpy(hdr, all[0].data(), sizeof(hdr));
   if (!hdr[0]) return T;   // no block on rank 0: every rank takes the gather path
   const int b = int(hdr[2]);
   ShmMap& m = C.shm[b];
-  if (C.rank != 0 && (!m.host || m.gen != hdr[3])) {
+  if (C.rank != 0 && (!m.blk || m.gen != hdr[3])) {
     m.release();
     const std::string name = "/lakeside-" + std::to_string(hdr[1]) + "-" + std::to_string(b) + "-" + std::to_string(hdr[3]);
-    if (map_block(m, name, size_t(hdr[4]), false)) m.gen = hdr[3];
+    m.blk = map_block(name, size_t(hdr[4]), false);
+    m.gen = hdr[3];
   }
-  // a rank that could not map the block reports it with its rows (comm_emit_end fails the call on every rank)
+  // a rank that could not map the block reports it with its rows (the caller's agreement fails the call everywhere)
   T.ok = true;   // uniform over the ranks: rank 0 offered a block
-  T.host = static_cast<uint8_t*>(m.host);
-  T.dev = static_cast<uint8_t*>(m.dev);
-  T.cap = m.cap;
+  T.mapped = m.blk != nullptr;
+  T.host = m.blk ? static_cast<uint8_t*>(m.blk->host) : nullptr;
+  T.dev = m.blk ? static_cast<uint8_t*>(m.blk->dev) : nullptr;
+  T.cap = m.cap();
   T.lease = lease;
-  T.mapped = m.host != nullptr;
   return T;
+}
+
+void comm_emit_end(Engine& E) {
+  Comm& C = need_comm(E);
+  if (C.rank != 0) return;
+  // every rank has mapped this generation (the caller's agreement follows their writes): the names can go
+  for (auto& kv : C.shm)
+    if (kv.second.blk) kv.second.blk->unlink();
 }
 
 }  // namespace lk

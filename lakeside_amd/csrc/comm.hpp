@@ -5,8 +5,10 @@
 #include <string>
 #include <vector>
 
+#include "../../include/lakeside_gpu.h"
 #include "engine.hpp"
 #include "layout.hpp"
+#include "plan.hpp"
 
 namespace lk {
 
@@ -14,18 +16,45 @@ int comm_world(const Engine& E);
 int comm_rank(const Engine& E);
 // RCCL loopback test mode at world 1 (LK_COMM_LOOPBACK=1): collectives and point-to-point transfers run anyway.
 bool comm_loopback(const Engine& E);
-// Element-wise max of a small host byte array across ranks (glob column unions, null flags).
-void comm_allreduce_max_u8(Engine& E, CallCtx& X, uint8_t* host, size_t n);
 // Concatenation, in rank order, of every rank's byte blob (variable length): one all-gather of the sizes,
 // one of the blobs padded to the largest.
 std::vector<std::string> comm_allgather_bytes(Engine& E, CallCtx& X, const std::string& mine);
+// The agreement point: every rank contributes (status, payload) to one all-gather; when any rank's status is set
+// (its `code`, or else its pending X.pend_code), every rank throws the lowest failing rank's PlanError -- no rank is
+// left waiting in a later collective.  Returns every rank's payload, rank order.
+std::vector<std::string> comm_allgather_status(Engine& E, CallCtx& X, int code, const std::string& msg,
+                                               const std::string& payload);
 // Every rank reports its local status (0 = ok); if any rank failed, every rank throws the first failure
 // (PlanError with that rank's code), so no rank is left waiting in a later collective.
 void comm_agree(Engine& E, CallCtx& X, int code, const std::string& msg);
-// comm_agree and comm_allreduce_max_u8 in one all-gather (status, then the byte array).
+// Run a rank-local stage that precedes a collective: a PlanError (or any std::exception) is kept as the call's
+// pending status instead of unwinding this rank alone; the next agreement point fails every rank with it.
+template <class F>
+bool comm_local(CallCtx& X, F&& f) {
+  if (X.pend_code) return false;
+  try {
+    f();
+    return true;
+  } catch (const PlanError& e) {
+    X.pend_code = e.code;
+    X.pend_msg = e.what();
+  } catch (const std::exception& e) {
+    X.pend_code = LK_ERR_DEVICE;
+    X.pend_msg = e.what();
+  }
+  return false;
+}
+// After the last collective of a distributed call: a pending rank-local failure is thrown on this rank.
+void comm_throw_pending(CallCtx& X);
+// Tests only (env LK_FAULT=<stage>[@rank]): throws an injected LK_ERR_DEVICE at that stage on that rank (any rank
+// without @rank), so the multi-rank failure paths can be exercised on hardware that does not fail.
+void fault_point(const Engine& E, const char* stage);
+// comm_agree and an element-wise max of a small host byte array (glob column unions, NULL flags) in one all-gather.
 void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n);
 // Dense mode: reduce the partial aggregation table (P.rows/cnt/hi/lo/ext, nc cells) onto rank 0: counts by
 // sum, min/max by min/max on order-preserving bits (exact), compensated sums gathered and added in rank order.
+// Rank 0's receive buffer (world x the table) is placed by comm_reduce_prepare before the scan's agreement point.
+void comm_reduce_prepare(Engine& E, CallCtx& X, size_t nc);
 void comm_reduce_table(Engine& E, CallCtx& X, const QParams& P, int agg, size_t nc);
 // Hash mode: every rank compacts its occupied slots into records; rank 0 gathers them and inserts every rank's
 // records, in rank order, into a fresh table sized for their union (launch_merge_records).  On rank 0, P's table
@@ -58,6 +87,9 @@ struct EmitTarget {
   std::shared_ptr<void> lease;
 };
 EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes);
+// After the agreement that follows every rank's writes (so every rank holds its mapping): rank 0 unlinks the block
+// names, so a crash leaves no block behind in /dev/shm.
+void comm_emit_end(Engine& E);
 
 // Agreed dim space of an unrestricted group dimension over the ranks (dims.cpp; collective: every rank calls it in
 // the same order).  The cached union is reused while no rank's dictionary changed (one all-gather); `rebuilt` says a

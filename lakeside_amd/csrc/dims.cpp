@@ -67,40 +67,33 @@ std::shared_ptr<DimUnion> agree_dim_union(Engine& E, CallCtx& X, const std::stri
     err = e.code;
     msg = e.what();
   }
-  // blob: status (4) | n (8) | fingerprint (16) | hash of this rank's cached agreement key (8) | message
+  // payload: n (8) | fingerprint (16) | this rank's cached agreement key (the exact string, W x 24 bytes); the status
+  // travels in front (comm_allgather_status)
   std::shared_ptr<DimUnion>& slot = E.unions[col];
-  auto key_hash = [](const std::string& k) { return uint64_t(std::hash<std::string>()(k)) | 1u; };   // 0: none
-  std::string mine(36, '\0');
+  std::string mine(24, '\0');
   {
     const uint64_t n = dict_n, f0 = order ? order->fp[0] : 0, f1 = order ? order->fp[1] : 0;
-    const uint64_t ch = slot ? key_hash(slot->agree_key) : 0;
-    memcpy(&mine[0], &err, 4);
-    memcpy(&mine[4], &n, 8);
-    memcpy(&mine[12], &f0, 8);
-    memcpy(&mine[20], &f1, 8);
-    memcpy(&mine[28], &ch, 8);
-    if (err) mine += msg;
+    memcpy(&mine[0], &n, 8);
+    memcpy(&mine[8], &f0, 8);
+    memcpy(&mine[16], &f1, 8);
   }
-  const std::vector<std::string> all = comm_allgather_bytes(E, X, mine);
+  const std::string fp_mine = mine;
+  if (slot) mine += slot->agree_key;
+  const std::vector<std::string> all = comm_allgather_status(E, X, err, msg, mine);
   std::string agree_key;
   bool same = true;
   for (int r = 0; r < W; r++) {
-    int e;
-    memcpy(&e, all[size_t(r)].data(), 4);
-    if (e) throw PlanError(e, (r == me ? std::string() : "rank " + std::to_string(r) + ": ") + all[size_t(r)].substr(36));
-    agree_key += all[size_t(r)].substr(4, 24);
-    if (all[size_t(r)].substr(4, 24) != mine.substr(4, 24)) same = false;
+    if (all[size_t(r)].size() < 24) throw PlanError(LK_ERR_DEVICE, "internal: short dictionary fingerprint");
+    agree_key += all[size_t(r)].substr(0, 24);
+    if (all[size_t(r)].substr(0, 24) != fp_mine) same = false;
   }
-  // 2. the cached agreement is reused only when every rank holds it (each rank's cached-key hash travelled with its
-  // fingerprint, so every rank reaches the same decision without another collective)
+  // 2. the cached agreement is reused only when every rank holds exactly this one: decided from exchanged data alone
+  // (each rank's cached key travelled in full), so every rank reaches the same decision without another collective
+  // (a local-only comparison could split the ranks)
   bool all_hit = true;
-  const uint64_t want = key_hash(agree_key);
-  for (int r = 0; r < W; r++) {
-    uint64_t ch;
-    memcpy(&ch, all[size_t(r)].data() + 28, 8);
-    all_hit = all_hit && ch == want;
-  }
-  if (all_hit && slot && slot->agree_key == agree_key) {
+  for (int r = 0; r < W; r++) all_hit = all_hit && all[size_t(r)].compare(24, std::string::npos, agree_key) == 0;
+  (void)me;
+  if (all_hit) {
     agree_ms = ms_since_d(t0);
     return slot;
   }

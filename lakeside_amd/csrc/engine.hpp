@@ -119,6 +119,10 @@ struct CallCtx {
   std::map<std::string, Workspace> ws;
   void* pinned = nullptr;
   size_t pinned_cap = 0;
+  // Distributed calls: a rank-local failure met after a collective step, held until the next agreement point (an
+  // all-gather every rank takes) so that every rank fails together instead of leaving peers inside a collective.
+  int pend_code = 0;
+  std::string pend_msg;
   explicit CallCtx(int dev);
   ~CallCtx();
   CallCtx(const CallCtx&) = delete;

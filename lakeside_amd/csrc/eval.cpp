@@ -270,6 +270,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   std::unique_lock<std::mutex> comm_lock;
   if (dist) comm_lock = std::unique_lock<std::mutex>(E.comm_mu);
   CtxLease X(E);
+  X->pend_code = 0;
+  X->pend_msg.clear();
   static const bool plan_timing = getenv("LK_PLAN_TIMING") != nullptr;   // diagnostics: host planning stages
   auto stage = [&](const char* what) {
     if (plan_timing) fprintf(stderr, "[lk plan] %-10s %.3f ms\n", what, ms_since(t_start));
@@ -954,7 +956,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // ---- device: upload, zero table, scan ----
   stage("truth");
   const double plan_ms = ms_since(t_start);
-  HIP_TRY(hipSetDevice(E.device));
   hipStream_t st = X->stream;
   QParams P{};
   P.nsegs = uint32_t(qsegs.size());
@@ -1030,8 +1031,21 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       }
   const size_t o_maps = reserve(flat.size() * 4);
   const size_t stage_bytes = off;
-  uint8_t* hbuf = static_cast<uint8_t*>(X->pinned_buf(stage_bytes));
-  uint8_t* dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
+  // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)
+  uint8_t* hbuf = nullptr;
+  uint8_t* dbuf = nullptr;
+  try {
+    HIP_TRY(hipSetDevice(E.device));
+    hbuf = static_cast<uint8_t*>(X->pinned_buf(stage_bytes));
+    dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
+  } catch (const PlanError& e) {
+    if (!dist) throw;
+    if (!local_err) {
+      local_err = e.code;
+      local_msg = e.what();
+    }
+  }
+  if (hbuf && dbuf) {
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
   memcpy(hbuf + o_gsegs, gsegs.data(), gsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
@@ -1050,7 +1064,16 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   memset(hbuf + o_flags, 0, 16);
   if (!name_rank.empty()) memcpy(hbuf + o_rank, name_rank.data(), name_rank.size() * 4);
   if (!flat.empty()) memcpy(hbuf + o_maps, flat.data(), flat.size() * 4);
-  HIP_TRY(hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st));
+  const hipError_t up = hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st);
+  if (up != hipSuccess) {
+    (void)hipGetLastError();
+    if (!dist) throw PlanError(LK_ERR_DEVICE, std::string("HIP: query upload: ") + hipGetErrorString(up));
+    if (!local_err) {
+      local_err = LK_ERR_DEVICE;
+      local_msg = std::string("HIP: query upload: ") + hipGetErrorString(up);
+    }
+  }
+  }
   P.segs = reinterpret_cast<const QSeg*>(dbuf + o_segs);
   P.flags = reinterpret_cast<uint32_t*>(dbuf + o_flags);
   P.truth = truth.empty() ? nullptr : reinterpret_cast<const uint32_t*>(dbuf + o_truth);
@@ -1147,8 +1170,27 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, ncl * 8, st));
     if (hashed) HIP_TRY(hipMemsetAsync(P.hkeys, 0xff, ncl * 8, st));
   };
+  // Multi-GPU reduce shape (decided before the scan: its receive buffers are placed before the scan's agreement
+  // point, so no rank can fail alone between that agreement and the first point-to-point transfer).
+  const char* kr_env = getenv("LK_KEYRANGE_MIN_CELLS");
+  const uint64_t kr_min = kr_env ? uint64_t(atoll(kr_env)) : (uint64_t(1) << 20);
+  const bool keyrange = dist && (comm_world(E) > 1 || comm_loopback(E)) && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
+                        !ces && nslots == 1 && ncells >= std::max<uint64_t>(kr_min, 1);
+  const int W = dist ? comm_world(E) : 1;
+  std::vector<uint64_t> kb(size_t(W) + 1);   // key-range bounds: rank j owns cells [kb[j], kb[j+1])
+  for (int j = 0; j <= W; j++) kb[size_t(j)] = j == W ? ncells : (ncells * uint64_t(j) / uint64_t(W)) & ~63ull;
+  const size_t kr_len = size_t(kb[size_t(rank) + 1] - kb[size_t(rank)]);
   auto run_scan = [&]() -> uint32_t {
     nc = hash_mode ? size_t(cap) : size_t(std::max<uint64_t>(ncells, 1));
+    if (dist && !hash_mode) {   // the reduce stage's buffers
+      fault_point(E, "reduce");
+      if (keyrange) {
+        (void)X->workspace("kr_parts", size_t(W) * 5 * kr_len * 8 + 64);
+        (void)X->workspace("kr_counts", (size_t(finalize_blocks(kr_len)) + 2) * 4);
+      } else {
+        comm_reduce_prepare(E, *X, nc);
+      }
+    }
     zero_table(nc, hash_mode);
     HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));   // flags + the 64-bit plan-bytes counter behind them
     P.plan_bytes = (flags & LK_PLAN_BYTES) ? reinterpret_cast<unsigned long long*>(P.flags + 2) : nullptr;
@@ -1236,18 +1278,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (err) throw PlanError(err, msg);
       return fl;
     }
-    std::string mine(8, '\0');
-    memcpy(&mine[0], &err, 4);
-    memcpy(&mine[4], &fl, 4);
-    mine += msg;
     uint32_t all_fl = 0;
-    const std::vector<std::string> all = comm_allgather_bytes(E, *X, mine);
-    for (size_t r = 0; r < all.size(); r++) {
-      int e;
-      uint32_t f;
-      memcpy(&e, all[r].data(), 4);
-      memcpy(&f, all[r].data() + 4, 4);
-      if (e) throw PlanError(e, (int(r) == rank ? std::string() : "rank " + std::to_string(r) + ": ") + all[r].substr(8));
+    const std::vector<std::string> all =
+        comm_allgather_status(E, *X, err, msg, std::string(reinterpret_cast<const char*>(&fl), 4));
+    for (const std::string& b : all) {
+      uint32_t f = 0;
+      memcpy(&f, b.data(), std::min<size_t>(4, b.size()));
       all_fl |= f;
     }
     return all_fl;
@@ -1296,10 +1332,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   uint32_t nrows_out = 0;
   bool rows_done = false;   // key-range path: rank 0's result rows are already in place
   const char* emit_mode = "local";
-  const char* kr_env = getenv("LK_KEYRANGE_MIN_CELLS");
-  const uint64_t kr_min = kr_env ? uint64_t(atoll(kr_env)) : (uint64_t(1) << 20);
-  const bool keyrange = dist && (comm_world(E) > 1 || comm_loopback(E)) && !hash_mode && !per_glob_rows && !collapse && !rekey && !sketch &&
-                        !ces && nslots == 1 && ncells >= kr_min && ncells == nc;
   if (dist) {
     if (hash_mode) {
       unsigned long long cap0 = cap;
@@ -1312,10 +1344,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       // table to rank j (grouped send/recv: all xGMI links at once, 7/8 of a table per rank instead of every table
       // into rank 0); rank j folds the W slices in rank order (merge_tables: the same deterministic fold) and
       // finalizes its range; the ranges' rows, already in key order, are concatenated on rank 0 in rank order.
-      const int W = comm_world(E);
-      std::vector<uint64_t> kb(size_t(W) + 1);
-      for (int j = 0; j <= W; j++) kb[size_t(j)] = j == W ? uint64_t(nc) : (uint64_t(nc) * uint64_t(j) / uint64_t(W)) & ~63ull;
-      const size_t len = size_t(kb[size_t(rank) + 1] - kb[size_t(rank)]);
+      // (buffers placed before the scan's agreement: nothing between it and the exchange fails on one rank)
+      const size_t len = kr_len;
       uint8_t* tb = reinterpret_cast<uint8_t*>(P.rows);   // [rows | cnt | hi | lo | ext], nc cells each
       uint8_t* parts = static_cast<uint8_t*>(X->workspace("kr_parts", size_t(W) * 5 * len * 8 + 64));
       std::vector<Piece> sends, recvs;
@@ -1329,7 +1359,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       TableRef T{reinterpret_cast<unsigned long long*>(parts), reinterpret_cast<unsigned long long*>(parts + len * 8),
                  reinterpret_cast<double*>(parts + 2 * len * 8), reinterpret_cast<double*>(parts + 3 * len * 8),
                  reinterpret_cast<unsigned long long*>(parts + 4 * len * 8)};
-      if (len) HIP_TRY(launch_merge_tables(T, reinterpret_cast<const unsigned long long*>(parts), W, len, kagg, st));
       FParams Fk{};
       Fk.rows = T.rows;
       Fk.cnt = T.cnt;
@@ -1349,16 +1378,21 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       const uint32_t nfk = finalize_blocks(len);
       uint32_t* kc = static_cast<uint32_t*>(X->workspace("kr_counts", (size_t(nfk) + 2) * 4));
       uint32_t mine_n = 0;
-      if (len) {
+      // fold + count this rank's range; a failure travels with the row-count all-gather (every rank fails there)
+      comm_local(*X, [&] {
+        fault_point(E, "keyrange_merge");
+        if (!len) return;
+        HIP_TRY(launch_merge_tables(T, reinterpret_cast<const unsigned long long*>(parts), W, len, kagg, st));
         HIP_TRY(launch_finalize_count(Fk, kc, st));
         HIP_TRY(hipMemcpyAsync(&mine_n, kc + nfk, 4, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
-      }
+      });
       const uint64_t n64 = mine_n;
       std::vector<uint64_t> ncnt(static_cast<size_t>(W)), noff(static_cast<size_t>(W));
       uint64_t total_rows = 0;
       {
-        const std::vector<std::string> all = comm_allgather_bytes(E, *X, std::string(reinterpret_cast<const char*>(&n64), 8));
+        const std::vector<std::string> all =
+            comm_allgather_status(E, *X, 0, std::string(), std::string(reinterpret_cast<const char*>(&n64), 8));
         for (int j = 0; j < W; j++) {
           memcpy(&ncnt[size_t(j)], all[size_t(j)].data(), 8);
           noff[size_t(j)] = total_rows;
@@ -1382,7 +1416,15 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
             wst = LK_ERR_DEVICE;
         }
         if (hipStreamSynchronize(st) != hipSuccess) wst = LK_ERR_DEVICE;
+        if (!wst && getenv("LK_FAULT")) {   // tests only: an injected failure of the row write
+          try {
+            fault_point(E, "emit");
+          } catch (const PlanError&) {
+            wst = LK_ERR_DEVICE;
+          }
+        }
         comm_agree(E, *X, wst, "shared result block: mapping or write failed");   // every range written
+        comm_emit_end(E);   // every rank holds its mapping: the block names can go
         if (rank == 0) {
           nrows_out = uint32_t(total_rows);
           res->adopt_rows(ET.host, N, ET.lease);
@@ -1390,12 +1432,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         }
         emit_mode = "shared_host_block";
       } else {
-      uint8_t* ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 20 + 64));
-      if (mine_n)
-        HIP_TRY(launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ob), reinterpret_cast<double*>(ob + size_t(mine_n) * 8),
-                                      reinterpret_cast<uint32_t*>(ob + size_t(mine_n) * 16), nullptr, st));
-      HIP_TRY(hipStreamSynchronize(st));   // rows complete before they are sent
-      uint8_t* rb = rank == 0 ? static_cast<uint8_t*>(X->workspace("kr_rows_all", size_t(total_rows) * 20 + 64)) : nullptr;
+      uint8_t* ob = nullptr;
+      uint8_t* rb = nullptr;
+      comm_local(*X, [&] {   // this rank's rows (and rank 0's receive buffer), agreed on before they move
+        ob = static_cast<uint8_t*>(X->workspace("kr_rows_mine", size_t(mine_n) * 20 + 64));
+        if (mine_n)
+          HIP_TRY(launch_finalize_write(Fk, kc, reinterpret_cast<int64_t*>(ob), reinterpret_cast<double*>(ob + size_t(mine_n) * 8),
+                                        reinterpret_cast<uint32_t*>(ob + size_t(mine_n) * 16), nullptr, st));
+        HIP_TRY(hipStreamSynchronize(st));   // rows complete before they are sent
+        if (rank == 0) rb = static_cast<uint8_t*>(X->workspace("kr_rows_all", size_t(total_rows) * 20 + 64));
+      });
+      comm_agree(E, *X, 0, std::string());
       std::vector<Piece> s2, r2;   // [ts 8 B | value 8 B | group id 4 B] per row, column by column
       const size_t wcol[3] = {8, 8, 4};
       for (int a = 0; a < 3; a++) s2.push_back(Piece{0, ob + size_t(a) * mine_n * 8, size_t(mine_n) * wcol[a]});
@@ -1404,6 +1451,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
           for (int a = 0; a < 3; a++)
             r2.push_back(Piece{j, rb + size_t(a) * total_rows * 8 + noff[size_t(j)] * wcol[a], size_t(ncnt[size_t(j)]) * wcol[a]});
       comm_exchange(E, *X, s2, r2);
+      comm_throw_pending(*X);   // (host transport) a failed unpacking of the last round; no collective follows
       if (rank == 0) {
         nrows_out = uint32_t(total_rows);
         res->alloc_rows(nrows_out, false);
@@ -1420,6 +1468,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     } else {
       comm_reduce_table(E, *X, P, kagg, nc);
     }
+    comm_throw_pending(*X);   // past the last collective: a rank-local failure unwinds this rank alone
   }
   const bool emit = (!dist || rank == 0) && !rows_done;
 

@@ -364,3 +364,55 @@ def _worker_regrow(rank, world, port):
 def test_dist_hash_regrowth_uneven_shards():
     import torch.multiprocessing as mp
     mp.spawn(_worker_regrow, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _worker_fault(rank, world, port):
+    """a rank-local device failure injected at each stage between the first and the last
+    collective (LK_FAULT=<stage>@<rank>) fails the call with LK_ERR_DEVICE on every rank -- no rank is left inside a
+    collective -- and the next call on the same communicator succeeds."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd._lib import LK_ERR_DEVICE, LakesideError
+    from lakeside_amd.evaluator import Engine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        case = next(c for c in _cases() if c["name"] == "neq_notin_sum_by_svc")   # :sum :by -> key-range eligible
+        paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+        agg = case["request"]["baseExpr"]["chart"]["aggregation"]
+        # (stage, reduce shape env): the dense gather, the key-range all-to-all legs, the hash-record gather
+        stages = [("reduce@1", {}), ("reduce@0", {}), ("gather@1", {}),
+                  ("reduce@1", {"LK_KEYRANGE_MIN_CELLS": "1"}), ("keyrange_merge@1", {"LK_KEYRANGE_MIN_CELLS": "1"}),
+                  ("keyrange_merge@0", {"LK_KEYRANGE_MIN_CELLS": "1"}), ("emit@1", {"LK_KEYRANGE_MIN_CELLS": "1"}),
+                  ("records@1", {"LK_DENSE_MAX_CELLS": "1"}), ("gather@0", {"LK_DENSE_MAX_CELLS": "1"})]
+        for stage, env in stages:
+            for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            os.environ["LK_FAULT"] = stage
+            try:
+                eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
+                raise AssertionError(f"rank {rank}: no failure with LK_FAULT={stage} {env}")
+            except LakesideError as e:
+                assert e.code == LK_ERR_DEVICE, (stage, env, e.code, str(e))
+                assert "injected fault" in str(e), (stage, str(e))
+            os.environ.pop("LK_FAULT")
+            res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
+            if rank == 0:
+                assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"after fault {stage} {env}")
+            print(f"rank {rank}: {stage} {env} ok", flush=True)
+        dist.barrier()
+    finally:
+        for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS", "LK_FAULT"):
+            os.environ.pop(k, None)
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dist_injected_device_fault_fails_every_rank():
+    import torch.multiprocessing as mp
+    mp.spawn(_worker_fault, args=(2, _free_port()), nprocs=2, join=True)
