@@ -79,6 +79,10 @@ def main():
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N > 1 exchange: RCCL over xGMI (default), or the host transport over gloo (rehearsal of the "
                          "multi-rank path with several ranks on one GPU; RCCL refuses two ranks on one device)")
+    ap.add_argument("--dist-loopback", action="store_true",
+                    help="N=1 only: evaluate through lk_eval_pushdown_dist on a world-1 RCCL communicator with "
+                         "LK_COMM_LOOPBACK=1, so every collective of the N > 1 path (all-gathers, grouped "
+                         "ncclSend/ncclRecv of the table reduce or the key-range all-to-all) runs on this GPU")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -94,6 +98,11 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo")
+    loopback = args.dist_loopback and world == 1
+    if args.dist_loopback and world > 1:
+        log("note: --dist-loopback applies at N=1 only; ignored")
+    if loopback:
+        os.environ["LK_COMM_LOOPBACK"] = "1"   # read by lk_comm_init
     device = local_rank if args.comm == "rccl" else 0
     torch.cuda.set_device(device)
     eng = Engine(device)
@@ -103,6 +112,9 @@ def main():
         obj = [Engine.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         eng.comm_init(obj[0], world, rank)
+    elif loopback:
+        eng.comm_init(Engine.unique_id(), 1, 0)
+    use_dist = world > 1 or loopback
 
     # ---- segments of this rank (weak scaling: rank r owns global segments [r*S, (r+1)*S)) ----
     q = QUERIES[args.query]
@@ -148,14 +160,14 @@ def main():
         req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag")))
 
     def step(extra=0):
-        if world > 1:
+        if use_dist:
             return eng.eval_pushdown_dist(req, keys, shard, 10)
         return eng.eval_pushdown(req, keys, 10, LK_MERGED | extra)
 
     # Plan bytes (the roofline numerator) are a property of the query and the data: counted by the kernel in one
     # untimed call (LK_PLAN_BYTES costs ~5% of scan time), then the timed steps run without the counter.
     if world == 1:
-        pbytes = float(step(LK_PLAN_BYTES).stats.get("plan_bytes", 0))
+        pbytes = float(eng.eval_pushdown(req, keys, 10, LK_MERGED | LK_PLAN_BYTES).stats.get("plan_bytes", 0))
     else:   # per GPU: this rank's shard alone (the same scan work it does inside the distributed call)
         local = json.dumps(synth.pushdown(q["filter"], [segs[i] for i in mine], q["agg"], q["group_bys"],
                                           tag=q.get("tag")))
@@ -163,11 +175,22 @@ def main():
                        .stats.get("plan_bytes", 0))
     for _ in range(args.warmup):
         res = step()
+    # Cold evaluation: the request as if never seen -- parse, leaf-outcome, value-key-order and group-dim caches
+    # dropped (segments stay resident) -- one call, wall time; then one warm call so the timed steps start warm.
+    if world > 1:
+        dist.barrier()
+    eng.drop_caches()
+    tc = time.perf_counter()
+    cold = step()
+    cold_ms = (time.perf_counter() - tc) * 1e3
+    cold_total_ms = cold.stats.get("total_ms")
+    del cold
+    res = step()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
-    launch_ms, sync_ms, alloc_ms, copy_ms, dims_ms = [], [], [], [], []
+    launch_ms, sync_ms, alloc_ms, copy_ms, dims_ms, reduce_ms, agreed_ms = [], [], [], [], [], [], []
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
@@ -180,6 +203,8 @@ def main():
         alloc_ms.append(res.stats.get("alloc_ms", 0.0))
         copy_ms.append(res.stats.get("copy_ms", 0.0))
         dims_ms.append(res.stats.get("dims_ms", 0.0))
+        reduce_ms.append(res.stats.get("reduce_ms", 0.0))
+        agreed_ms.append(res.stats.get("scan_agreed_ms", 0.0))
         alg_bytes = res.stats.get("algorithmic_bytes", 0)
         out_rows = len(res)
     torch.cuda.synchronize()
@@ -207,7 +232,8 @@ def main():
         f"plan {sum(plan_ms) / len(plan_ms):.2f} ms, device {sum(device_ms) / len(device_ms):.2f} ms, "
         f"total {sum(total_ms) / len(total_ms):.2f} ms" +
         (f"; group-dim agreement {sum(dims_ms) / len(dims_ms):.2f} ms, reduce {res.stats.get('reduce')}, "
-         f"emit {res.stats.get('emit')}" if world > 1 else ""))
+         f"emit {res.stats.get('emit')}, reduce stage {sum(reduce_ms) / len(reduce_ms):.3f} ms, "
+         f"collectives {res.stats.get('collectives')}" if use_dist else "") + f"; cold eval {cold_ms:.2f} ms")
 
     # measured device-to-device copy rate on this GPU (a stream-copy peak beside the spec peak)
     copy_gbs = None
@@ -265,11 +291,19 @@ def main():
                      "ms_per_segment": load_s / S * 1e3},
             "rows_scanned": rows_total, "output_rows": out_rows,
             "scan_kernel_ms": scan_avg, "eval_ms": ms_per_step,
+            "cold_eval_ms": cold_ms,
+            "cold_eval": {"what": "first evaluation of the request after lk_engine_drop_caches (parsed request, "
+                                  "leaf outcomes, value-key orders, group-dim unions dropped; segments resident); "
+                                  "wall time of the call", "ms": cold_ms, "engine_total_ms": cold_total_ms},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "definition": "achieved = plan bytes per launch (counted by the scan kernel: streams "
                                        "decoded in full + distinct 128-B lines of every per-row gather + tile "
-                                       "metadata) / scan-kernel time (HIP events on the call's stream)",
+                                       "metadata) / scan-kernel time (HIP events on the call's stream). `value` "
+                                       "counts every row of the workload as scanned, including rows of tiles whose "
+                                       "load-time zone map (timestamp min/max per tile) pins them to a single "
+                                       "bucket: their timestamps are never read, and value lines with no passing "
+                                       "row are skipped, so plan bytes < SURVEY's algorithmic bytes",
                          "plan_bytes_per_launch": pbytes,
                          "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_gbs": alg_gbs,
                          "traffic_source": traffic_src,
@@ -278,9 +312,18 @@ def main():
             "validated": validated,
             "cpu_baseline": cpu,
         }
-        if world > 1:   # the distributed call's own stages (rank 0): group-dim agreement, table reduce, row emission
+        if use_dist:   # the distributed call's own stages (rank 0): group-dim agreement, table reduce, row emission
             line["dist"] = {"dims_ms": sum(dims_ms) / len(dims_ms), "reduce": res.stats.get("reduce"),
-                            "emit": res.stats.get("emit"), "comm": args.comm}
+                            "emit": res.stats.get("emit"), "comm": args.comm,
+                            "loopback": loopback,
+                            "scan_agreed_ms": sum(agreed_ms) / len(agreed_ms),
+                            "reduce_ms": sum(reduce_ms) / len(reduce_ms),
+                            "collectives_per_query": res.stats.get("collectives"),
+                            "allgathers": res.stats.get("allgathers"), "allgather_bytes": res.stats.get("allgather_bytes"),
+                            "p2p_groups": res.stats.get("p2p_groups"), "p2p_bytes": res.stats.get("p2p_bytes")}
+            if loopback:
+                line["config"]["parallelism"] = ("segment-sharded x1 through lk_eval_pushdown_dist on a world-1 RCCL "
+                                                 "communicator in loopback (every collective of the N>1 path runs)")
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -72,6 +72,10 @@ size_t lk_segment_bytes(const lk_engine* e);
 /* Engine counters as JSON: {"segments", "segment_bytes", "evictions", "dict_compactions",
  * "dictionaries": {column: {"size", "live", "generation"}}}; valid until the calling thread's next call. */
 const char* lk_engine_stats(lk_engine* e);
+/* Drops the engine's per-query caches -- parsed requests, per-(column, leaf) dictionary outcomes, value-key orders,
+ * bulk-export pointer tables and distributed group-dim unions -- but keeps the cached segments and dictionaries: the
+ * next evaluation of any request runs cold (the bench's cold_eval_ms).  Waits for in-flight evaluations. */
+int lk_engine_drop_caches(lk_engine* e);
 
 /* Mirrors one Commons.evaluatePushDownRequest call (Commons.scala:343-397).
  * push_down_json: PushDownRequest.toJson wire format (core/.../model/SegmentRequest.scala:30-60).

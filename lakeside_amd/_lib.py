@@ -33,6 +33,7 @@ SIGNATURES = [
     ("lk_segment_count", _c.c_size_t, [_P]),
     ("lk_segment_bytes", _c.c_size_t, [_P]),
     ("lk_engine_stats", _c.c_char_p, [_P]),
+    ("lk_engine_drop_caches", _c.c_int, [_P]),
     ("lk_eval_pushdown", _c.c_int, [_P, _c.c_char_p, _c.POINTER(_c.c_char_p), _c.c_size_t, _c.c_int, _c.c_uint,
                                     _c.POINTER(_P)]),
     ("lk_result_num_rows", _c.c_size_t, [_P]),

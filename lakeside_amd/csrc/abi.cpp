@@ -150,6 +150,32 @@ const char* lk_engine_stats(lk_engine* e) {
   return t_stats.c_str();
 }
 
+int lk_engine_drop_caches(lk_engine* e) {
+  if (!e) return LK_ERR_ARG;
+  lk::Engine& E = *e->e;
+  std::unique_lock<std::shared_mutex> gen(E.gen_mu);   // no evaluation in flight
+  std::lock_guard<std::mutex> cm(E.comm_mu);
+  {
+    std::lock_guard<std::mutex> g(E.parsed_mu);
+    E.parsed.clear();
+  }
+  {
+    std::lock_guard<std::mutex> g(E.leaf_mu);
+    E.leaf_cache.clear();
+  }
+  {
+    std::lock_guard<std::mutex> g(E.order_mu);
+    E.orders.clear();
+  }
+  {
+    std::lock_guard<std::mutex> g(E.ptrs_mu);
+    E.ptrs.clear();
+  }
+  E.unions.clear();
+  t_err.clear();
+  return LK_OK;
+}
+
 size_t lk_segment_count(const lk_engine* e) {
   if (!e) return 0;
   std::lock_guard<std::mutex> g(e->e->cache_mu);

@@ -96,6 +96,7 @@ struct Comm {
   // ncclSend/ncclRecv to self -- and the merge reads what came back through RCCL, so the single-GPU box executes
   // (and checks) every RCCL data-path call the 8-GPU run makes.
   bool loopback = false;
+  CommCounters cnt;             // collectives issued by this rank (stats)
   bool active() const { return world > 1 || loopback; }
   virtual ~Comm() = default;   // mappings go with their last reference (pool entry or a live result)
   // host blobs of every rank, rank order
@@ -125,6 +126,7 @@ struct RcclComm final : Comm {
     sz[size_t(rank)] = mine.size();
     HIP_TRY2(hipMemcpyAsync(dsz + rank, &sz[size_t(rank)], 8, hipMemcpyHostToDevice, st));
     NCCL_TRY(ncclAllGather(dsz + rank, dsz, 1, ncclUint64, comm, st));
+    cnt.allgathers++;
     HIP_TRY2(hipMemcpyAsync(sz.data(), dsz, size_t(world) * 8, hipMemcpyDeviceToHost, st));
     HIP_TRY2(hipStreamSynchronize(st));
     uint64_t mx = 1;
@@ -133,6 +135,8 @@ struct RcclComm final : Comm {
     if (!mine.empty())
       HIP_TRY2(hipMemcpyAsync(d + size_t(rank) * mx, mine.data(), mine.size(), hipMemcpyHostToDevice, st));
     NCCL_TRY(ncclAllGather(d + size_t(rank) * mx, d, mx, ncclUint8, comm, st));
+    cnt.allgathers++;
+    cnt.allgather_bytes += uint64_t(world) * mx;
     std::string all(size_t(world) * mx, '\0');
     HIP_TRY2(hipMemcpyAsync(&all[0], d, all.size(), hipMemcpyDeviceToHost, st));
     HIP_TRY2(hipStreamSynchronize(st));
@@ -146,6 +150,9 @@ struct RcclComm final : Comm {
     if (!active()) return;
     // grouped point-to-point: every peer streams into rank 0 over its own xGMI link at once (loopback: rank 0's own
     // block too, into slot 0)
+    cnt.p2p_groups++;
+    for (int r = 0; r < world; r++)
+      if (r != 0 || loopback) cnt.p2p_bytes += bytes[size_t(r)];
     NCCL_TRY(ncclGroupStart());
     if (rank == 0) {
       for (int r = loopback ? 0 : 1; r < world; r++)
@@ -158,6 +165,9 @@ struct RcclComm final : Comm {
 
   void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) override {
     // loopback: own pieces go through RCCL as well (send / recv to self, matched in list order)
+    cnt.p2p_groups++;
+    for (const Piece& p : sends)
+      if (p.peer != rank || loopback) cnt.p2p_bytes += p.bytes;
     NCCL_TRY(ncclGroupStart());
     for (const Piece& p : sends)
       if ((p.peer != rank || loopback) && p.bytes) NCCL_TRY(ncclSend(p.ptr, p.bytes, ncclUint8, p.peer, comm, X.stream));
@@ -172,6 +182,8 @@ struct HostComm final : Comm {
   void* user = nullptr;
 
   void allgather(const void* send, size_t bytes, void* recv) {
+    cnt.allgathers++;
+    cnt.allgather_bytes += uint64_t(world) * bytes;
     if (fn(user, send, bytes, recv) != 0) throw PlanError(LK_ERR_DEVICE, "host transport: all-gather callback failed");
   }
 
@@ -285,6 +297,7 @@ struct HostComm final : Comm {
 }  // namespace
 
 int comm_world(const Engine& E) { return E.comm ? E.comm->world : 1; }
+CommCounters comm_counters(const Engine& E) { return E.comm ? E.comm->cnt : CommCounters{}; }
 bool comm_loopback(const Engine& E) { return E.comm && E.comm->loopback; }
 int comm_rank(const Engine& E) { return E.comm ? E.comm->rank : 0; }
 

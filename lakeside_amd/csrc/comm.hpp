@@ -13,6 +13,13 @@
 namespace lk {
 
 int comm_world(const Engine& E);
+// Collectives this rank has issued on the communicator (cumulative; a call's stats report the difference).  RCCL: one
+// ncclAllGather per all-gather, one grouped ncclSend/ncclRecv set per point-to-point group; host transport: one
+// callback all-gather each.
+struct CommCounters {
+  uint64_t allgathers = 0, allgather_bytes = 0, p2p_groups = 0, p2p_bytes = 0;
+};
+CommCounters comm_counters(const Engine& E);
 int comm_rank(const Engine& E);
 // RCCL loopback test mode at world 1 (LK_COMM_LOOPBACK=1): collectives and point-to-point transfers run anyway.
 bool comm_loopback(const Engine& E);

@@ -272,6 +272,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   CtxLease X(E);
   X->pend_code = 0;
   X->pend_msg.clear();
+  const CommCounters cc0 = dist ? comm_counters(E) : CommCounters{};
   static const bool plan_timing = getenv("LK_PLAN_TIMING") != nullptr;   // diagnostics: host planning stages
   auto stage = [&](const char* what) {
     if (plan_timing) fprintf(stderr, "[lk plan] %-10s %.3f ms\n", what, ms_since(t_start));
@@ -1317,6 +1318,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
     break;
   }
+  const double scan_agreed_ms = ms_since(t_start);   // every rank's scan done and its status agreed
   if (hflags & FLAG_METRICS_UNALIGNED) {
     if (step == 1) throw PlanError(LK_ERR_DEVICE, "internal: metrics timestamp off a 1 ms grid");
     throw MetricsUnaligned{};
@@ -1332,6 +1334,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   uint32_t nrows_out = 0;
   bool rows_done = false;   // key-range path: rank 0's result rows are already in place
   const char* emit_mode = "local";
+  const double t_reduce0 = ms_since(t_start);
   if (dist) {
     if (hash_mode) {
       unsigned long long cap0 = cap;
@@ -1470,6 +1473,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
     comm_throw_pending(*X);   // past the last collective: a rank-local failure unwinds this rank alone
   }
+  const double reduce_ms = ms_since(t_start) - t_reduce0;   // dist: table reduce (+ key-range emission)
   const bool emit = (!dist || rank == 0) && !rows_done;
 
   FParams F{};
@@ -1879,6 +1883,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
            !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")), dims_ms,
            dims_rebuilt, emit_mode);
   res->stats = buf;
+  if (dist) {   // the distributed call's stages and collectives (this rank)
+    const CommCounters cc = comm_counters(E);
+    char b2[384];
+    snprintf(b2, sizeof(b2),
+             ",\"reduce_ms\":%.6f,\"scan_agreed_ms\":%.6f,\"collectives\":%llu,\"allgathers\":%llu,"
+             "\"allgather_bytes\":%llu,\"p2p_groups\":%llu,\"p2p_bytes\":%llu",
+             reduce_ms, scan_agreed_ms, (unsigned long long)(cc.allgathers - cc0.allgathers + cc.p2p_groups - cc0.p2p_groups),
+             (unsigned long long)(cc.allgathers - cc0.allgathers), (unsigned long long)(cc.allgather_bytes - cc0.allgather_bytes),
+             (unsigned long long)(cc.p2p_groups - cc0.p2p_groups), (unsigned long long)(cc.p2p_bytes - cc0.p2p_bytes));
+    res->stats += b2;
+  }
   if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
   if (redo) res->stats += ",\"redo\":" + std::to_string(redo);   // 1: metrics at 1 ms, 2: MIN cells kept per glob
   res->stats += "}";

@@ -180,6 +180,11 @@ class Engine:
         """Engine counters: cached segments, evictions, dictionary sizes / live ids / compactions."""
         return json.loads(_lib.lib().lk_engine_stats(self._h).decode())
 
+    def drop_caches(self):
+        """Forget parsed requests, leaf outcomes, value-key orders and group-dim unions (segments stay cached): the
+        next evaluation runs cold."""
+        check(_lib.lib().lk_engine_drop_caches(self._h))
+
     # ---- evaluation ----
     def eval_pushdown(self, request_json: str, paths: Sequence[str], glob_size: int = 10,
                       flags: int = LK_PER_GLOB_ROWS) -> Result:

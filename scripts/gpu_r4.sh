@@ -18,6 +18,11 @@ for e in ${ENVS:--}; do
     echo "== $q [$e]"; grep -h "scan kernel\|validation" gpurun_out/r4/${q}_${tag}.log | sed 's/; in the call.*//'
   done
 done
+for q in ${LOOPBACK_QUERIES:-}; do   # lk_eval_pushdown_dist on a world-1 RCCL loopback communicator
+  cs=0; [ -n "$VALIDATE" ] && [ "$q" != c5 ] && cs=-1
+  timeout -k 10 ${PER:-400} python3 bench.py --query $q --dist-loopback --steps ${STEPS:-10} --warmup 3 --cpu-sample $cs > gpurun_out/r4/${q}_loopback.json 2> gpurun_out/r4/${q}_loopback.log || exit $?
+  echo "== $q [loopback]"; grep -h "scan kernel\|validation" gpurun_out/r4/${q}_loopback.log | sed 's/; in the call.*//'
+done
 for q in ${PROF_QUERIES:-}; do
   env $PROF_ENV timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/r4/kt_$q -o kt --output-format csv -- python3 bench.py --query $q --steps 5 --warmup 2 --cpu-sample 0 > gpurun_out/r4/kt_$q.json 2> gpurun_out/r4/kt_$q.log || exit $?
   head -6 gpurun_out/r4/kt_$q/kt_kernel_stats.csv
