@@ -39,7 +39,8 @@ enum {
   LK_ERR_UNSUPPORTED = -2,  /* query or file shape outside the implemented path */
   LK_ERR_IO = -3,           /* file read / Parquet parse */
   LK_ERR_DEVICE = -4,       /* HIP / RCCL failure, or no GPU */
-  LK_ERR_MEMORY = -5
+  LK_ERR_MEMORY = -5,
+  LK_ERR_EVICTED = -6       /* a key registered with lk_segment_put was evicted from the HBM cache: re-put it */
 };
 
 /* Flags of lk_eval_pushdown. */

@@ -15,6 +15,7 @@ LK_ERR_ARG = -1
 LK_ERR_UNSUPPORTED = -2
 LK_ERR_IO = -3
 LK_ERR_DEVICE = -4
+LK_ERR_EVICTED = -6
 LK_ERR_MEMORY = -5
 LK_PER_GLOB_ROWS = 1
 LK_MERGED = 2

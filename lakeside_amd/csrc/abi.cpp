@@ -107,6 +107,7 @@ int lk_segment_evict(lk_engine* e, const char* key) {
     std::shared_ptr<lk::Segment> victim;   // released after cache_mu (~Segment returns its dictionary references)
     {
       std::lock_guard<std::mutex> g(e->e->cache_mu);
+      e->e->evicted_puts.erase(key);   // the caller dropped the key itself
       auto it = e->e->cache.find(key);
       if (it == e->e->cache.end()) return int(LK_ERR_ARG);
       e->e->cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
@@ -124,7 +125,8 @@ const char* lk_engine_stats(lk_engine* e) {
   {
     std::lock_guard<std::mutex> g(E.cache_mu);
     o += "\"segments\":" + std::to_string(E.cache.size()) + ",\"segment_bytes\":" + std::to_string(E.cache_bytes) +
-         ",\"evictions\":" + std::to_string(E.evictions);
+         ",\"evictions\":" + std::to_string(E.evictions) + ",\"load_ms\":" + std::to_string(E.load_ms_total) +
+         ",\"load_host_ms\":" + std::to_string(E.load_host_ms_total);
   }
   o += ",\"dict_compactions\":" + std::to_string(E.compactions) + ",\"dictionaries\":{";
   {

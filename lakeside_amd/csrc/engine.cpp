@@ -15,6 +15,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <new>
+#include <exception>
+#include <string_view>
+#include <thread>
 #include <deque>
 #include <fstream>
 #include <map>
@@ -414,19 +417,33 @@ struct HostPage {
   const uint8_t* host_vals = nullptr;
 };
 
-struct Builder {
-  Engine& E;
-  const uint8_t* F;
-  size_t size;
-  Segment& S;
-  std::vector<uint8_t> stage;
-  std::vector<std::vector<HostPage>> pages;   // per column
-  std::deque<std::vector<uint8_t>> plain;     // decompressed pages (host_vals point into them until tiling)
+// A byte range of one page stream: copied from `src` (the file, or a decompressed / re-encoded page buffer) to `off`
+// in its chunk's stream area.
+struct StreamRef {
+  const uint8_t* src;
+  size_t len;
+  size_t off;
+};
 
+// One column chunk (column, row group) walked on the host: page descriptors, run tables and the byte ranges of its
+// page streams.  Chunks are independent, so the walk runs on several threads (Engine::load_threads); string
+// dictionary values are interned into the engine dictionaries afterwards, per column in row-group order, so the
+// engine-global ids do not depend on thread timing.
+struct ChunkOut {
+  std::vector<StreamRef> streams;
+  size_t bytes = 0;                       // the chunk's stream area (every stream 128-B aligned: one HBM line start)
+  std::vector<HostPage> pages;            // d.vals / d.defs: offsets in the chunk's area; run_lo / drun_lo: indices into
+                                          // `runs`; d.remap: index into `dict`
+  std::vector<RunDesc> runs;
+  std::vector<std::string> dict;          // strings: the dictionary page's values, then every PLAIN page's own values
+  std::deque<std::vector<uint8_t>> plain; // decompressed / re-encoded pages (streams and zone maps read them)
+  uint64_t compressed = 0;
+  int code = 0;                           // LK_ERR_IO: the file is corrupt; LK_ERR_UNSUPPORTED: this column's shape
+  std::string msg;
   size_t put(const uint8_t* p, size_t n) {
-    size_t off = align_up(stage.size(), 128);   // every page stream starts on an HBM line (plan-bytes counting)
-    stage.resize(off + n);
-    if (n) memcpy(stage.data() + off, p, n);
+    const size_t off = (bytes + 127) / 128 * 128;
+    if (n) streams.push_back(StreamRef{p, n, off});
+    bytes = off + n;
     return off;
   }
 };
@@ -466,18 +483,18 @@ PageStreams split_page(const pq::PageHeader& h, const uint8_t* data, size_t n, b
   return s;
 }
 
-void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m) {
-  HostCol& col = B.S.cols[ci];
+// Walks one column chunk's pages (thread-safe: reads only `col`'s schema fields and the file bytes).
+void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32_t rg, int64_t rg_rows,
+                       const pq::ColumnMeta& m, ChunkOut& C) {
   if (!pq::codec_supported(m.codec))
     throw PlanError(LK_ERR_UNSUPPORTED, "parquet: compression codec " + std::to_string(m.codec) + " in column " +
                                             col.name + " is not supported");
   int64_t start = m.data_page_offset;
   if (m.dictionary_page_offset > 0 && m.dictionary_page_offset < start) start = m.dictionary_page_offset;
-  if (start < 4 || size_t(start) >= B.size) throw PlanError(LK_ERR_IO, "parquet: bad page offset");
-  col.compressed_bytes += uint64_t(m.total_compressed);
+  if (start < 4 || size_t(start) >= size) throw PlanError(LK_ERR_IO, "parquet: bad page offset");
+  C.compressed += uint64_t(m.total_compressed);
   size_t pos = size_t(start);
   int64_t seen = 0;
-  uint32_t remap_off = uint32_t(col.remap.size());
   uint32_t dict_n = 0;
   bool have_dict = false;
   // numeric columns: fixed width of a PLAIN value (BOOLEAN: bit-packed) and the chunk's dictionary, if any (its
@@ -486,11 +503,11 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
   std::vector<uint8_t> ndict;
   uint32_t first_row = 0;
   while (seen < m.num_values) {
-    if (pos >= B.size) throw PlanError(LK_ERR_IO, "parquet: page walk ran past the file");
-    pq::PageHeader h = pq::parse_page_header(B.F + pos, B.size - pos);
-    const uint8_t* data = B.F + pos + h.header_len;
+    if (pos >= size) throw PlanError(LK_ERR_IO, "parquet: page walk ran past the file");
+    pq::PageHeader h = pq::parse_page_header(F + pos, size - pos);
+    const uint8_t* data = F + pos + h.header_len;
     size_t n = size_t(h.compressed);
-    if (pos + h.header_len + n > B.size) throw PlanError(LK_ERR_IO, "parquet: page overruns the file");
+    if (pos + h.header_len + n > size) throw PlanError(LK_ERR_IO, "parquet: page overruns the file");
     pos += h.header_len + n;
     if (m.codec != pq::CODEC_UNCOMPRESSED &&
         (h.type == pq::DICTIONARY_PAGE || h.type == pq::DATA_PAGE || h.type == pq::DATA_PAGE_V2)) {
@@ -500,8 +517,8 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       if (h.uncompressed < 0 || lv > n || lv > size_t(h.uncompressed))
         throw PlanError(LK_ERR_IO, "parquet: bad page sizes");
       if (h.type != pq::DATA_PAGE_V2 || h.v2_compressed) {
-        B.plain.emplace_back(size_t(h.uncompressed));
-        std::vector<uint8_t>& out = B.plain.back();
+        C.plain.emplace_back(size_t(h.uncompressed));
+        std::vector<uint8_t>& out = C.plain.back();
         if (lv) memcpy(out.data(), data, lv);
         pq::decompress(m.codec, data + lv, n - lv, out.data() + lv, out.size() - lv);
         data = out.data();
@@ -518,17 +535,17 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       continue;
     }
     if (h.type == pq::DICTIONARY_PAGE) {
-      GlobalDict& gd = B.E.dict(col.name);
-      std::lock_guard<std::mutex> g(gd.mu);
+      if (h.dict_num_values < 0) throw PlanError(LK_ERR_IO, "parquet: bad dictionary page in " + col.name);
+      if (have_dict) throw PlanError(LK_ERR_IO, "parquet: second dictionary page in " + col.name);
       size_t p = 0;
-      col.remap.reserve(col.remap.size() + size_t(h.dict_num_values));
+      C.dict.reserve(size_t(h.dict_num_values));
       for (int32_t i = 0; i < h.dict_num_values; i++) {
         if (p + 4 > n) throw PlanError(LK_ERR_IO, "parquet: truncated dictionary page");
         uint32_t L;
         memcpy(&L, data + p, 4);
         p += 4;
         if (p + L > n) throw PlanError(LK_ERR_IO, "parquet: truncated dictionary entry");
-        col.remap.push_back(gd.intern(std::string(reinterpret_cast<const char*>(data + p), L)));
+        C.dict.emplace_back(reinterpret_cast<const char*>(data + p), L);
         p += L;
       }
       dict_n = uint32_t(h.dict_num_values);
@@ -547,12 +564,26 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
     uint32_t nvals = st.nrows;
     if (col.nullable) {
       auto druns = pq::hybrid_runs(st.defs, st.defs_len, 1, st.nrows);
-      std::vector<uint32_t> defv(st.nrows);
-      pq::hybrid_decode(st.defs, st.defs_len, 1, st.nrows, defv.data());
+      // non-null count from the runs: RLE runs by their value, bit-packed runs by popcount of their bytes
       nvals = 0;
-      for (uint32_t v : defv) nvals += v ? 1 : 0;
+      bool any_null = false;
+      for (auto& r : druns) {
+        if (!r.literal) {
+          if (r.value) nvals += r.count;
+          else any_null = any_null || r.count;
+          continue;
+        }
+        const uint8_t* b = st.defs + r.off;
+        uint32_t k = 0, c = 0;
+        for (; k + 8 <= r.count; k += 8) c += uint32_t(__builtin_popcount(b[k >> 3]));
+        for (; k < r.count; k++) c += (b[k >> 3] >> (k & 7)) & 1u;
+        nvals += c;
+      }
+      (void)any_null;
       d.has_nulls = nvals < st.nrows;
       if (d.has_nulls) {
+        std::vector<uint32_t> defv(st.nrows);
+        pq::hybrid_decode(st.defs, st.defs_len, 1, st.nrows, defv.data());
         hp.vprefix.resize(st.nrows + 1);
         uint32_t acc = 0;
         for (uint32_t i = 0; i < st.nrows; i++) {
@@ -560,46 +591,41 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
           acc += defv[i] ? 1 : 0;
         }
         hp.vprefix[st.nrows] = acc;
-        hp.drun_lo = uint32_t(col.runs.size());
-        for (auto& r : druns)
-          col.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
+        hp.drun_lo = uint32_t(C.runs.size());
+        for (auto& r : druns) C.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
         hp.drun_n = uint32_t(druns.size());
-        d.defs = B.put(st.defs, st.defs_len);
+        d.defs = C.put(st.defs, st.defs_len);
         d.defs_len = uint32_t(st.defs_len);
       }
     }
     d.nvals = nvals;
     if (col.is_string) {
-      uint32_t page_remap = remap_off, page_dict_n = dict_n;
+      uint32_t page_remap = 0, page_dict_n = dict_n;
       if (st.encoding == pq::PLAIN) {
         // PLAIN BYTE_ARRAY page (a writer's dictionary fallback, or no dictionary at all): the page gets its own
-        // dictionary — its distinct values in first-seen order, remapped to engine-global ids — and its values
-        // are re-encoded as one bit-packed literal run of indices, so the kernels see a dictionary page.
-        std::unordered_map<std::string, uint32_t> local;
+        // dictionary -- its distinct values in first-seen order, interned with the chunk -- and its values are
+        // re-encoded as one bit-packed literal run of indices, so the kernels see a dictionary page.
+        std::unordered_map<std::string_view, uint32_t> local;
         std::vector<uint32_t> idx(nvals);
-        page_remap = uint32_t(col.remap.size());
-        {
-          GlobalDict& gd = B.E.dict(col.name);
-          std::lock_guard<std::mutex> g(gd.mu);
-          size_t p = 0;
-          for (uint32_t i = 0; i < nvals; i++) {
-            if (p + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY page in " + col.name);
-            uint32_t L;
-            memcpy(&L, st.vals + p, 4);
-            p += 4;
-            if (p + L > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY value in " + col.name);
-            auto ins = local.emplace(std::string(reinterpret_cast<const char*>(st.vals + p), L), uint32_t(local.size()));
-            if (ins.second) col.remap.push_back(gd.intern(ins.first->first));
-            idx[i] = ins.first->second;
-            p += L;
-          }
+        page_remap = uint32_t(C.dict.size());
+        size_t p = 0;
+        for (uint32_t i = 0; i < nvals; i++) {
+          if (p + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY page in " + col.name);
+          uint32_t L;
+          memcpy(&L, st.vals + p, 4);
+          p += 4;
+          if (p + L > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY value in " + col.name);
+          auto ins = local.emplace(std::string_view(reinterpret_cast<const char*>(st.vals + p), L), uint32_t(local.size()));
+          if (ins.second) C.dict.emplace_back(ins.first->first);
+          idx[i] = ins.first->second;
+          p += L;
         }
         page_dict_n = uint32_t(local.size());
         int pbw = 1;
         while (pbw < 32 && (1ull << pbw) < page_dict_n) pbw++;
         const size_t ngroups = (size_t(nvals) + 7) / 8;
-        B.plain.emplace_back();
-        std::vector<uint8_t>& enc = B.plain.back();
+        C.plain.emplace_back();
+        std::vector<uint8_t>& enc = C.plain.back();
         enc.push_back(uint8_t(pbw));
         for (uint64_t hdr = (uint64_t(ngroups) << 1) | 1u;; hdr >>= 7) {   // literal-run header (ULEB128)
           enc.push_back(uint8_t((hdr & 0x7f) | (hdr >= 0x80 ? 0x80 : 0)));
@@ -620,27 +646,29 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       } else if (!have_dict) {
         throw PlanError(LK_ERR_IO, "parquet: dictionary page missing for " + col.name);
       }
-      const uint32_t dict_n = page_dict_n;
+      const uint32_t pdict = page_dict_n;
       if (st.vals_len < 1 && nvals) throw PlanError(LK_ERR_IO, "parquet: empty dictionary-index page");
       int bw = st.vals_len ? st.vals[0] : 0;
       if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
       const uint8_t* stream = st.vals_len ? st.vals + 1 : st.vals;
       size_t slen = st.vals_len ? st.vals_len - 1 : 0;
       auto runs = pq::hybrid_runs(stream, slen, bw, nvals);
-      // validate every index against the dictionary so a corrupt page can never index out of bounds on the GPU
-      std::vector<uint32_t> idx(nvals);
-      pq::hybrid_decode(stream, slen, bw, nvals, idx.data());
-      for (uint32_t v : idx)
-        if (v >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
-      hp.run_lo = uint32_t(col.runs.size());
-      for (auto& r : runs)
-        col.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
+      // validate every index against the dictionary so a corrupt page can never index out of bounds on the GPU:
+      // RLE runs by their value, bit-packed runs by their largest index
+      if (!runs.empty() && pdict < (bw >= 32 ? 0xffffffffu : (1u << bw))) {
+        for (auto& r : runs) {
+          const uint32_t mx = r.literal ? pq::hybrid_literal_max(stream + r.off, slen - r.off, bw, r.count) : r.value;
+          if (r.count && mx >= pdict) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
+        }
+      }
+      hp.run_lo = uint32_t(C.runs.size());
+      for (auto& r : runs) C.runs.push_back(RunDesc{r.start, (r.literal ? 0x80000000u : 0u) | r.off, r.value, r.count});
       hp.run_n = uint32_t(runs.size());
       d.kind = PAGE_DICT;
       d.bw = uint8_t(bw);
       d.remap = page_remap;
-      d.dict_n = dict_n;
-      d.vals = B.put(stream, slen);
+      d.dict_n = pdict;
+      d.vals = C.put(stream, slen);
       d.vals_len = uint32_t(slen);
     } else {
       if ((st.encoding == pq::RLE_DICTIONARY || st.encoding == pq::PLAIN_DICTIONARY) && width) {
@@ -652,8 +680,8 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
         if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
         std::vector<uint32_t> idx(nvals);
         pq::hybrid_decode(st.vals_len ? st.vals + 1 : st.vals, st.vals_len ? st.vals_len - 1 : 0, bw, nvals, idx.data());
-        B.plain.emplace_back(size_t(nvals) * width);
-        std::vector<uint8_t>& out = B.plain.back();
+        C.plain.emplace_back(size_t(nvals) * width);
+        std::vector<uint8_t>& out = C.plain.back();
         for (uint32_t i = 0; i < nvals; i++) {
           if (idx[i] >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
           memcpy(out.data() + size_t(i) * width, ndict.data() + size_t(idx[i]) * width, width);
@@ -667,15 +695,15 @@ void load_column_chunk(Builder& B, int ci, uint32_t rg, const pq::ColumnMeta& m)
       const size_t bytes = width ? size_t(nvals) * width : (size_t(nvals) + 7) / 8;
       if (st.vals_len < bytes) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN page in " + col.name);
       d.kind = width == 8 ? PAGE_PLAIN64 : (width == 4 ? PAGE_PLAIN32 : PAGE_BOOL);
-      d.vals = B.put(st.vals, bytes);
+      d.vals = C.put(st.vals, bytes);
       d.vals_len = uint32_t(bytes);
       hp.host_vals = st.vals;
     }
-    B.pages[ci].push_back(std::move(hp));
+    C.pages.push_back(std::move(hp));
     first_row += st.nrows;
     seen += h.type == pq::DATA_PAGE ? h.num_values : st.nrows;
   }
-  if (first_row != uint32_t(B.S.rg_rows[rg]))
+  if (int64_t(first_row) != rg_rows)
     throw PlanError(LK_ERR_IO, "parquet: column " + col.name + " row count disagrees with its row group");
 }
 
@@ -698,104 +726,139 @@ inline uint32_t run_containing(const std::vector<RunDesc>& runs, uint32_t lo, ui
   return a;
 }
 
-void build_tiles(Builder& B) {
-  Segment& S = B.S;
+// Tiles of one row group: row ranges inside one page of every column, clipped so each stream's runs over a tile fit
+// RUN_CAP; the timestamp zone map per tile.  `page0[c]`: index of column c's first page of this row group.
+void build_tiles_rg(const Segment& S, const std::vector<std::vector<HostPage>>& pages, uint32_t rg,
+                    const std::vector<size_t>& page0, std::vector<TileDesc>& tiles, std::vector<std::vector<TileCol>>& tcols) {
   const int nc = int(S.cols.size());
-  std::vector<size_t> page_cursor(nc, 0);
-  int ts_col = S.col_index(kTimestamp);
-  for (uint32_t rg = 0; rg < S.rg_rows.size(); rg++) {
-    uint32_t nrows = uint32_t(S.rg_rows[rg]);
-    uint32_t a = 0;
-    while (a < nrows) {
-      uint32_t e = std::min<uint64_t>(nrows, uint64_t(a) + TILE_ROWS);
-      // page of every column containing row a; clip e to that page's end and to the run caps
-      std::vector<size_t> pidx(nc);
-      for (int c = 0; c < nc; c++) {
-        auto& pg = B.pages[c];
-        size_t& k = page_cursor[c];
-        while (k < pg.size() && (pg[k].rg < rg || (pg[k].rg == rg && pg[k].d.first_row + pg[k].d.nrows <= a))) k++;
-        if (k >= pg.size() || pg[k].rg != rg) throw PlanError(LK_ERR_IO, "parquet: page index inconsistent");
-        pidx[c] = k;
-        const HostPage& p = pg[k];
-        e = std::min(e, p.d.first_row + p.d.nrows);
-        uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
-        if (p.d.kind == PAGE_DICT && p.run_n) {
-          uint32_t va = vindex(p, ra), ve = vindex(p, re);
-          if (ve > va) {
-            uint32_t r0 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, va);
-            uint32_t r1 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, ve - 1);
-            if (r1 - r0 + 1 > RUN_CAP) {
-              uint32_t vcut = S.cols[c].runs[r0 + RUN_CAP].start;
-              e = std::min(e, p.d.first_row + row_of_vindex(p, vcut));
-            }
-          }
-        }
-        if (p.d.has_nulls) {
-          re = e - p.d.first_row;
-          uint32_t r0 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, ra);
-          uint32_t r1 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, re - 1);
-          if (r1 - r0 + 1 > RUN_CAP) e = std::min(e, p.d.first_row + S.cols[c].runs[r0 + RUN_CAP].start);
-        }
-      }
-      if (e <= a) throw PlanError(LK_ERR_IO, "parquet: tile construction made no progress");
-      TileDesc t{};
-      t.rg = rg;
-      t.row0 = a;
-      t.nrows = e - a;
-      t.ts_min = INT64_MAX;
-      t.ts_max = INT64_MIN;
-      uint32_t tile_index = uint32_t(S.tiles.size());
-      for (int c = 0; c < nc; c++) {
-        const HostPage& p = B.pages[c][pidx[c]];
-        TileCol tc{};
-        tc.page = uint32_t(pidx[c]);
-        uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
+  const int ts_col = S.col_index(kTimestamp);
+  std::vector<size_t> cursor(page0);
+  const uint32_t nrows = uint32_t(S.rg_rows[rg]);
+  tcols.assign(size_t(nc), {});
+  uint32_t a = 0;
+  std::vector<size_t> pidx(static_cast<size_t>(nc));
+  while (a < nrows) {
+    uint32_t e = std::min<uint64_t>(nrows, uint64_t(a) + TILE_ROWS);
+    // page of every column containing row a; clip e to that page's end and to the run caps
+    for (int c = 0; c < nc; c++) {
+      auto& pg = pages[size_t(c)];
+      size_t& k = cursor[size_t(c)];
+      while (k < pg.size() && pg[k].rg == rg && pg[k].d.first_row + pg[k].d.nrows <= a) k++;
+      if (k >= pg.size() || pg[k].rg != rg) throw PlanError(LK_ERR_IO, "parquet: page index inconsistent");
+      pidx[size_t(c)] = k;
+      const HostPage& p = pg[k];
+      e = std::min(e, p.d.first_row + p.d.nrows);
+      uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
+      if (p.d.kind == PAGE_DICT && p.run_n) {
         uint32_t va = vindex(p, ra), ve = vindex(p, re);
-        tc.vbase = va;
-        tc.vals = p.d.vals;
-        tc.defs = p.d.defs;
-        tc.vals_len = p.d.vals_len;
-        tc.defs_len = p.d.defs_len;
-        tc.row_in_page = ra;
-        tc.remap = p.d.remap;
-        tc.dict_n = p.d.dict_n;
-        tc.bw = p.d.bw;
-        tc.kind = p.d.kind;
-        tc.has_nulls = p.d.has_nulls;
-        if (p.d.kind == PAGE_DICT && p.run_n && ve > va) {
-          uint32_t r0 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, va);
-          uint32_t r1 = run_containing(S.cols[c].runs, p.run_lo, p.run_n, ve - 1);
-          tc.run_lo = r0;
-          tc.nruns = r1 - r0 + 1;
-        }
-        if (p.d.has_nulls) {
-          uint32_t r0 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, ra);
-          uint32_t r1 = run_containing(S.cols[c].runs, p.drun_lo, p.drun_n, re - 1);
-          tc.drun_lo = r0;
-          tc.ndruns = r1 - r0 + 1;
-        }
-        S.cols[c].tcols.push_back(tc);
-        if (c == ts_col && p.d.kind == PAGE_PLAIN64 && !S.cols[c].is_string) {
-          for (uint32_t v = va; v < ve; v++) {
-            int64_t x;
-            memcpy(&x, p.host_vals + size_t(v) * 8, 8);
-            t.ts_min = std::min(t.ts_min, x);
-            t.ts_max = std::max(t.ts_max, x);
-          }
-        } else if (c == ts_col && p.d.kind == PAGE_PLAIN32 && S.cols[c].ptype == pq::INT32) {
-          for (uint32_t v = va; v < ve; v++) {   // INT32 timestamps (BIGINT in a union_by_name glob)
-            int32_t x;
-            memcpy(&x, p.host_vals + size_t(v) * 4, 4);
-            t.ts_min = std::min<int64_t>(t.ts_min, x);
-            t.ts_max = std::max<int64_t>(t.ts_max, x);
+        if (ve > va) {
+          uint32_t r0 = run_containing(S.cols[size_t(c)].runs, p.run_lo, p.run_n, va);
+          uint32_t r1 = run_containing(S.cols[size_t(c)].runs, p.run_lo, p.run_n, ve - 1);
+          if (r1 - r0 + 1 > RUN_CAP) {
+            uint32_t vcut = S.cols[size_t(c)].runs[r0 + RUN_CAP].start;
+            e = std::min(e, p.d.first_row + row_of_vindex(p, vcut));
           }
         }
       }
-      (void)tile_index;
-      S.tiles.push_back(t);
-      a = e;
+      if (p.d.has_nulls) {
+        re = e - p.d.first_row;
+        uint32_t r0 = run_containing(S.cols[size_t(c)].runs, p.drun_lo, p.drun_n, ra);
+        uint32_t r1 = run_containing(S.cols[size_t(c)].runs, p.drun_lo, p.drun_n, re - 1);
+        if (r1 - r0 + 1 > RUN_CAP) e = std::min(e, p.d.first_row + S.cols[size_t(c)].runs[r0 + RUN_CAP].start);
+      }
     }
+    if (e <= a) throw PlanError(LK_ERR_IO, "parquet: tile construction made no progress");
+    TileDesc t{};
+    t.rg = rg;
+    t.row0 = a;
+    t.nrows = e - a;
+    t.ts_min = INT64_MAX;
+    t.ts_max = INT64_MIN;
+    for (int c = 0; c < nc; c++) {
+      const HostPage& p = pages[size_t(c)][pidx[size_t(c)]];
+      TileCol tc{};
+      tc.page = uint32_t(pidx[size_t(c)]);
+      uint32_t ra = a - p.d.first_row, re = e - p.d.first_row;
+      uint32_t va = vindex(p, ra), ve = vindex(p, re);
+      tc.vbase = va;
+      tc.vals = p.d.vals;
+      tc.defs = p.d.defs;
+      tc.vals_len = p.d.vals_len;
+      tc.defs_len = p.d.defs_len;
+      tc.row_in_page = ra;
+      tc.remap = p.d.remap;
+      tc.dict_n = p.d.dict_n;
+      tc.bw = p.d.bw;
+      tc.kind = p.d.kind;
+      tc.has_nulls = p.d.has_nulls;
+      if (p.d.kind == PAGE_DICT && p.run_n && ve > va) {
+        uint32_t r0 = run_containing(S.cols[size_t(c)].runs, p.run_lo, p.run_n, va);
+        uint32_t r1 = run_containing(S.cols[size_t(c)].runs, p.run_lo, p.run_n, ve - 1);
+        tc.run_lo = r0;
+        tc.nruns = r1 - r0 + 1;
+      }
+      if (p.d.has_nulls) {
+        uint32_t r0 = run_containing(S.cols[size_t(c)].runs, p.drun_lo, p.drun_n, ra);
+        uint32_t r1 = run_containing(S.cols[size_t(c)].runs, p.drun_lo, p.drun_n, re - 1);
+        tc.drun_lo = r0;
+        tc.ndruns = r1 - r0 + 1;
+      }
+      tcols[size_t(c)].push_back(tc);
+      if (c == ts_col && p.d.kind == PAGE_PLAIN64 && !S.cols[size_t(c)].is_string) {
+        const int64_t* v = reinterpret_cast<const int64_t*>(p.host_vals);   // (host_vals: 8-B PLAIN values)
+        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        for (uint32_t i = va; i < ve; i++) {
+          int64_t x;
+          memcpy(&x, v + i, 8);
+          lo = std::min(lo, x);
+          hi = std::max(hi, x);
+        }
+        t.ts_min = lo;
+        t.ts_max = hi;
+      } else if (c == ts_col && p.d.kind == PAGE_PLAIN32 && S.cols[size_t(c)].ptype == pq::INT32) {
+        for (uint32_t v = va; v < ve; v++) {   // INT32 timestamps (BIGINT in a union_by_name glob)
+          int32_t x;
+          memcpy(&x, p.host_vals + size_t(v) * 4, 4);
+          t.ts_min = std::min<int64_t>(t.ts_min, x);
+          t.ts_max = std::max<int64_t>(t.ts_max, x);
+        }
+      }
+    }
+    tiles.push_back(t);
+    a = e;
   }
+}
+
+// Runs fn(i) for i in [0, n) on up to `threads` threads (the calling thread included); the first exception is
+// rethrown after every worker has finished.
+template <class F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  const size_t T = std::max<size_t>(1, std::min<size_t>(size_t(threads), n));
+  if (T <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex err_mu;
+  auto work = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      try {
+        fn(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!err) err = std::current_exception();
+        next.store(n);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < T; t++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
 }
 
 }  // namespace
@@ -823,78 +886,245 @@ Segment::~Segment() {
 }
 
 // Physical types the engine loads: BYTE_ARRAY strings, INT64 / DOUBLE (the scan's timestamp and value columns), and
-// INT32 / FLOAT / BOOLEAN (read by exemplar rows).  INT96 / FIXED_LEN_BYTE_ARRAY stay unloaded ("absent" for queries).
-static bool loadable_type(const HostCol& c) {
-  return c.is_string || c.ptype == pq::INT64 || c.ptype == pq::DOUBLE || c.ptype == pq::INT32 || c.ptype == pq::FLOAT ||
-         c.ptype == pq::BOOLEAN;
+// INT32 / FLOAT / BOOLEAN (read by exemplar rows).  INT96 / FIXED_LEN_BYTE_ARRAY are not loaded.
+static bool loadable_type(int ptype) {
+  return ptype == pq::BYTE_ARRAY || ptype == pq::INT64 || ptype == pq::DOUBLE || ptype == pq::INT32 ||
+         ptype == pq::FLOAT || ptype == pq::BOOLEAN;
 }
 
+int Engine::load_thread_count() const {
+  if (load_threads > 0) return load_threads;
+  int t = int(std::thread::hardware_concurrency());
+  if (const char* o = getenv("OMP_NUM_THREADS")) t = std::min(t > 0 ? t : 16, std::max(1, atoi(o)));
+  return std::max(1, std::min(t > 0 ? t : 8, 16));
+}
+
+// Parquet bytes -> an HBM segment.  Host: footer, schema walk, then every column chunk walked on its own thread
+// (pages, run tables, decompression, index validation), string dictionaries interned per column in row-group order,
+// tiles built per row group in parallel; device: the page streams copied once into a pinned staging area (in
+// parallel) and uploaded with one DMA, then one metadata blob.
+// A column the engine cannot decode (nested / repeated, INT96 / FIXED_LEN_BYTE_ARRAY, a page encoding or codec
+// outside the implemented set) is left unloaded with its reason (Segment::unloaded): the segment still serves every
+// query that does not reference it, and a query that does fails with LK_ERR_UNSUPPORTED -- a capability gap, not an
+// empty glob.  A corrupt file is LK_ERR_IO.
 std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uint8_t* F, size_t size) {
+  const auto t0 = std::chrono::steady_clock::now();
   auto S = std::make_shared<Segment>();
   S->key = key;
   pq::FileMeta fm = pq::parse_footer(F, size);
   if (fm.schema.empty()) throw PlanError(LK_ERR_IO, "parquet: empty schema");
-  for (size_t i = 1; i < fm.schema.size(); i++) {
-    const auto& e = fm.schema[i];
-    if (e.num_children > 0 || e.type < 0) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: nested schema");
-    if (e.repetition == pq::REPEATED) throw PlanError(LK_ERR_UNSUPPORTED, "parquet: repeated column " + e.name);
-    S->all_columns.insert(e.name);
-    S->schema.emplace_back(e.name, e.type);
-    HostCol c;
-    c.name = e.name;
-    c.ptype = e.type;
-    c.nullable = e.repetition == pq::OPTIONAL;
-    c.is_string = e.type == pq::BYTE_ARRAY;
-    S->by_name[c.name] = int(S->cols.size());
-    S->cols.push_back(std::move(c));
+  // Schema walk: top-level primitive fields are columns; a group (struct / list / map) is one top-level name whose
+  // leaves occupy column chunks but are not loaded.  leaf_col[i] = index into S->cols of the i-th leaf, or -1.
+  std::vector<int> leaf_col;
+  {
+    size_t i = 1;
+    const int ntop = fm.schema[0].num_children > 0 ? fm.schema[0].num_children : int(fm.schema.size()) - 1;
+    for (int f = 0; f < ntop && i < fm.schema.size(); f++) {
+      const auto& e = fm.schema[i];
+      if (e.num_children > 0) {   // nested group: skip its subtree, counting its leaves
+        S->all_columns.insert(e.name);
+        S->unloaded[e.name] = "nested column " + e.name + " (struct / list / map) is not loaded";
+        S->schema.emplace_back(e.name, -1);   // SELECT * names it (a query that reads it fails: unloaded)
+        size_t pending = 1;
+        while (pending && i < fm.schema.size()) {
+          const auto& g = fm.schema[i++];
+          pending--;
+          if (g.num_children > 0) pending += size_t(g.num_children);
+          else leaf_col.push_back(-1);
+        }
+        continue;
+      }
+      i++;
+      S->all_columns.insert(e.name);
+      S->schema.emplace_back(e.name, e.type);
+      if (e.repetition == pq::REPEATED) {
+        S->unloaded[e.name] = "repeated column " + e.name + " is not loaded";
+        leaf_col.push_back(-1);
+        continue;
+      }
+      if (!loadable_type(e.type)) {
+        S->unloaded[e.name] = "column " + e.name + " of Parquet physical type " + std::to_string(e.type) +
+                              " (INT96 / FIXED_LEN_BYTE_ARRAY) is not loaded";
+        leaf_col.push_back(-1);
+        continue;
+      }
+      HostCol c;
+      c.name = e.name;
+      c.ptype = e.type;
+      c.nullable = e.repetition == pq::OPTIONAL;
+      c.is_string = e.type == pq::BYTE_ARRAY;
+      leaf_col.push_back(int(S->cols.size()));
+      S->cols.push_back(std::move(c));
+    }
   }
   S->num_rows = fm.num_rows;
+  const size_t nrg = fm.row_groups.size();
   for (auto& g : fm.row_groups) {
-    if (g.columns.size() != S->cols.size()) throw PlanError(LK_ERR_IO, "parquet: row group column count mismatch");
+    if (g.columns.size() != leaf_col.size()) throw PlanError(LK_ERR_IO, "parquet: row group column count mismatch");
     S->rg_rows.push_back(g.num_rows);
   }
-  Builder B{*this, F, size, *S, {}, {}, {}};
-  B.pages.resize(S->cols.size());
-  B.stage.reserve(size);
-  for (uint32_t rg = 0; rg < fm.row_groups.size(); rg++) {
-    for (size_t ci = 0; ci < S->cols.size(); ci++) {
-      HostCol& col = S->cols[ci];
-      // only the physical types the kernels decode are loaded; others stay "absent" for queries
-      if (!loadable_type(col)) continue;
-      load_column_chunk(B, int(ci), rg, fm.row_groups[rg].columns[ci]);
+  const int threads = load_thread_count();
+
+  // ---- 1. every (column, row group) chunk walked in parallel ----
+  const size_t ncol = S->cols.size();
+  std::vector<int> leaf_of(ncol);
+  for (size_t l = 0; l < leaf_col.size(); l++)
+    if (leaf_col[l] >= 0) leaf_of[size_t(leaf_col[l])] = int(l);
+  std::vector<ChunkOut> chunks(ncol * nrg);   // [column][row group]
+  parallel_for(chunks.size(), threads, [&](size_t k) {
+    const size_t ci = k / std::max<size_t>(nrg, 1), rg = k % std::max<size_t>(nrg, 1);
+    ChunkOut& C = chunks[k];
+    try {
+      walk_column_chunk(F, size, S->cols[ci], uint32_t(rg), S->rg_rows[rg], fm.row_groups[rg].columns[size_t(leaf_of[ci])], C);
+    } catch (const PlanError& e) {
+      C.code = e.code;
+      C.msg = e.what();
+    } catch (const std::bad_alloc&) {
+      throw;
+    } catch (const std::exception& e) {   // thrift / codec parse errors: the file is corrupt
+      C.code = LK_ERR_IO;
+      C.msg = e.what();
     }
-  }
-  // drop columns of unsupported types from the index
-  for (size_t ci = 0; ci < S->cols.size(); ci++) {
-    HostCol& col = S->cols[ci];
-    if (!loadable_type(col)) col.unsupported = true;
-  }
-  // unsupported columns still need page lists for tile building: give them none and skip in build_tiles
-  {
+  });
+  // a corrupt chunk fails the segment (LK_ERR_IO); a chunk outside the implemented shapes unloads its column
+  std::vector<char> keep(ncol, 1);
+  for (size_t ci = 0; ci < ncol; ci++)
+    for (size_t rg = 0; rg < nrg; rg++) {
+      const ChunkOut& C = chunks[ci * nrg + rg];
+      if (C.code == LK_ERR_IO) throw PlanError(LK_ERR_IO, C.msg);
+      if (C.code && keep[ci]) {
+        keep[ci] = 0;
+        S->unloaded[S->cols[ci].name] = C.code == LK_ERR_UNSUPPORTED ? C.msg : ("column " + S->cols[ci].name + ": " + C.msg);
+      }
+    }
+  {   // drop unloaded columns (and their chunks) from the index
     std::vector<HostCol> kept;
-    std::vector<std::vector<HostPage>> kept_pages;
+    std::vector<ChunkOut> kept_chunks;
     S->by_name.clear();
-    for (size_t ci = 0; ci < S->cols.size(); ci++) {
-      if (S->cols[ci].unsupported) continue;
+    for (size_t ci = 0; ci < ncol; ci++) {
+      if (!keep[ci]) continue;
       S->by_name[S->cols[ci].name] = int(kept.size());
       kept.push_back(std::move(S->cols[ci]));
-      kept_pages.push_back(std::move(B.pages[ci]));
+      for (size_t rg = 0; rg < nrg; rg++) kept_chunks.push_back(std::move(chunks[ci * nrg + rg]));
     }
     S->cols = std::move(kept);
-    B.pages = std::move(kept_pages);
+    chunks = std::move(kept_chunks);
   }
-  if (S->num_rows > 0 && !S->cols.empty()) build_tiles(B);
-  for (size_t ci = 0; ci < S->cols.size(); ci++) {
-    auto& col = S->cols[ci];
-    for (auto& hp : B.pages[ci]) col.pages.push_back(hp.d);
-  }
+  const size_t nc = S->cols.size();
 
-  // ---- upload: streams, then one metadata blob per segment ----
+  // ---- 2. per column, in row-group order: intern dictionaries, concatenate runs and pages, place streams ----
+  std::vector<size_t> chunk_base(chunks.size());   // byte offset of each chunk's stream area in the segment
+  {
+    size_t off = 0;
+    for (size_t k = 0; k < chunks.size(); k++) {
+      off = (off + 127) / 128 * 128;
+      chunk_base[k] = off;
+      off += chunks[k].bytes;
+    }
+    S->data_bytes = align_up(off + 64);
+  }
+  std::vector<std::vector<HostPage>> pages(nc);
+  std::vector<std::vector<size_t>> page0(nc, std::vector<size_t>(nrg, 0));   // first page of (column, row group)
+  parallel_for(nc, threads, [&](size_t ci) {
+    HostCol& col = S->cols[ci];
+    size_t npages = 0, nruns = 0, ndict = 0;
+    for (size_t rg = 0; rg < nrg; rg++) {
+      npages += chunks[ci * nrg + rg].pages.size();
+      nruns += chunks[ci * nrg + rg].runs.size();
+      ndict += chunks[ci * nrg + rg].dict.size();
+    }
+    pages[ci].reserve(npages);
+    col.runs.reserve(nruns);
+    col.remap.reserve(ndict);
+    if (col.is_string && ndict) {
+      GlobalDict& gd = dict(col.name);
+      std::lock_guard<std::mutex> g(gd.mu);
+      for (size_t rg = 0; rg < nrg; rg++)
+        for (const std::string& v : chunks[ci * nrg + rg].dict) col.remap.push_back(gd.intern(v));
+    }
+    uint32_t remap_base = 0;
+    for (size_t rg = 0; rg < nrg; rg++) {
+      ChunkOut& C = chunks[ci * nrg + rg];
+      const uint32_t run_base = uint32_t(col.runs.size());
+      const uint64_t base = chunk_base[ci * nrg + rg];
+      page0[ci][rg] = pages[ci].size();
+      col.runs.insert(col.runs.end(), C.runs.begin(), C.runs.end());
+      col.compressed_bytes += C.compressed;
+      for (HostPage& hp : C.pages) {
+        hp.run_lo += run_base;
+        hp.drun_lo += run_base;
+        hp.d.vals += base;
+        if (hp.d.has_nulls) hp.d.defs += base;
+        if (hp.d.kind == PAGE_DICT) hp.d.remap += remap_base;
+        pages[ci].push_back(std::move(hp));
+      }
+      remap_base += uint32_t(C.dict.size());
+      std::vector<RunDesc>().swap(C.runs);
+    }
+  });
+
+  // ---- 3. tiles, per row group in parallel ----
+  std::vector<std::vector<TileDesc>> rg_tiles(nrg);
+  std::vector<std::vector<std::vector<TileCol>>> rg_tcols(nrg);
+  if (S->num_rows > 0 && nc) {
+    parallel_for(nrg, threads, [&](size_t rg) {
+      std::vector<size_t> p0(nc);
+      for (size_t c = 0; c < nc; c++) p0[c] = page0[c][rg];
+      build_tiles_rg(*S, pages, uint32_t(rg), p0, rg_tiles[rg], rg_tcols[rg]);
+    });
+    for (size_t rg = 0; rg < nrg; rg++) {
+      S->tiles.insert(S->tiles.end(), rg_tiles[rg].begin(), rg_tiles[rg].end());
+      for (size_t c = 0; c < nc; c++)
+        S->cols[c].tcols.insert(S->cols[c].tcols.end(), rg_tcols[rg][c].begin(), rg_tcols[rg][c].end());
+    }
+  }
+  for (size_t ci = 0; ci < nc; ci++) {
+    auto& col = S->cols[ci];
+    col.pages.reserve(pages[ci].size());
+    for (auto& hp : pages[ci]) col.pages.push_back(hp.d);
+  }
+  const double host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+
+  // ---- 4. upload: the streams through the pinned staging area (filled in parallel), then the metadata blob ----
   std::lock_guard<std::mutex> dg(dev_mu);
   HIP_CHECK(hipSetDevice(device));
-  S->data_bytes = align_up(B.stage.size() + 64);
   HIP_CHECK(hipMalloc(&S->d_data, S->data_bytes));
-  HIP_CHECK(hipMemcpy(S->d_data, B.stage.data(), B.stage.size(), hipMemcpyHostToDevice));
+  {
+    // every stream, with its destination offset, cut at staging-piece boundaries
+    struct Copy {
+      const uint8_t* src;
+      size_t len;
+      size_t dst;
+    };
+    std::vector<Copy> copies;
+    for (size_t k = 0; k < chunks.size(); k++)
+      for (const StreamRef& r : chunks[k].streams) copies.push_back(Copy{r.src, r.len, chunk_base[k] + r.off});
+    const size_t piece = std::min<size_t>(S->data_bytes, size_t(1) << 30);
+    if (load_pinned_cap < piece) {
+      if (load_pinned) HIP_CHECK(hipHostFree(load_pinned));
+      load_pinned = nullptr;
+      load_pinned_cap = 0;
+      HIP_CHECK(hipHostMalloc(&load_pinned, piece));
+      load_pinned_cap = piece;
+    }
+    uint8_t* pin = static_cast<uint8_t*>(load_pinned);
+    size_t ci0 = 0;
+    for (size_t lo = 0; lo < S->data_bytes; lo += piece) {
+      const size_t hi = std::min(S->data_bytes, lo + piece);
+      // the copies overlapping [lo, hi): split into ~8 MB work items
+      std::vector<Copy> work;
+      while (ci0 < copies.size() && copies[ci0].dst + copies[ci0].len <= lo) ci0++;
+      for (size_t c = ci0; c < copies.size() && copies[c].dst < hi; c++) {
+        size_t a = std::max(lo, copies[c].dst), b = std::min(hi, copies[c].dst + copies[c].len);
+        for (size_t x = a; x < b; x += size_t(8) << 20) {
+          const size_t y = std::min(b, x + (size_t(8) << 20));
+          work.push_back(Copy{copies[c].src + (x - copies[c].dst), y - x, x - lo});
+        }
+      }
+      parallel_for(work.size(), threads, [&](size_t w) { memcpy(pin + work[w].dst, work[w].src, work[w].len); });
+      HIP_CHECK(hipMemcpy(S->d_data + lo, pin, hi - lo, hipMemcpyHostToDevice));
+    }
+  }
   size_t meta = align_up(S->tiles.size() * sizeof(TileDesc));
   for (auto& c : S->cols) {
     meta += align_up(c.pages.size() * sizeof(PageDesc)) + align_up(c.runs.size() * sizeof(RunDesc)) +
@@ -939,6 +1169,8 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     std::vector<TileCol>().swap(c.tcols);
     std::vector<uint32_t>().swap(c.remap);
   }
+  S->load_host_ms = host_ms;
+  S->load_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   return S;
 }
 
@@ -953,6 +1185,10 @@ size_t Engine::evict_lru_locked(size_t target_bytes, const std::string& keep, st
     cache_bytes -= b;
     freed += b;
     evictions++;
+    if (victim->second->from_put) {
+      if (evicted_puts.size() >= (size_t(1) << 20)) evicted_puts.clear();   // bounded (then: a missing-file error)
+      evicted_puts.insert(victim->first);
+    }
     if (out) out->push_back(std::move(victim->second));   // destroyed by the caller after cache_mu
     cache.erase(victim);
   }
@@ -976,7 +1212,7 @@ static std::shared_ptr<Segment> build_checked(Engine& E, const std::string& key,
   }
 }
 
-int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size) {
+int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size, bool from_put) {
   std::shared_ptr<Segment> S;
   try {
     S = build_checked(*this, key, data, size);
@@ -995,8 +1231,12 @@ int Engine::put_segment(const std::string& key, const uint8_t* data, size_t size
     S = build_checked(*this, key, data, size);
   }
   S->last_use = ++use_clock;
+  S->from_put = from_put;
   std::vector<std::shared_ptr<Segment>> dead;   // replaced / evicted segments, destroyed after cache_mu
   std::lock_guard<std::mutex> g(cache_mu);
+  evicted_puts.erase(key);
+  load_host_ms_total += S->load_host_ms;
+  load_ms_total += S->load_ms;
   auto it = cache.find(key);
   if (it != cache.end()) {
     cache_bytes -= it->second->data_bytes + it->second->meta_bytes;
@@ -1018,10 +1258,15 @@ std::shared_ptr<Segment> Engine::get_segment(const std::string& key, bool load_o
     }
   }
   if (!load_on_miss) return nullptr;
+  {
+    std::lock_guard<std::mutex> g(cache_mu);
+    if (evicted_puts.count(key))
+      throw PlanError(LK_ERR_EVICTED, "segment " + key + " was evicted from the HBM cache (lk_segment_put it again)");
+  }
   std::ifstream f(key, std::ios::binary);
   if (!f) throw PlanError(LK_ERR_IO, "cannot open segment " + key);
   std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-  put_segment(key, buf.data(), buf.size());
+  put_segment(key, buf.data(), buf.size(), false);
   std::lock_guard<std::mutex> g(cache_mu);
   return cache[key];
 }
@@ -1043,6 +1288,7 @@ Engine::~Engine() {
   comm_destroy();
   ctx_free.clear();
   cache.clear();
+  if (load_pinned) (void)hipHostFree(load_pinned);
 }
 
 std::unique_ptr<CallCtx> Engine::acquire_ctx() {

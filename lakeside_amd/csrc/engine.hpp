@@ -13,6 +13,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 
 #include "layout.hpp"
@@ -90,6 +91,11 @@ struct Segment {
   std::vector<int64_t> rg_rows;
   std::vector<HostCol> cols;                     // loadable columns
   std::set<std::string> all_columns;             // every column of the file (DESCRIBE, Commons.scala:214-221)
+  // columns of the file the engine does not decode (nested / repeated, INT96 / FIXED_LEN_BYTE_ARRAY, an encoding or
+  // codec outside the implemented set) -> why; a query referencing one fails with LK_ERR_UNSUPPORTED
+  std::map<std::string, std::string> unloaded;
+  double load_host_ms = 0, load_ms = 0;          // build_segment: host walk / total (stats)
+  bool from_put = false;                         // registered by lk_segment_put (its key is not a file path)
   std::vector<std::pair<std::string, int>> schema;   // (name, Parquet physical type) in file order (SELECT *)
   std::unordered_map<std::string, int> by_name;
   std::vector<TileDesc> tiles;
@@ -205,6 +211,17 @@ struct Engine {
   size_t hbm_budget = 0;
   std::atomic<uint64_t> use_clock{0};
   size_t evictions = 0;
+  // Keys registered with lk_segment_put that the LRU policy evicted since: an evaluation naming one fails with
+  // LK_ERR_EVICTED (the caller re-puts it) instead of treating the key as a missing file.  Cleared per key
+  // by a re-put or lk_segment_evict; bounded.
+  std::unordered_set<std::string> evicted_puts;
+  // Segment ingest: host threads of build_segment (lk_engine_create {"load_threads": N}; 0 = OMP_NUM_THREADS or the
+  // hardware threads, at most 16) and the pinned staging area its upload goes through (under dev_mu).
+  int load_threads = 0;
+  int load_thread_count() const;
+  void* load_pinned = nullptr;
+  size_t load_pinned_cap = 0;
+  double load_host_ms_total = 0, load_ms_total = 0;   // cumulative (lk_engine_stats)
   // evict LRU segments (never `keep`) until cache_bytes + extra <= budget; caller holds cache_mu
   size_t evict_lru_locked(size_t target_bytes, const std::string& keep, std::vector<std::shared_ptr<Segment>>* out);
   std::mutex dict_mu;
@@ -247,7 +264,7 @@ struct Engine {
   ~Engine();
   GlobalDict& dict(const std::string& col);
   std::shared_ptr<Segment> build_segment(const std::string& key, const uint8_t* data, size_t size);
-  int put_segment(const std::string& key, const uint8_t* data, size_t size);
+  int put_segment(const std::string& key, const uint8_t* data, size_t size, bool from_put = true);
   std::shared_ptr<Segment> get_segment(const std::string& key, bool load_on_miss);
   std::unique_ptr<CallCtx> acquire_ctx();
   void release_ctx(std::unique_ptr<CallCtx> c);

@@ -454,7 +454,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         try {
           segs[i] = E.get_segment(paths[i], true);
         } catch (const PlanError& e) {
-          if (e.code != LK_ERR_IO && e.code != LK_ERR_UNSUPPORTED) throw;
+          // only the file's own faults (missing, unreadable, corrupt) empty its glob; an engine capability gap
+          // (LK_ERR_UNSUPPORTED) or an evicted put key (LK_ERR_EVICTED) fails the call
+          if (e.code != LK_ERR_IO) throw;
           seg_bad[i] = 1;
           if (bad_msg.empty()) bad_msg = e.what();
         }
@@ -492,6 +494,12 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const size_t np = probe_cols.size();
   const size_t ng = globs.size();
   std::vector<uint8_t> exists(ng * np + 2 * ng + 1, 0);
+  // A referenced column this engine does not decode (Segment::unloaded) fails the call with LK_ERR_UNSUPPORTED: DuckDB
+  // would read it, so the shim must fall back rather than see an empty glob.  Rank-local (it depends on
+  // this rank's segments): agreed on with the load status below.
+  std::vector<std::string> ref_cols(probe_cols);
+  for (auto& sc : strs) ref_cols.push_back(sc.name);
+  for (auto& nm : nums) ref_cols.push_back(nm);
   uint8_t* gfail = exists.data() + ng * np;
   uint8_t* gvrank = gfail + ng;
   for (size_t gi = 0; gi < ng; gi++)
@@ -501,6 +509,15 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       const Segment& S = *segs[si];
       for (size_t k = 0; k < np; k++)
         if (S.all_columns.count(probe_cols[k])) exists[gi * np + k] = 1;
+      if (!S.unloaded.empty() && !load_err)
+        for (auto& c : ref_cols) {
+          auto u = S.unloaded.find(c);
+          if (u == S.unloaded.end()) continue;
+          if (!dist) throw PlanError(LK_ERR_UNSUPPORTED, u->second + " (" + S.key + ")");
+          load_err = LK_ERR_UNSUPPORTED;
+          load_msg = u->second + " (" + S.key + ")";
+          break;
+        }
       int vc = S.col_index(vcol);
       // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
       if (vc < 0 || S.cols[vc].any_nulls) exists.back() = 1;
@@ -519,7 +536,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       };
       if (bad(kTimestamp, 0)) gfail[gi] = 1;
       if (!tagq) {
-        if (bad(vcol, 1)) gfail[gi] = 1;
+        if (bad(vcol, 1)) {
+          // sum / avg over a VARCHAR value column is DuckDB's Binder Error (empty glob); count / min / max over it
+          // run in DuckDB and this engine does not implement them: the call fails (LK_ERR_UNSUPPORTED)
+          if (vc >= 0 && S.cols[size_t(vc)].is_string && agg != AGG_SUM && agg != AGG_AVG && !load_err) {
+            const std::string m = "aggregation over the VARCHAR value column " + vcol + " (" + S.key + ")";
+            if (!dist) throw PlanError(LK_ERR_UNSUPPORTED, m);
+            load_err = LK_ERR_UNSUPPORTED;
+            load_msg = m;
+          }
+          gfail[gi] = 1;
+        }
         else if (vc >= 0) gvrank[gi] = std::max<uint8_t>(gvrank[gi], uint8_t(value_rank(S.cols[size_t(vc)].ptype)));
       }
       for (auto& sc : strs)

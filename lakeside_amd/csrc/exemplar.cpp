@@ -265,7 +265,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     try {
       segs[i] = E.get_segment(paths[i], true);
     } catch (const PlanError& e) {
-      if (e.code != LK_ERR_IO && e.code != LK_ERR_UNSUPPORTED) throw;
+      if (e.code != LK_ERR_IO) throw;   // capability gaps / evicted keys fail the call
       seg_bad[i] = 1;
     }
   }
@@ -289,11 +289,9 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       }
       for (auto& [name, pt] : segs[si]->schema) {
         if (!g.types.count(name)) uni.push_back(name);
-        try {
-          g.types[name] = union_type(g.types.count(name) ? g.types[name] : -1, pt);
-        } catch (const PlanError&) {   // a union DuckDB cannot form / this engine does not decode: the glob fails
-          g.skip = true;
-        }
+        // a union this engine does not form (e.g. VARCHAR with a number, which DuckDB unifies to VARCHAR): the call
+        // fails with LK_ERR_UNSUPPORTED so the caller can fall back, not an empty glob
+        g.types[name] = union_type(g.types.count(name) ? g.types[name] : -1, pt);
       }
     }
     for (auto& l : leaves)   // nonExistentFields -> literal false (Commons.scala:224, BaseExpr.scala:462-464)
@@ -354,6 +352,23 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   std::vector<uint32_t> qseg_pos, qseg_glob;
   uint64_t rows_scanned = 0;
   uint32_t max_tiles = 0;
+  // a referenced column this engine does not decode fails the call (LK_ERR_UNSUPPORTED: the caller falls back), where
+  // a column of a type the query cannot bind is DuckDB's Binder Error (empty glob, below)
+  for (size_t gi = 0; gi < globs.size(); gi++) {
+    if (globs[gi].skip) continue;
+    for (int si : globs[gi].segs) {
+      if (!segs[si] || segs[si]->unloaded.empty()) continue;
+      const Segment& S = *segs[si];
+      auto check = [&](const std::string& c) {
+        auto u = S.unloaded.find(c);
+        if (u != S.unloaded.end()) throw PlanError(LK_ERR_UNSUPPORTED, u->second + " (" + S.key + ")");
+      };
+      check(kTimestamp);
+      for (auto& sc : strs) check(sc.name);
+      for (auto& nm : nums) check(nm);
+      for (auto& c : globs[gi].cols) check(c);
+    }
+  }
   for (size_t gi = 0; gi < globs.size(); gi++) {
     XGlob& g = globs[gi];
     if (g.skip || g.win_lo >= g.win_hi || limit == 0) continue;

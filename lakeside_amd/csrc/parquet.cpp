@@ -236,6 +236,20 @@ std::vector<HRun> hybrid_runs(const uint8_t* p, size_t len, int bw, uint32_t nva
   return runs;
 }
 
+// The i-th bw-bit value of a bit-packed group stream (LSB first) of `avail` bytes: one unaligned 8-byte load where
+// it fits, else byte by byte at the stream's end.
+static inline uint32_t unpack_at(const uint8_t* d, size_t avail, int bw, uint64_t mask, uint64_t i) {
+  const uint64_t bit = i * uint64_t(bw);
+  const size_t b0 = size_t(bit >> 3);
+  uint64_t w = 0;
+  if (b0 + 8 <= avail) {
+    memcpy(&w, d + b0, 8);
+  } else {
+    for (size_t k = 0; k < 8 && b0 + k < avail; k++) w |= uint64_t(d[b0 + k]) << (8 * k);
+  }
+  return uint32_t((w >> (bit & 7)) & mask);
+}
+
 void hybrid_decode(const uint8_t* p, size_t len, int bw, uint32_t nvalues, uint32_t* out) {
   auto runs = hybrid_runs(p, len, bw, nvalues);
   const uint64_t mask = bw >= 32 ? 0xffffffffull : ((1ull << bw) - 1);
@@ -243,16 +257,16 @@ void hybrid_decode(const uint8_t* p, size_t len, int bw, uint32_t nvalues, uint3
     if (!r.literal) {
       for (uint32_t i = 0; i < r.count; i++) out[r.start + i] = r.value;
     } else {
-      const uint8_t* d = p + r.off;
-      for (uint32_t i = 0; i < r.count; i++) {
-        uint64_t bit = uint64_t(i) * bw;
-        uint64_t w = 0;
-        size_t b0 = bit >> 3;
-        for (int k = 0; k < 8 && d + b0 + k < p + len; k++) w |= uint64_t(d[b0 + k]) << (8 * k);
-        out[r.start + i] = uint32_t((w >> (bit & 7)) & mask);
-      }
+      for (uint32_t i = 0; i < r.count; i++) out[r.start + i] = unpack_at(p + r.off, len - r.off, bw, mask, i);
     }
   }
+}
+
+uint32_t hybrid_literal_max(const uint8_t* d, size_t avail, int bw, uint32_t count) {
+  const uint64_t mask = bw >= 32 ? 0xffffffffull : ((1ull << bw) - 1);
+  uint32_t mx = 0;
+  for (uint32_t i = 0; i < count; i++) mx = std::max(mx, unpack_at(d, avail, bw, mask, i));
+  return mx;
 }
 
 }  // namespace pq

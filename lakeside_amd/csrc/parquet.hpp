@@ -81,6 +81,8 @@ struct HRun {
 std::vector<HRun> hybrid_runs(const uint8_t* p, size_t len, int bw, uint32_t nvalues);
 // Decode the whole stream (host reference; used for zone maps and validity counts).
 void hybrid_decode(const uint8_t* p, size_t len, int bw, uint32_t nvalues, uint32_t* out);
+// Largest value of a bit-packed run of `count` bw-bit values at `d` (`avail` bytes readable): index validation.
+uint32_t hybrid_literal_max(const uint8_t* d, size_t avail, int bw, uint32_t count);
 
 }  // namespace pq
 }  // namespace lk

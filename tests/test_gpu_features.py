@@ -236,6 +236,7 @@ def test_hbm_budget_lru_eviction():
     cache, WorkerApi.scala:53-64): inserts past the budget evict the least recently used segments; a segment used
     by a query is recent; an evicted key is re-loaded on demand (here: put again) and answers identically."""
     from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd._lib import LK_ERR_EVICTED, LakesideError
     from lakeside_amd.evaluator import Engine
     blobs = []
     for i in range(4):
@@ -255,9 +256,14 @@ def test_hbm_budget_lru_eviction():
         e.put_segment("s2", blobs[2])                              # over budget: s1 (LRU) goes
         assert e.segment_count == 2 and e.segment_bytes <= int(2.5 * one)
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
-        gone = e.eval_pushdown(req, ["s1"], 10, LK_MERGED)         # evicted, and not a file path: its glob
-        assert len(gone) == 0 and gone.stats["failed_globs"] == 1   # fails alone (Commons.scala:249-253)
-        e.put_segment("s3", blobs[3])                              # s2 is now the LRU
+        # evicted put key: the call fails with LK_ERR_EVICTED so the caller re-puts it -- it is not a
+        # missing file, whose glob alone would be empty
+        with pytest.raises(LakesideError) as ei:
+            e.eval_pushdown(req, ["s1"], 10, LK_MERGED)
+        assert ei.value.code == LK_ERR_EVICTED, ei.value
+        e.put_segment("s1", blobs[1])                              # re-put: answers again (s2 goes, LRU)
+        assert len(e.eval_pushdown(req, ["s1"], 10, LK_MERGED)) == len(want)
+        e.put_segment("s3", blobs[3])                              # s0 is now the LRU
         assert e.segment_count == 2
         e.put_segment("s0", blobs[0])
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want

@@ -120,8 +120,8 @@ def test_three_globs_missing_path_int64_value_clean(engine, glob_files, agg):
 def test_value_type_unions(engine, glob_files, agg):
     """union_by_name over the value column: INT32 + FLOAT -> FLOAT (integers cast to FLOAT first: |v| > 2^24 round),
     INT64 + INT32 -> BIGINT, a corrupt file fails only its own glob, and so does (for sum: a Binder Error) a VARCHAR
-    value column.  (min / max / count over a VARCHAR value column would run in DuckDB -- string order, then
-    getDouble of the text; the engine empties that glob instead: DESIGN.md §9.)"""
+    value column.  (min / max / count over a VARCHAR value column run in DuckDB; the engine does not implement them
+    and fails the call with LK_ERR_UNSUPPORTED, so the caller can fall back: test_text_value_column_minmax_unsupported.)"""
     from lakeside_amd import synth
     f = glob_files
     paths = [f["int32v"], f["floatv"], f["int64v_b"], f["int32v_b"], f["corrupt"], f["clean0"]]
@@ -133,6 +133,19 @@ def test_value_type_unions(engine, glob_files, agg):
     assert stats["failed_globs"] == (2 if agg == "sum" else 1), stats
     if agg == "sum":
         assert cells[3] == []
+
+
+@pytest.mark.parametrize("agg", ["min", "max", "count"])
+def test_text_value_column_minmax_unsupported(engine, glob_files, agg):
+    """an engine capability gap fails the call (LK_ERR_UNSUPPORTED) instead of emptying a glob."""
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd._lib import LK_ERR_UNSUPPORTED, LakesideError
+    f = glob_files
+    paths = [f["clean0"], f["textv"]]
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "!=", "metric_03"), _segs(len(paths)), agg, []))
+    with pytest.raises(LakesideError) as ei:
+        engine.eval_pushdown(req, paths, 1, LK_MERGED)
+    assert ei.value.code == LK_ERR_UNSUPPORTED, ei.value
 
 
 def test_bad_regex_fails_only_globs_with_the_field(engine, glob_files):
@@ -258,3 +271,50 @@ def test_merged_min_absorbs_all_nan_glob(engine, tmp_path):
     req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(2), "max", [])
     _compare(engine, req, [pa_, pb], 1, "max", "max nan")
     assert "redo" not in engine.eval_pushdown(json.dumps(req), [pa_, pb], 1, LK_MERGED).stats
+
+
+def _write_exotic(path, rng, hour):
+    """clean columns + columns this engine does not decode: a struct, a list, an INT96 timestamp, a 16-byte
+    FIXED_LEN_BYTE_ARRAY, a DELTA_BINARY_PACKED int64 and a BROTLI-compressed double."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    base = pq.read_table(_write(path, rng, hour))
+    n = base.num_rows
+    t = base.append_column("attrs", pa.array([{"a": int(i), "b": f"x{i % 7}"} for i in range(n)]))
+    t = t.append_column("tags", pa.array([[f"t{i % 3}", "u"] for i in range(n)], pa.list_(pa.string())))
+    t = t.append_column("ts96", pa.array(rng.integers(0, 1 << 50, n), pa.timestamp("ns")))
+    t = t.append_column("uuid", pa.array([bytes(16) for _ in range(n)], pa.binary(16)))
+    t = t.append_column("delta_col", pa.array(rng.integers(0, 1000, n), pa.int64()))
+    t = t.append_column("brot", pa.array(rng.random(n), pa.float64()))
+    plain = ["_cardinalhq.timestamp", "_cardinalhq.value", "ts96", "brot"]
+    enc = {c: "PLAIN" for c in plain}
+    enc["delta_col"] = "DELTA_BINARY_PACKED"
+    comp = {c: "NONE" for c in t.column_names}
+    comp["brot"] = "BROTLI"
+    pq.write_table(t, path, compression=comp, use_dictionary=["_cardinalhq.name", "resource.service.name"],
+                   column_encoding=enc, row_group_size=30_000, data_page_size=1 << 16,
+                   use_deprecated_int96_timestamps=True)
+    return path
+
+
+def test_unloaded_columns_serve_other_queries(engine, tmp_path):
+    """a file with columns this engine does not decode (nested struct / list, INT96,
+    FIXED_LEN_BYTE_ARRAY, DELTA_BINARY_PACKED, BROTLI) still serves every query that does not reference them (GPU ==
+    oracle); a query that references one fails the call with LK_ERR_UNSUPPORTED (the caller falls back) instead of
+    silently emptying the glob."""
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd._lib import LK_ERR_UNSUPPORTED, LakesideError
+    rng = np.random.default_rng(7)
+    paths = [_write_exotic(str(tmp_path / f"exotic{i}.parquet"), rng, i) for i in range(2)]
+    req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(2), "sum", [synth.SERVICE])
+    cells, stats = _compare(engine, req, paths, 1, "sum", "exotic columns unreferenced")
+    assert stats["failed_globs"] == 0 and cells[0] and cells[1], stats
+    for col, leaf in [("uuid", synth.leaf("uuid", "eq", "x")), ("attrs", synth.leaf("attrs", "eq", "x")),
+                      ("tags", synth.leaf("tags", "eq", "x")),
+                      ("delta_col", {"k": "delta_col", "v": ["5"], "op": "gt", "dataType": "number"}),
+                      ("brot", {"k": "brot", "v": ["0.5"], "op": "lt", "dataType": "number"}),
+                      ("ts96", {"k": "ts96", "v": ["5"], "op": "gt", "dataType": "number"})]:
+        filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"), "q2": leaf}
+        with pytest.raises(LakesideError) as ei:
+            engine.eval_pushdown(json.dumps(synth.pushdown(filt, _segs(2), "sum", [])), paths, 1, LK_MERGED)
+        assert ei.value.code == LK_ERR_UNSUPPORTED and col in str(ei.value), (col, ei.value)
