@@ -25,6 +25,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstring>
 #include <map>
 #include <string>
@@ -381,8 +382,11 @@ void fault_point(const Engine& E, const char* stage) {
   if (!f || !*f) return;
   const std::string spec(f);
   const size_t at = spec.find('@');
-  if (spec.substr(0, at) != stage) return;
-  if (at != std::string::npos && atoi(spec.c_str() + at + 1) != comm_rank(E)) return;
+  const bool hit = spec.substr(0, at) == stage &&
+                   (at == std::string::npos || atoi(spec.c_str() + at + 1) == comm_rank(E));
+  if (getenv("LK_FAULT_TRACE"))
+    fprintf(stderr, "[lk fault] rank %d stage %s spec %s -> %s\n", comm_rank(E), stage, f, hit ? "inject" : "pass");
+  if (!hit) return;
   throw PlanError(LK_ERR_DEVICE, std::string("injected fault at stage '") + stage + "' (LK_FAULT)");
 }
 

@@ -292,8 +292,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   //   SELECT "<tag>", COUNT(*) AS count FROM {table} WHERE <filter> AND <window> GROUP BY "<tag>"
   // i.e. the same scan with one group dim (the tag), one bucket and COUNT(*) (rows, NULL values included).
   const bool tagq = R.is_tag_query && !R.tag_name.empty();
-  if (tagq && R.tag_data_type != "string")
-    throw PlanError(LK_ERR_UNSUPPORTED, "tag query over a " + R.tag_data_type + " tag");
+  // (tagDataType -- "string", "number", ... from the API's query parameter, QueryApi.scala:128-129 -- does not enter
+  // the worker's SQL: the tag column's own type decides; a numeric tag column takes the row scan, below)
   if (!tagq && R.is_tag_query)   // isTagQuery without a tagDataType: SELECT * ... WHERE <filter> (BaseExpr.scala:231-232)
     throw PlanError(LK_ERR_UNSUPPORTED, "tag queries without a tagDataType");
   if (R.field_chart || R.has_extract || R.has_compute)
@@ -473,6 +473,19 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     load_err = err;
     load_msg = msg;
   }
+  // A tag query over a numeric tag column (INT32 / INT64 / FLOAT / DOUBLE / BOOLEAN in a loaded segment): the values are
+  // grouped and printed by the row scan's TAGNUM mode (exemplar.cpp).  Distributed: agreed on with the glob unions.
+  bool tag_numeric = false;
+  if (tagq)
+    for (size_t i = 0; i < n_paths && !tag_numeric; i++) {
+      if (!segs[i]) continue;
+      const int c = segs[i]->col_index(R.tag_name);
+      tag_numeric = c >= 0 && !segs[i]->cols[size_t(c)].is_string;
+    }
+  if (tag_numeric && !dist) {
+    segs.clear();
+    return evaluate_exemplar(E, *X, R, paths, n_paths, glob_size, flags, false, res, R.tag_name);
+  }
 
   stage("segments");
   // ---- globs ----
@@ -493,7 +506,10 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // be NULL".  Layout: [globs x np exists | globs fail | globs value-type rank | value NULLs].
   const size_t np = probe_cols.size();
   const size_t ng = globs.size();
-  std::vector<uint8_t> exists(ng * np + 2 * ng + 1, 0);
+  // [.. | value NULLs | numeric tag column]
+  std::vector<uint8_t> exists(ng * np + 2 * ng + 2, 0);
+  const size_t vnull_at = ng * np + 2 * ng;
+  exists[vnull_at + 1] = tag_numeric ? 1 : 0;
   // A referenced column this engine does not decode (Segment::unloaded) fails the call with LK_ERR_UNSUPPORTED: DuckDB
   // would read it, so the shim must fall back rather than see an empty glob.  Rank-local (it depends on
   // this rank's segments): agreed on with the load status below.
@@ -520,7 +536,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         }
       int vc = S.col_index(vcol);
       // a NULL value anywhere (or no value column): a glob cell may hold only NULLs and read back 0.0
-      if (vc < 0 || S.cols[vc].any_nulls) exists.back() = 1;
+      if (vc < 0 || S.cols[vc].any_nulls) exists[vnull_at] = 1;
       // Column types per role.  read_parquet(union_by_name=True) (Commons.scala:213) unifies each column's type
       // over the glob's files; a column the query cannot bind (the value column as text, a string filter /
       // groupBy column stored as a number, a numeric comparison on text, INT96 / FIXED_LEN_BYTE_ARRAY, which the
@@ -556,7 +572,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     }
   // every rank sees every glob's union, failures and value type; a rank-local engine failure fails every rank here
   if (dist) comm_agree_max_u8(E, *X, load_err, load_msg, exists.data(), exists.size());
-  const bool value_nulls = exists.back() != 0;
+  const bool value_nulls = exists[vnull_at] != 0;
+  if (exists[vnull_at + 1])   // agreed: every rank fails alike
+    throw PlanError(LK_ERR_UNSUPPORTED, "distributed tag query over the numeric tag column " + R.tag_name);
   size_t nfailed = 0;
   for (size_t gi = 0; gi < ng; gi++)
     if (gfail[gi]) {

@@ -29,11 +29,15 @@ void collect_leaves(const FilterNode* n, std::vector<const FilterNode*>& out);
 // Truth table of a postfix program over L leaves: bit (T | F << L) = TRUE.
 std::vector<uint32_t> truth_table(const std::vector<uint8_t>& prog, uint32_t L);
 bool null_like(const std::string& s);
+// NoisyTagsDropper: tag names dropped from tag-query rows
+bool noisy_tag(const std::string& t);
 double ms_since(std::chrono::steady_clock::time_point t0);
 
 // Exemplar queries (no chart): exemplar.cpp.
+// numtag: a tag query (isTagQuery) whose tag column is numeric -- the same row scan planning (filter, globs,
+// union_by_name types), counting passing rows per canonical tag value instead of selecting rows (ex_scan TAGNUM).
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
-                      int glob_size, unsigned flags, bool dist, lk_result* res);
+                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag = std::string());
 // Numeric comparison leaves (numleaf.cpp): gt / ge / lt / le; the normalized literal (PlanError(LK_ERR_ARG) where the
 // reference's SQL fails); the leaf's interval on numeric filter column `col`.
 bool numeric_op(const std::string& op);

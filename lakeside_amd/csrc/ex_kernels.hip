@@ -66,6 +66,51 @@ __device__ __forceinline__ uint32_t lanes_below(unsigned long long m) {
   return __builtin_amdgcn_mbcnt_hi(uint32_t(m >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(m), 0u));
 }
 
+// Canonical group key of a tag value (pad: Parquet physical type | glob union type << 8), as DuckDB groups the
+// union_by_name column: integers as BIGINT / INTEGER, FLOAT / DOUBLE unions with every NaN as one value and -0.0 as
+// +0.0, BOOLEAN as 0 / 1.
+__device__ __forceinline__ unsigned long long tag_key(unsigned long long raw, uint32_t pad) {
+  const uint32_t pt = pad & 0xffu, ut = (pad >> 8) & 0xffu;
+  const long long iv = pt == 2u ? (long long)raw : (long long)int32_t(uint32_t(raw));
+  if (ut == 2u || ut == 1u) return (unsigned long long)iv;
+  if (ut == 0u) return raw & 1ull;
+  if (ut == 4u) {
+    float f = pt == 4u ? __uint_as_float(uint32_t(raw)) : float(iv);
+    if (f != f) return 0x7fc00000ull;
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x7fffffffu) == 0u ? 0ull : (unsigned long long)b;
+  }
+  const double d = pt == 5u ? __longlong_as_double((long long)raw) : (pt == 4u ? double(__uint_as_float(uint32_t(raw))) : double(iv));
+  if (d != d) return 0x7ff8000000000000ull;
+  const unsigned long long b = (unsigned long long)__double_as_longlong(d);
+  return (b & 0x7fffffffffffffffull) == 0ull ? 0ull : b;
+}
+
+__device__ __forceinline__ unsigned long long tag_hash(unsigned long long k) {
+  k ^= k >> 33;
+  k *= 0xff51afd7ed558ccdull;
+  k ^= k >> 33;
+  k *= 0xc4ceb9fe1a85ec53ull;
+  k ^= k >> 33;
+  return k;
+}
+
+// (key, c) into glob g's device table (linear probing; a table without room sets FLAG_HASH_FULL: the host regrows)
+__device__ void tag_global_add(const XParams& X, uint32_t g, unsigned long long k, unsigned long long c) {
+  const unsigned long long mask = X.tcap - 1, base = (unsigned long long)g * X.tcap;
+  unsigned long long s = tag_hash(k) & mask;
+  for (unsigned long long i = 0; i <= mask && i < 4096; i++, s = (s + 1) & mask) {
+    const unsigned long long prev = atomicCAS(X.tkeys + base + s, TAG_EMPTY, k);
+    if (prev == TAG_EMPTY || prev == k) {
+      atomicAdd(X.tcnt + base + s, c);
+      return;
+    }
+  }
+  atomicOr(X.tflags, FLAG_HASH_FULL);
+}
+
+constexpr uint32_t TAG_LDS_SLOTS = 512;   // per workgroup (aliases the HIST bins)
+
 }  // namespace
 
 template <int AGG, bool HASH>
@@ -80,7 +125,7 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
   __shared__ LRun dr[MAXQCOL][RUN_CAP];
   __shared__ uint32_t truth[(1u << (2 * TT_MAX_LEAVES)) / 32];
   __shared__ uint32_t wsum[MAXQCOL][BLOCK / 64];
-  __shared__ uint32_t hist[XBINS];
+  __shared__ __attribute__((aligned(16))) uint32_t hist[XBINS];   // HIST bins, or the TAGNUM table (64-bit keys)
 
   const QSeg* Sp = X.segs + blockIdx.y;
   const uint32_t t = blockIdx.x;
@@ -121,6 +166,16 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
     for (uint32_t i = tid; i < ((1u << (2 * X.nleaves)) + 31) / 32; i += BLOCK) truth[i] = X.truth[i];
   if (X.mode == XMODE_HIST)
     for (uint32_t i = tid; i < X.nbins; i += BLOCK) hist[i] = 0;
+  // TAGNUM: the workgroup's table in the bins' LDS: [512 keys (u64) | 512 counts | NULL rows | all-ones-key rows]
+  unsigned long long* tk = reinterpret_cast<unsigned long long*>(hist);
+  uint32_t* tc = hist + 2 * TAG_LDS_SLOTS;
+  if (X.mode == XMODE_TAGNUM) {
+    for (uint32_t i = tid; i < TAG_LDS_SLOTS; i += BLOCK) {
+      tk[i] = TAG_EMPTY;
+      tc[i] = 0;
+    }
+    if (tid < 2) tc[TAG_LDS_SLOTS + tid] = 0;
+  }
   __syncthreads();
   for (int qc = 0; qc < nc; qc++) {
     if (!H[qc].present) continue;
@@ -148,7 +203,8 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
     const uint32_t r = c0 + uint32_t(tid);
     const bool inb = r < nrows;
     uint32_t T = 0, F = 0;
-    bool ts_ok = false, v_ok = false;
+    bool ts_ok = false, v_ok = false, tag_ok = false;
+    unsigned long long tag_raw = 0;
     int64_t ts = 0;
     double v = 0.0;
     unsigned long long gid = 0;
@@ -180,14 +236,21 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
       }
       if (qc < 2 || qc >= 2 + ns) {   // PLAIN numeric: timestamp, value, numeric filter column
         const bool w8 = h.kind == PAGE_PLAIN64;
-        if (!w8 && h.kind != PAGE_PLAIN32) ok = false;
+        const bool bl = h.kind == PAGE_BOOL && uint32_t(qc) == X.tag_qc;   // BOOLEAN: a numeric tag only
+        if (!w8 && h.kind != PAGE_PLAIN32 && !bl) ok = false;
         const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len);
         uint64_t raw = 0;
         if (w8) {
           const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? vi * 8u : OOB, 0, 0);
           raw = (uint64_t(w.y) << 32) | w.x;
+        } else if (bl) {
+          raw = (__builtin_amdgcn_raw_buffer_load_b32(rs, ok ? (vi >> 5) * 4u : OOB, 0, 0) >> (vi & 31u)) & 1u;
         } else {
           raw = __builtin_amdgcn_raw_buffer_load_b32(rs, ok ? vi * 4u : OOB, 0, 0);
+        }
+        if (uint32_t(qc) == X.tag_qc) {
+          tag_raw = raw;
+          tag_ok = ok;
         }
         if (qc == 0) {   // BIGINT over INT64 / INT32 files (union_by_name)
           ts = w8 ? int64_t(raw) : int64_t(int32_t(uint32_t(raw)));
@@ -213,6 +276,11 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
           for (uint32_t k = 0; k < X.nnl; k++) {
             const NumLeaf& L = X.nl[k];
             if (int(L.col) != qc - 2 - ns) continue;
+            if (L.pad & NUMLEAF_NOTNULL) {   // IS NOT NULL: never UNKNOWN
+              T |= uint32_t(ok) << L.leaf;
+              F |= uint32_t(!ok) << L.leaf;
+              continue;
+            }
             if (!ok) continue;   // NULL: UNKNOWN
             bool pass;
             const double x = is_int ? double(iv) : dv;   // integers vs a DOUBLE (scientific) literal: cast first
@@ -291,6 +359,37 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
           }
         }
       }
+    } else if (X.mode == XMODE_TAGNUM) {
+      // every passing row of the glob window: NULL tags and the all-ones key counted apart; the other keys deduplicated
+      // across the wave (one leader per distinct key) and added into the workgroup's LDS table
+      const int cls = !pass ? 0 : (!tag_ok ? 2 : 1);
+      const unsigned long long key = cls == 1 ? tag_key(tag_raw, Sp->cols[X.tag_qc].pad) : 0ull;
+      const int cl2 = (cls == 1 && key == TAG_EMPTY) ? 3 : cls;
+      const unsigned long long mn = __ballot(cl2 == 2), mo = __ballot(cl2 == 3);
+      if (lane == 0 && mn) atomicAdd(&tc[TAG_LDS_SLOTS], uint32_t(__popcll(mn)));
+      if (lane == 0 && mo) atomicAdd(&tc[TAG_LDS_SLOTS + 1], uint32_t(__popcll(mo)));
+      unsigned long long act = __ballot(cl2 == 1);
+      while (act) {
+        const int leader = __ffsll((long long)act) - 1;
+        const uint32_t lo32 = __shfl(uint32_t(key), leader), hi32 = __shfl(uint32_t(key >> 32), leader);
+        const unsigned long long lk = (unsigned long long)hi32 << 32 | lo32;
+        const unsigned long long m = __ballot(cl2 == 1 && key == lk);
+        if (lane == leader) {
+          const uint32_t c = uint32_t(__popcll(m));
+          uint32_t s = uint32_t(tag_hash(lk)) & (TAG_LDS_SLOTS - 1);
+          bool done = false;
+          for (uint32_t i = 0; i < TAG_LDS_SLOTS; i++, s = (s + 1) & (TAG_LDS_SLOTS - 1)) {
+            const unsigned long long prev = atomicCAS(&tk[s], TAG_EMPTY, lk);
+            if (prev == TAG_EMPTY || prev == lk) {
+              atomicAdd(&tc[s], c);
+              done = true;
+              break;
+            }
+          }
+          if (!done) tag_global_add(X, g, lk, c);   // the workgroup's table is full
+        }
+        act &= ~m;
+      }
     } else if (X.mode == XMODE_HIST) {
       if (pass) {
         int64_t b = (ts - hbase) / hwidth;
@@ -315,6 +414,31 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
     for (uint32_t i = tid; i < X.nbins; i += BLOCK)
       if (hist[i]) atomicAdd(&X.hist[size_t(g) * X.nbins + i], hist[i]);
   }
+  if (X.mode == XMODE_TAGNUM) {   // flush: one device atomic per distinct key of the tile
+    __syncthreads();
+    for (uint32_t i = tid; i < TAG_LDS_SLOTS; i += BLOCK)
+      if (tk[i] != TAG_EMPTY) tag_global_add(X, g, tk[i], tc[i]);
+    if (tid < 2 && tc[TAG_LDS_SLOTS + tid]) atomicAdd(X.tspec + 2 * size_t(g) + tid, (unsigned long long)tc[TAG_LDS_SLOTS + tid]);
+  }
+}
+
+__global__ __launch_bounds__(256) void tag_compact(const unsigned long long* keys, const unsigned long long* cnt,
+                                                   unsigned long long n, unsigned long long tcap,
+                                                   unsigned long long* out, uint32_t* out_n) {
+  const unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n || keys[i] == TAG_EMPTY) return;
+  const uint32_t o = atomicAdd(out_n, 1u);
+  out[3 * size_t(o)] = keys[i];
+  out[3 * size_t(o) + 1] = cnt[i];
+  out[3 * size_t(o) + 2] = i / tcap;
+}
+
+hipError_t launch_tag_compact(const unsigned long long* keys, const unsigned long long* cnt, unsigned long long tcap,
+                              uint32_t nglobs, unsigned long long* out, uint32_t* out_n, hipStream_t stream) {
+  const unsigned long long n = tcap * nglobs;
+  if (!n) return hipSuccess;
+  hipLaunchKernelGGL(tag_compact, dim3(uint32_t((n + 255) / 256)), dim3(256), 0, stream, keys, cnt, n, tcap, out, out_n);
+  return hipGetLastError();
 }
 
 namespace {

@@ -160,13 +160,15 @@ struct PinnedTmp {
 }  // namespace
 
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
-                      int glob_size, unsigned flags, bool dist, lk_result* res) {
+                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag) {
   const auto t_start = std::chrono::steady_clock::now();
-  if (dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed exemplar queries (each worker streams its own rows)");
+  const bool tagnum = !numtag.empty();
+  if (dist) throw PlanError(LK_ERR_UNSUPPORTED, tagnum ? "distributed tag queries over a numeric tag column"
+                                                       : "distributed exemplar queries (each worker streams its own rows)");
   if (R.has_extract || R.has_compute)
     throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute exemplar queries are not on the hot path");
   const bool logs = R.dataset == "logs";
-  if (!logs && R.dataset != "traces") {
+  if (!tagnum && !logs && R.dataset != "traces") {
     // metrics: the projection's second column is "_cardinalhq.name" (BaseExpr.scala:41); getDouble of a metric
     // name fails the stream, which query-api turns into an empty source (QueryEngineV2.scala:141-145)
     if (R.dataset == "metrics") throw PlanError(LK_ERR_ARG, "metrics exemplar: getDouble of \"_cardinalhq.name\"");
@@ -174,18 +176,24 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   }
   std::string order = R.order;
   for (auto& c : order) c = char(toupper(static_cast<unsigned char>(c)));
+  if (tagnum) order = "DESC";   // (a tag query has no ORDER BY / LIMIT)
   if (order != "DESC" && order != "ASC") throw PlanError(LK_ERR_ARG, "ORDER BY direction '" + R.order + "'");
-  if (R.limit < 0) throw PlanError(LK_ERR_ARG, "negative LIMIT");
+  if (R.limit < 0 && !tagnum) throw PlanError(LK_ERR_ARG, "negative LIMIT");
   const bool desc = order == "DESC";
-  const uint64_t limit = uint64_t(R.limit);
+  const uint64_t limit = tagnum ? 0 : uint64_t(R.limit);
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
 
   std::vector<const FilterNode*> all_leaves;
   collect_leaves(R.filter.get(), all_leaves);
   std::vector<std::string> nums;   // numeric comparison columns (gt/ge/lt/le, BaseExpr.scala:488-498)
+  // numeric tag: its leaves (query-api's `exists` on the tag) are numeric IS NOT NULL leaves; the tag column is a
+  // numeric column of the scan either way
+  auto num_col = [&](const FilterNode* l) { return numeric_op(l->op) || (tagnum && l->k == numtag); };
   for (auto* l : all_leaves) {
     if (l->extracted || l->computed) throw PlanError(LK_ERR_UNSUPPORTED, "extracted/computed filter fields");
-    if (numeric_op(l->op)) {
+    if (tagnum && l->k == numtag && !numeric_op(l->op) && l->op != "exists" && l->op != "has")
+      throw PlanError(LK_ERR_UNSUPPORTED, "string comparison '" + l->op + "' on the numeric tag column " + numtag);
+    if (num_col(l)) {
       if (std::find(nums.begin(), nums.end(), l->k) == nums.end()) nums.push_back(l->k);
       continue;
     }
@@ -193,6 +201,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     if (std::none_of(std::begin(ok), std::end(ok), [&](const char* o) { return l->op == o; }))
       throw PlanError(LK_ERR_ARG, "Invalid operator " + l->op);
   }
+  if (tagnum && std::find(nums.begin(), nums.end(), numtag) == nums.end()) nums.push_back(numtag);
   res->exemplar = true;
   res->per_glob = true;
   if (R.segments.empty()) {   // Commons.scala:393-396: the sentinel DataPoint(-1, -1, {})
@@ -215,7 +224,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   };
   std::vector<XStr> strs;
   for (auto* l : all_leaves) {
-    if (numeric_op(l->op)) continue;
+    if (num_col(l)) continue;
     auto it = std::find_if(strs.begin(), strs.end(), [&](const XStr& s) { return s.name == l->k; });
     if (it == strs.end()) {
       strs.push_back(XStr{});
@@ -245,11 +254,20 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   std::vector<NumLeaf> nleaves;
   std::vector<std::string> bad_literal;   // fields whose numeric literal fails the SQL (per glob where they exist)
   for (auto* l : all_leaves)
-    if (numeric_op(l->op)) {
+    if (num_col(l)) {
       const uint32_t idx = uint32_t(leaves.size());
       leaves.push_back(LeafInfo{l, -1, int(idx)});
+      const uint32_t col = uint32_t(std::find(nums.begin(), nums.end(), l->k) - nums.begin());
+      if (!numeric_op(l->op)) {   // IS NOT NULL on the numeric tag (BaseExpr: "<tag>" IS NOT NULL)
+        NumLeaf nl{};
+        nl.col = col;
+        nl.leaf = idx;
+        nl.pad = NUMLEAF_NOTNULL;
+        nleaves.push_back(nl);
+        continue;
+      }
       bool bad = false;
-      nleaves.push_back(make_num_leaf(*l, uint32_t(std::find(nums.begin(), nums.end(), l->k) - nums.begin()), idx, bad));
+      nleaves.push_back(make_num_leaf(*l, col, idx, bad));
       if (bad) bad_literal.push_back(l->k);
     }
   std::vector<uint8_t> prog;
@@ -270,8 +288,9 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
     }
   }
   if (glob_size <= 0) glob_size = 10;
-  const std::vector<std::string> proj = logs ? std::vector<std::string>{kTimestamp, kValue, kName, kMessage}
-                                             : std::vector<std::string>{kTimestamp, kValue, kSpanName, kSpanKind};
+  const std::vector<std::string> proj = tagnum ? std::vector<std::string>{kTimestamp, numtag}
+                                       : logs ? std::vector<std::string>{kTimestamp, kValue, kName, kMessage}
+                                              : std::vector<std::string>{kTimestamp, kValue, kSpanName, kSpanKind};
   const std::set<std::string> fset = field_set(R);
   std::vector<XGlob> globs;
   for (size_t i = 0; i < n_paths; i += size_t(glob_size)) {
@@ -302,6 +321,8 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       if (!(g.leaf_false >> l.index & 1u) && !g.types.count(l.node->k)) g.skip = true;
     for (auto& k : bad_literal)   // normalizedValue failed for a field this glob has
       if (!(fset.count(k) && !g.types.count(k))) g.skip = true;
+    if (tagnum && g.types.count(numtag) && g.types[numtag] == pq::BYTE_ARRAY)   // VARCHAR in a glob of numbers
+      throw PlanError(LK_ERR_UNSUPPORTED, "tag column " + numtag + " is text in some files and numeric in others");
     for (auto& nm : nums)   // a VARCHAR compared with a number: Binder Error -> empty glob
       if (g.types.count(nm) && g.types[nm] == pq::BYTE_ARRAY) g.skip = true;
     g.cols = proj;
@@ -371,7 +392,7 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   }
   for (size_t gi = 0; gi < globs.size(); gi++) {
     XGlob& g = globs[gi];
-    if (g.skip || g.win_lo >= g.win_hi || limit == 0) continue;
+    if (g.skip || g.win_lo >= g.win_hi || (limit == 0 && !tagnum)) continue;
     // the glob's descriptors go in together: a column its query cannot bind empties the glob (Binder Error,
     // Commons.scala:249-253), the other globs are unaffected
     const size_t mark = qsegs.size();
@@ -396,10 +417,13 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
           throw PlanError(LK_ERR_UNSUPPORTED, "column " + name + " has an unexpected type for its role");
         if (qc == 0 && hc.ptype != pq::INT64 && hc.ptype != pq::INT32)
           throw PlanError(LK_ERR_UNSUPPORTED, "timestamp column must be INT64 or INT32");
+        const bool is_tag = tagnum && name == numtag;
         if (qc >= 2 + int(strs.size()) && hc.ptype != pq::INT64 && hc.ptype != pq::DOUBLE && hc.ptype != pq::INT32 &&
-            hc.ptype != pq::FLOAT)
+            hc.ptype != pq::FLOAT && !(is_tag && hc.ptype == pq::BOOLEAN))
           throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison on column " + name + " of an undecoded type");
-        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, uint32_t(hc.ptype)};
+        uint32_t pad = uint32_t(hc.ptype);
+        if (is_tag) pad |= uint32_t(g.types.count(numtag) ? g.types[numtag] : hc.ptype) << 8;   // the glob's union type
+        q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, pad};
       };
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;
@@ -477,6 +501,168 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   P.hbase = d_rng + 2 * ng;
   P.hwidth = d_rng + 3 * ng;
   P.out_n = reinterpret_cast<uint32_t*>(dbuf + o_n);
+  P.tag_qc = ~0u;
+
+  if (tagnum) {
+    // ---- tag query over a numeric tag: SELECT "<tag>", COUNT(*) ... GROUP BY "<tag>" per glob (BaseExpr.scala:
+    // 127-138): one TAGNUM pass counts passing rows per (glob, canonical tag value); the host prints each value as JDBC
+    // getString does for the glob's union_by_name type (Long / Integer / Double / Float / Boolean .toString) ----
+    const uint32_t tagk = uint32_t(std::find(nums.begin(), nums.end(), numtag) - nums.begin());
+    P.tag_qc = uint32_t(2 + strs.size() + tagk);
+    uint64_t max_rows = 1;
+    for (size_t gi = 0; gi < ng; gi++) {
+      const XGlob& g = globs[gi];
+      const bool live = !g.skip && g.win_lo < g.win_hi;
+      hr[gi] = live ? g.win_lo : 0;
+      hr[ng + gi] = live ? g.win_hi : 0;
+    }
+    {
+      std::vector<uint64_t> grow(ng, 0);
+      for (size_t q = 0; q < qsegs.size(); q++) grow[qseg_glob[q]] += uint64_t(qseg_seg[q]->num_rows);
+      for (uint64_t r : grow) max_rows = std::max(max_rows, r);
+    }
+    auto pow2 = [](uint64_t x) {
+      uint64_t p = 1;
+      while (p < x) p <<= 1;
+      return p;
+    };
+    const uint64_t cap_max = std::max<uint64_t>(1 << 12, pow2(2 * max_rows));
+    uint64_t tcap = std::min<uint64_t>(cap_max, uint64_t(1) << 12);
+    if (const char* e = getenv("LK_TAGNUM_INIT_SLOTS")) tcap = std::min<uint64_t>(cap_max, pow2(std::max<uint64_t>(64, strtoull(e, nullptr, 10))));
+    XHIP_TRY(hipMemcpyAsync(dbuf, hbuf, stage_bytes, hipMemcpyHostToDevice, st));
+    P.mode = XMODE_TAGNUM;
+    float scan_ms = 0.f;
+    int attempts = 0;
+    uint8_t* tb = nullptr;
+    for (;;) {
+      attempts++;
+      const size_t tbytes = ng * tcap * 16 + ng * 16 + 64;
+      tb = static_cast<uint8_t*>(X.workspace("tagnum", tbytes));
+      P.tkeys = reinterpret_cast<unsigned long long*>(tb);
+      P.tcnt = reinterpret_cast<unsigned long long*>(tb + ng * tcap * 8);
+      P.tspec = reinterpret_cast<unsigned long long*>(tb + ng * tcap * 16);
+      P.tflags = reinterpret_cast<uint32_t*>(tb + ng * tcap * 16 + ng * 16);
+      P.tcap = tcap;
+      XHIP_TRY(hipMemsetAsync(tb, 0xff, ng * tcap * 8, st));
+      XHIP_TRY(hipMemsetAsync(tb + ng * tcap * 8, 0, ng * tcap * 8 + ng * 16 + 64, st));
+      XHIP_TRY(hipEventRecord(X.ev_scan0, st));
+      XHIP_TRY(launch_ex_scan(P, st));
+      XHIP_TRY(hipEventRecord(X.ev_scan1, st));
+      uint32_t fl = 0;
+      XHIP_TRY(hipMemcpyAsync(&fl, P.tflags, 4, hipMemcpyDeviceToHost, st));
+      XHIP_TRY(hipStreamSynchronize(st));
+      float ms = 0.f;
+      XHIP_TRY(hipEventElapsedTime(&ms, X.ev_scan0, X.ev_scan1));
+      scan_ms += ms;
+      if (!(fl & FLAG_HASH_FULL)) break;
+      if (tcap >= cap_max) throw PlanError(LK_ERR_MEMORY, "tag value table full at its bound");
+      tcap = std::min(cap_max, tcap * 8);
+    }
+    // occupied slots -> (key, count, glob) records; per-glob NULL / all-ones counts
+    auto* recs = static_cast<unsigned long long*>(X.workspace("tagrecs", ng * tcap * 24 + 64));
+    uint32_t* d_n = reinterpret_cast<uint32_t*>(recs);
+    XHIP_TRY(hipMemsetAsync(d_n, 0, 4, st));
+    XHIP_TRY(launch_tag_compact(P.tkeys, P.tcnt, tcap, uint32_t(ng), recs + 1, d_n, st));
+    uint32_t nrec = 0;
+    std::vector<unsigned long long> spec(ng * 2);
+    XHIP_TRY(hipMemcpyAsync(&nrec, d_n, 4, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipMemcpyAsync(spec.data(), P.tspec, ng * 16, hipMemcpyDeviceToHost, st));
+    XHIP_TRY(hipStreamSynchronize(st));
+    std::vector<unsigned long long> hrec(size_t(nrec) * 3);
+    if (nrec) {
+      XHIP_TRY(hipMemcpyAsync(hrec.data(), recs + 1, size_t(nrec) * 24, hipMemcpyDeviceToHost, st));
+      XHIP_TRY(hipStreamSynchronize(st));
+    }
+    // per glob: (key, count) in the union type's value order, NULL last
+    struct TRow {
+      uint32_t glob;
+      bool null;
+      unsigned long long key;
+      uint64_t count;
+      std::string text;
+    };
+    std::vector<TRow> rows;
+    auto union_of = [&](uint32_t gi) {
+      auto it = globs[gi].types.find(numtag);
+      return it == globs[gi].types.end() ? int(pq::INT64) : it->second;
+    };
+    for (uint32_t i = 0; i < nrec; i++)
+      rows.push_back(TRow{uint32_t(hrec[3 * i + 2]), false, hrec[3 * i], hrec[3 * i + 1], std::string()});
+    for (uint32_t gi = 0; gi < ng; gi++) {
+      if (spec[2 * gi + 1]) rows.push_back(TRow{gi, false, TAG_EMPTY, spec[2 * gi + 1], std::string()});
+      if (spec[2 * gi]) rows.push_back(TRow{gi, true, 0, spec[2 * gi], std::string()});
+    }
+    auto num_of = [&](const TRow& r) -> double {   // value order within a glob
+      const int ut = union_of(r.glob);
+      if (ut == pq::DOUBLE) {
+        double d;
+        memcpy(&d, &r.key, 8);
+        return d;
+      }
+      if (ut == pq::FLOAT) {
+        float f;
+        const uint32_t u = uint32_t(r.key);
+        memcpy(&f, &u, 4);
+        return double(f);
+      }
+      return double(int64_t(r.key));
+    };
+    for (auto& r : rows)
+      if (!r.null) r.text = value_text(r.key, union_of(r.glob), union_of(r.glob));
+    std::sort(rows.begin(), rows.end(), [&](const TRow& a, const TRow& b) {
+      if (a.glob != b.glob) return a.glob < b.glob;
+      if (a.null != b.null) return b.null;
+      if (a.null) return false;
+      const double x = num_of(a), y = num_of(b);
+      if (x != y && x == x && y == y) return x < y;
+      return a.text < b.text;
+    });
+    if (!per_glob_rows) {   // merged: counts summed per tag text (NULL apart), in first-seen order
+      std::vector<TRow> m;
+      std::map<std::pair<bool, std::string>, size_t> at;
+      for (auto& r : rows) {
+        auto k = std::make_pair(r.null, r.text);
+        auto it = at.find(k);
+        if (it == at.end()) {
+          at.emplace(k, m.size());
+          m.push_back(r);
+          m.back().glob = 0;
+        } else {
+          m[it->second].count += r.count;
+        }
+      }
+      rows.swap(m);
+    }
+    // rows: Commons.toDataPoint's tag branch (Commons.scala:406-423): the tag (dropped when NULL / "" / "null" or a
+    // noisy name, NoisyTagsDropper) and "count"; value = the count, timestamp = now (as the string tag path)
+    const int64_t now_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                               std::chrono::system_clock::now().time_since_epoch()).count();
+    const bool hide = noisy_tag(numtag);
+    res->per_glob = per_glob_rows;
+    res->alloc_rows(rows.size());
+    res->tag_names = {numtag, "count"};
+    res->ex_tags.assign(rows.size() * 2, nullptr);
+    for (size_t i = 0; i < rows.size(); i++) {
+      res->ts[i] = now_ms;
+      res->val[i] = double(rows[i].count);
+      res->glob[i] = rows[i].glob;
+      res->gid[i] = uint32_t(i);
+      if (!rows[i].null && !hide && !null_like(rows[i].text)) {
+        res->owned.push_back(rows[i].text);
+        res->ex_tags[2 * i] = res->owned.back().c_str();
+      }
+      res->owned.push_back(std::to_string((unsigned long long)rows[i].count));
+      res->ex_tags[2 * i + 1] = res->owned.back().c_str();
+    }
+    char buf[320];
+    snprintf(buf, sizeof buf,
+             "{\"scan_ms\":%.4f,\"total_ms\":%.4f,\"rows_scanned\":%llu,\"tag_values\":%u,\"attempts\":%d,"
+             "\"slots\":%llu,\"table\":\"tagnum\",\"failed_globs\":%zu}",
+             double(scan_ms), ms_since(t_start), (unsigned long long)rows_scanned, nrec, attempts,
+             (unsigned long long)tcap, size_t(std::count_if(globs.begin(), globs.end(), [](const XGlob& g) { return g.skip; })));
+    res->stats = buf;
+    return LK_OK;
+  }
 
   // ---- HIST passes: narrow every glob to the rows that can make its top `limit` ----
   // rows listed beyond each glob's `limit` at most, unless tied on one millisecond (tests shrink it with

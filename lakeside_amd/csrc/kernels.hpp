@@ -111,7 +111,13 @@ hipError_t launch_sparse_write(const SParams& S, unsigned long long n, void* ws,
 // every tile meeting its glob's open range [rlo, rhi) and either counts passing rows per time bin (HIST) or appends
 // them as (timestamp, segment << 48 | tile << 16 | row) records (EMIT).
 constexpr uint32_t XBINS = 2048;
-enum XMode : uint32_t { XMODE_HIST = 0, XMODE_EMIT = 1, XMODE_AGG = 2 };
+enum XMode : uint32_t { XMODE_HIST = 0, XMODE_EMIT = 1, XMODE_AGG = 2, XMODE_TAGNUM = 3 };
+// XMODE_TAGNUM (tag queries over a numeric tag column): passing rows counted per (glob, canonical tag value) in a
+// per-glob open-addressing table (wave dedup -> LDS table -> device atomics); NULL tags and the one value whose
+// canonical key is the empty marker (all ones) are counted apart.  NumLeaf.pad bit 1 (NUMLEAF_NOTNULL): the leaf is
+// `IS NOT NULL` on that column (query-api's `exists` on the tag).
+constexpr uint32_t NUMLEAF_NOTNULL = 2u;
+constexpr unsigned long long TAG_EMPTY = ~0ull;
 // A numeric comparison leaf (`gt/ge/lt/le`, BaseExpr.scala:488-498) on numeric filter column `col` (QSeg column
 // 2 + nstr + col, its Parquet physical type in QCol.pad): TRUE iff the value lies in the interval, FALSE otherwise,
 // UNKNOWN on NULL.  Integer columns test [ilo, ihi] (exact); floating columns the double interval, NaN (ordered
@@ -151,7 +157,18 @@ struct XParams {
   int agg;                         // Agg (kernel aggregate)
   int hash;                        // q's table is the hash-mode table
   QParams q;
+  // TAGNUM: the tag's query column (its QCol.pad: Parquet type | glob union type << 8), per-glob tables of tcap slots
+  // (keys TAG_EMPTY-initialised, 64-bit counts), per-glob [NULL rows, all-ones-key rows], overflow flag
+  uint32_t tag_qc;
+  unsigned long long tcap;
+  unsigned long long* tkeys;
+  unsigned long long* tcnt;
+  unsigned long long* tspec;
+  uint32_t* tflags;
 };
+// TAGNUM tables -> records [key, count, glob] of the occupied slots (unordered); count at *out_n.
+hipError_t launch_tag_compact(const unsigned long long* keys, const unsigned long long* cnt, unsigned long long tcap,
+                              uint32_t nglobs, unsigned long long* out, uint32_t* out_n, hipStream_t stream);
 hipError_t launch_ex_scan(const XParams& X, hipStream_t stream);
 
 struct GCol {                      // one (segment, output column) of an exemplar gather

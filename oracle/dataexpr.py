@@ -284,9 +284,47 @@ class _Col:
         self.dictionary = dictionary
 
 
-def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[str], sources=None):
+def _tag_kind(typ) -> str:
+    import pyarrow as pa
+    if pa.types.is_dictionary(typ):
+        typ = typ.value_type
+    if pa.types.is_boolean(typ):
+        return "bool"
+    if pa.types.is_integer(typ):
+        return "int"
+    if pa.types.is_float32(typ):
+        return "float32"
+    if pa.types.is_floating(typ):
+        return "float64"
+    return "text"
+
+
+def numeric_tag_text(kinds: set, v) -> Optional[str]:
+    """JDBC getString of a numeric tag value read as the glob's union_by_name type (Commons.scala:406-423 via
+    DuckDBResultSet.getString = getObject(i).toString()): BIGINT / INTEGER -> Long / Integer.toString, FLOAT ->
+    Float.toString (integers of a FLOAT union cast to FLOAT first), DOUBLE -> Double.toString, BOOLEAN ->
+    Boolean.toString.  Grouping is by value: every NaN is one group and -0.0 groups (and prints) as 0.0 (this
+    repo's choice; DuckDB's representative of the 0.0 / -0.0 group is not pinned)."""
+    from oracle.exemplar import java_double_text, java_float_text
+    if v is None:
+        return None
+    if kinds == {"bool"}:
+        return "true" if v else "false"
+    if kinds <= {"int"}:
+        return str(int(v))
+    if "float64" in kinds:
+        x = float(v)
+        return "NaN" if x != x else java_double_text(0.0 if x == 0 else x)
+    x = float(np.float32(v))
+    return "NaN" if x != x else java_float_text(0.0 if x == 0 else x)
+
+
+def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[str], sources=None,
+               numeric_tags: Sequence[str] = ()):
     """union_by_name=True read of the glob (Commons.scala:210-213): a column missing from a file is NULL
-    for that file's rows.  Returns (union column names, numeric arrays + validity, string columns)."""
+    for that file's rows.  Returns (union column names, numeric arrays + validity, string columns).
+    `numeric_tags`: string-role columns (a tag query's tag) that may be numeric: their values become the JDBC
+    getString text of the glob's union type (numeric_tag_text) before they are coded."""
     import pyarrow as pa
     import pyarrow.parquet as pq
     union: List[str] = []
@@ -300,6 +338,20 @@ def _read_glob(paths: Sequence[str], numeric: Sequence[str], strings: Sequence[s
                 union.append(n)
         want = [c for c in list(numeric) + list(strings) if c in names]
         tables.append((pf.read(columns=want, use_threads=True), pf.metadata.num_rows))
+    for c in numeric_tags:
+        kinds = {_tag_kind(t.schema.field(c).type) for t, _ in tables if c in t.column_names}
+        if not kinds or kinds == {"text"}:
+            continue
+        if "text" in kinds or ("bool" in kinds and kinds != {"bool"}):
+            raise NotImplementedError(f"tag column {c}: union of {sorted(kinds)} (VARCHAR / BOOLEAN with numbers)")
+        conv = []
+        for t, n in tables:
+            if c in t.column_names:
+                vals = t.column(c).to_pylist()
+                col = pa.array([numeric_tag_text(kinds, v) for v in vals], pa.string())
+                t = t.set_column(t.column_names.index(c), c, col)
+            conv.append((t, n))
+        tables = conv
     nums = {}
     for c in numeric:
         # union_by_name type of the column over the glob's files (DuckDB's common supertype, INTEGER < BIGINT <
@@ -870,8 +922,10 @@ def evaluate_tag_glob(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], pat
     numcols = sorted({l.k for l in _leaves(be.filter) if l.op in NUMERIC_OPS})
     strings = sorted((set(_leaf_columns(be.filter)) - set(numcols)) | {tag})
     try:
-        union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources)
+        union, nums, strs = _read_glob(paths, [TIMESTAMP], strings, sources, numeric_tags=[tag])
         strs.update(_read_numeric(paths, [c for c in numcols if c in union], sources))
+    except NotImplementedError:
+        raise
     except Exception:   # Commons.scala:249-253: the glob's query fails -> empty
         return []
     nonexistent = fs - set(union)

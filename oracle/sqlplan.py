@@ -146,6 +146,20 @@ def run_tag_sql(pr: PushDownRequest, tag: str, seg_idx: Sequence[int], paths: Se
         return []
     out = [(v, int(c)) for v, c in con.execute(sql).fetchall()]
     con.close()
+    # a numeric tag column: SQLite groups the values; the row's tag is JDBC getString of the glob's union type
+    import pyarrow.parquet as pq
+    from oracle.dataexpr import _tag_kind, numeric_tag_text
+    kinds = set()
+    for p in paths:
+        sch = pq.read_schema(p)
+        if tag in sch.names:
+            kinds.add(_tag_kind(sch.field(tag).type))
+    if kinds and "text" not in kinds:
+        acc = {}
+        for v, c in out:
+            k = numeric_tag_text(kinds, v)
+            acc[k] = acc.get(k, 0) + c
+        out = list(acc.items())
     out.sort(key=lambda r: (r[0] is not None, r[0] or ""))
     return out
 

@@ -404,6 +404,20 @@ def _worker_fault(rank, world, port):
             if rank == 0:
                 assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"after fault {stage} {env}")
             print(f"rank {rank}: {stage} {env} ok", flush=True)
+        # a tag query over a numeric tag column is refused alike on every rank (the decision is agreed), and the
+        # communicator stays usable
+        with open(os.path.join(GOLDEN, "numtag_cases.json")) as f:
+            nt = json.load(f)[0]
+        ntp = [os.path.join(GOLDEN, p) for p in nt["segments"]]
+        from lakeside_amd._lib import LK_ERR_UNSUPPORTED
+        try:
+            eng.eval_pushdown_dist(json.dumps(nt["request"]), ntp, None, nt["glob_size"])
+            raise AssertionError("numeric tag query accepted by the distributed path")
+        except LakesideError as e:
+            assert e.code == LK_ERR_UNSUPPORTED, str(e)
+        res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
+        if rank == 0:
+            assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, "after numeric tag refusal")
         dist.barrier()
     finally:
         for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS", "LK_FAULT"):

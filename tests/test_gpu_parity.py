@@ -61,8 +61,11 @@ def test_golden_merged(golden_engine, case):
 
 
 def _tag_cases():
-    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
-        return json.load(f)
+    out = []
+    for fn in ("tag_cases.json", "numtag_cases.json"):   # string tags; numeric tags (make_numtag_cases.py)
+        with open(os.path.join(GOLDEN, fn)) as f:
+            out += json.load(f)
+    return out
 
 
 def _tag_key(t):
@@ -72,7 +75,9 @@ def _tag_key(t):
 @pytest.mark.parametrize("case", _tag_cases(), ids=lambda c: c["name"])
 def test_golden_tag_query(golden_engine, case):
     """Tag queries (isTagQuery + tagDataType; BaseExpr.scala:127-143): per-glob rows {tag, count} and merged
-    counts equal the golden rows (oracle pinned by the reference's tag SQL on SQLite)."""
+    counts equal the golden rows (oracle pinned by the reference's tag SQL on SQLite).  Numeric tag columns
+    (numtag_cases.json: INT64 / INT32 / DOUBLE / FLOAT / BOOLEAN and their union_by_name unions) print as JDBC
+    getString of the glob's union type (ex_scan TAGNUM)."""
     from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
     paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
     for p in paths:
@@ -493,3 +498,34 @@ def test_regex_non_ascii_dictionary_values(engine, tmp_path):
         got = engine.eval_pushdown(req, [path], 10, LK_MERGED)
         want = dx.evaluate_merged(dx.parse_pushdown(req), [path], 10)
         assert_rows_equal(got.rows(), want, "count", f"{op} {pat}")
+
+
+def test_numeric_tag_high_cardinality_regrowth(engine):
+    """A tag query over a DOUBLE column whose values are nearly all distinct (the value column itself): workgroup
+    LDS tables overflow to the device table, which starts at 64 slots (LK_TAGNUM_INIT_SLOTS) and is regrown; every
+    (value text, count) equals the oracle's."""
+    from lakeside_amd import LK_MERGED, synth
+    from oracle import dataexpr as dx
+    blobs, keys = [], []
+    for i in range(2):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 16, rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        engine.put_segment_ptr(f"numtag_hc/{i}", s.ptr, s.size)
+        s.free()
+        keys.append(f"numtag_hc/{i}")
+    tag = dx.VALUE
+    req = {"baseExpr": {"id": "A", "dataset": "logs", "limit": 1000, "order": "DESC", "returnResults": True,
+                        "filter": {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"),
+                                   "q2": synth.leaf(tag, "exists")}},
+           "segmentRequests": [synth.segment_request(i) for i in range(2)], "reverseSort": False,
+           "isTagQuery": True, "tagDataType": {"tagName": tag, "dataType": "number"}}
+    text = json.dumps(req)
+    os.environ["LK_TAGNUM_INIT_SLOTS"] = "64"
+    try:
+        res = engine.eval_pushdown(text, keys, 10, LK_MERGED)
+    finally:
+        os.environ.pop("LK_TAGNUM_INIT_SLOTS")
+    assert res.stats["attempts"] > 1 and res.stats["table"] == "tagnum", res.stats
+    want = dx.evaluate_tag_merged(dx.parse_pushdown(text), tag, keys, 10, sources=blobs)
+    assert len(want) > 1000
+    assert sorted(res.tags, key=_tag_key) == sorted(want, key=_tag_key)

@@ -96,8 +96,11 @@ def test_binary_clause_folds_left_in_json_order():
 
 
 def _tag_cases():
-    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
-        return json.load(f)
+    out = []
+    for fn in ("tag_cases.json", "numtag_cases.json"):   # string tags; numeric tags (make_numtag_cases.py)
+        with open(os.path.join(GOLDEN, fn)) as f:
+            out += json.load(f)
+    return out
 
 
 @pytest.mark.parametrize("case", _tag_cases(), ids=lambda c: c["name"])
