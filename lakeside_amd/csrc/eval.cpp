@@ -1142,6 +1142,14 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   // scan_tiles
   const bool lean_shape = P.nstr == 1 || (P.nstr <= 3 && P.late_mask == ((1u << P.nstr) - 2u));
   P.rows_only = tagq ? 1u : 0u;   // COUNT(*): no value column is bound (lean tiles need none)
+  // late columns decoded per chunk (scan_lean<..., EARLY>) where a late filter leaf exists: the late filter then runs
+  // before the rows are listed, and a listed row waits only on its value (env LK_NO_LATE_CHUNK: A/B only)
+  {
+    bool late_leaves = false;
+    for (size_t s = 0; s < strs.size(); s++)
+      if (((late_mask >> dev_of[s]) & 1u) && !strs[s].leaves.empty()) late_leaves = true;
+    P.late_chunk = (late_leaves && ngroups <= 65536u && !getenv("LK_NO_LATE_CHUNK")) ? 1u : 0u;
+  }
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric) P.lean = 0;   // the general row scan accumulates every table field

@@ -178,6 +178,8 @@ struct QParams {
   uint32_t dir_planes;
   uint32_t dir_rep;                  // replicas per direct-table cell (1, 2 or 4)
   uint32_t rows_only;                // COUNT(*) (tag queries): no value column bound; lean tiles take none
+  uint32_t late_chunk;               // scan_lean NL > 0: late columns decoded per 16-row chunk in the main loop (the
+                                     // list then carries each row's group term; lean_kernel.hpp)
 };
 // scan_lean's direct table: LDS words by late-column count NL (the hash table's 8 KB for NL >= 1, so the kernels keep
 // their occupancy), at most LEAN_DIR_MAXSPAN buckets

@@ -43,6 +43,8 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #define LEAN_WAVES(NL) ((NL) <= 1 ? 5 : LK_LEAN_WAVES2)   // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
+// the per-wave list is a ring indexed with & (LEAN_LIST - 1) and drained LEAN_TRIP rows at a time
+static_assert((LEAN_LIST & (LEAN_LIST - 1u)) == 0u && LEAN_TRIP <= LEAN_LIST, "LK_LEAN_LIST / LK_LEAN_ROWS");
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 
@@ -147,8 +149,10 @@ __device__ __forceinline__ void lean_rep(uint32_t v, uint32_t& w0, uint32_t& w1,
   w2 = w[2];
 }
 
-template <int AGG, bool HASH, int NL>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVES(NL)))) void scan_lean(QParams P) {
+// EARLY (NL > 0, a late filter leaf: P.late_chunk): tiles that allow it decode the late columns per chunk (early_late
+// below); its own kernel, built for 4 waves per SIMD, so the other shapes keep their occupancy.
+template <int AGG, bool HASH, int NL, bool EARLY = false>
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4 : LEAN_WAVES(NL)))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
   __shared__ LT L;
   const int tid = threadIdx.x;
@@ -388,6 +392,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
   bool late_trivial = true;   // no filter leaf on a late column: the late stage only adds group terms (uniform)
 #pragma unroll
   for (int k = 0; k < NL; k++) late_trivial = late_trivial && P.strp[1 + k].lmask == 0u;
+  // Late columns decoded per chunk (uniform): every present late column has its lookup values in LDS and <= 7-bit
+  // codes (16 codes + the window's bit offset fit one 20-B load), and the group space fits the list entry's high 16
+  // bits.  The chunk's late codes are then loaded one round ahead with its name codes, the late filter runs before
+  // the list, and a listed row waits only on its value gather -- one memory round trip per trip instead of two.
+  bool early_late = false;
+  if constexpr (NL > 0 && EARLY) {
+    early_late = P.ngroups <= 65536u;
+#pragma unroll
+    for (int k = 0; k < NL; k++)
+      if ((lpres >> k) & 1u) early_late = early_late && ((llut_on >> k) & 1u) && lbw[k] <= 7u;
+  }
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
@@ -471,8 +486,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
 
   // N rows per lane (rr[u] live when aa[u]) with group terms dd[u]: late columns (run lookup + packed word, all N
   // rows' loads in flight together), late filter, timestamp / value gather, accumulate
-  auto rowsN = [&](auto ncst, const uint32_t* rr, const bool* aa, uint32_t* dd) __attribute__((always_inline)) {
+  auto rowsN = [&](auto ncst, auto ldc, const uint32_t* rr, const bool* aa, uint32_t* dd) __attribute__((always_inline)) {
     constexpr int N = decltype(ncst)::value;
+    constexpr bool LATE_DONE = decltype(ldc)::value;   // late columns decoded already (dd complete): values only
     bool p[N];
     v2u tt[N], xx[N];
 #pragma unroll
@@ -487,7 +503,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
         if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, p[u] ? (vb1 + rr[u]) * 8u : OOB, 0, 0);
       }
     };
-    if constexpr (NL > 0) {
+    if constexpr (NL > 0 && !LATE_DONE) {
       // with no late filter leaf every row passes, so the timestamp / value loads go out with the late-column loads
       v2u lw[N][LT::NLA];
       uint32_t lm[N][LT::NLA];
@@ -584,7 +600,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
   // all their value loads in flight together -- is ready, across the tile's rounds; the rest drains at the tile's end.
   uint32_t lhead = 0, ltail = 0;   // wave-uniform list positions (mod LEAN_LIST)
   uint32_t* const wl = L.wlist[tid >> 6];
-  auto list_trip = [&](uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
+  auto list_trip = [&](auto ec, uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
+    constexpr bool ELIST = decltype(ec)::value;   // entries carry complete group terms (early_late)
     uint32_t rr[LEAN_ROWS], dd[LEAN_ROWS];
     bool aa[LEAN_ROWS];
 #pragma unroll
@@ -593,9 +610,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
       aa[u] = i < n;
       const uint32_t x = aa[u] ? wl[(lhead + i) & (LEAN_LIST - 1u)] : 0u;
       rr[u] = x & 0xffffu;
-      dd[u] = npass > 1 ? (L.lut[x >> 16] & DIM_MASK) * stride : dim_u;
+      dd[u] = ELIST ? (x >> 16) : (npass > 1 ? (L.lut[x >> 16] & DIM_MASK) * stride : dim_u);
     }
-    rowsN(std::integral_constant<int, LEAN_ROWS>{}, rr, aa, dd);
+    rowsN(std::integral_constant<int, LEAN_ROWS>{}, ec, rr, aa, dd);
     lhead += n;
   };
   auto wave_sync = [&]() __attribute__((always_inline)) {   // the wave's list writes / reads are ordered
@@ -604,8 +621,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   };
 
-  auto body = [&](auto bwc) __attribute__((always_inline)) {
+  auto body = [&](auto bwc, auto ec) __attribute__((always_inline)) {
     constexpr uint32_t BW = decltype(bwc)::value;
+    constexpr bool ECH = NL > 0 && decltype(ec)::value;   // early_late tile (its own body instantiation)
     constexpr bool POW2 = BW == 1 || BW == 2 || BW == 4;
     // SWAR filter: BW | 32, at most 4 passing codes (uniform)
     const bool swar = POW2 && npass <= 4;
@@ -630,6 +648,46 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
     };
     v4u xpre = v4u{0u, 0u, 0u, 0u};
     if constexpr (NL > 0) xpre = chunk_load(uint32_t(tid));
+    // early_late: chunk qq's late codes -- one 20-B window per late column over the late values of its valid rows
+    // (meta: bit 31 a bit-packed window, bits 0..7 its bit offset; bit 30 the rows straddle a run boundary: decoded
+    // row by row; else the RLE run's code)
+    struct LWin {
+      v4u x;
+      uint32_t x4, meta;
+    };
+    LWin lpre[LT::NLA];
+    auto late_load = [&](uint32_t qq) __attribute__((always_inline)) {
+      const bool lv = qq < total;
+      const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];
+      const uint32_t v0n = Rn.start + 16u * (qq - Rn.cbk);
+      const uint32_t an = (Rn.lo > v0n ? Rn.lo : v0n) - v0n;
+      const uint32_t bn = ((Rn.hi < v0n + 16u) ? Rn.hi : v0n + 16u) - v0n;
+#pragma unroll
+      for (int k = 0; k < NL; k++) {
+        lpre[k] = LWin{v4u{0u, 0u, 0u, 0u}, 0u, 0x40000000u};
+        if (!((lpres >> k) & 1u) || !lv || an >= bn) continue;
+        const uint32_t v = lvb[k] + (v0n + an - vb2);   // late value of the chunk's first valid row (no NULLs)
+        const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
+        const LRun lr = L.lruns[k][ri];
+        if (v + (bn - an) > L.lruns[k][ri + 1].start) continue;   // straddles a run boundary (sentinel at lnr)
+        if (!(lr.off_lit & 0x80000000u)) {
+          lpre[k].meta = lr.value;
+          continue;
+        }
+        const uint32_t bit = (v - lr.start) * lbw[k];
+        const uint32_t byte = (lr.off_lit & 0x7fffffffu) + (bit >> 3);
+        lpre[k].x = __builtin_amdgcn_raw_buffer_load_b128(lrs[k], byte & ~3u, 0, 0);
+        lpre[k].x4 = __builtin_amdgcn_raw_buffer_load_b32(lrs[k], (byte & ~3u) + 16u, 0, 0);
+        lpre[k].meta = 0x80000000u | ((byte & 3u) * 8u + (bit & 7u));
+        if (count_plan) {   // distinct 128-B lines of the late stream read
+          const uint32_t l0 = ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
+          const uint32_t la = ((byte & ~3u) >> 7) - l0, lb = (((byte & ~3u) + 19u) >> 7) - l0;
+          if (la < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][la >> 5], 1u << (la & 31u));
+          if (lb != la && lb < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][lb >> 5], 1u << (lb & 31u));
+        }
+      }
+    };
+    if constexpr (ECH) late_load(uint32_t(tid));
     for (uint32_t q0 = 0; q0 < total; q0 += BLOCK) {   // uniform trip count
       const uint32_t q = q0 + uint32_t(tid);
       const bool live = q < total;
@@ -643,9 +701,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
       const uint32_t rval = R.value & 63u;
       const uint32_t byte = (R.off_lit & 0x7fffffffu) + 2u * BW * k;
       v4u x;
+      LWin lcur[LT::NLA];
       if constexpr (NL > 0) {
         x = xpre;
         xpre = chunk_load(q + BLOCK);
+        if constexpr (ECH) {
+#pragma unroll
+          for (int k = 0; k < NL; k++) lcur[k] = lpre[k];
+          late_load(q + BLOCK);
+        }
       } else {
         x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
       }
@@ -772,7 +836,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
           const uint32_t rr[2] = {rbase + e1, rbase + e2};
           const bool aa[2] = {true, two};
           uint32_t dd[2] = {d1, d2};
-          rowsN(std::integral_constant<int, 2>{}, rr, aa, dd);
+          rowsN(std::integral_constant<int, 2>{}, std::false_type{}, rr, aa, dd);
         }
       } else {
         // Late columns: the wave's passing rows are appended to its LDS list (lane-major) and processed LEAN_TRIP at
@@ -783,6 +847,52 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
           f16 = 0;
 #pragma unroll
           for (int e = 0; e < 16; e++) f16 |= uint32_t((m >> (e * BW + BW - 1)) & 1ull) << e;
+        }
+        // early_late: row e's late code k from the chunk's window (chunk-relative index e - a), its lookup value
+        auto late_code = [&](int k, uint32_t e) __attribute__((always_inline)) -> uint32_t {
+          const LWin& w = lcur[k];
+          if (w.meta >> 31) {
+            const uint32_t sh = (w.meta & 0xffu) + (e - a) * lbw[k], wi = sh >> 5, off = sh & 31u;
+            const uint32_t lo = wi == 0 ? w.x.x : wi == 1 ? w.x.y : wi == 2 ? w.x.z : wi == 3 ? w.x.w : w.x4;
+            const uint32_t hi = wi == 0 ? w.x.y : wi == 1 ? w.x.z : wi == 2 ? w.x.w : wi == 3 ? w.x4 : 0u;
+            return __builtin_amdgcn_alignbit(hi, lo, off) & ((1u << lbw[k]) - 1u);
+          }
+          if (!(w.meta >> 30)) return w.meta;
+          // the chunk straddles a late run boundary: this row's run and packed word (synchronous; rare)
+          const uint32_t v = lvb[k] + rbase + e;
+          const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
+          const LRun lr = L.lruns[k][ri];
+          if (!(lr.off_lit & 0x80000000u)) return lr.value;
+          const uint32_t bit = (v - lr.start) * lbw[k];
+          const uint32_t byte = (lr.off_lit & 0x7fffffffu) + (bit >> 3);
+          const v2u ww = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], byte & ~3u, 0, 0);
+          const uint64_t xx = ((uint64_t)ww.y << 32) | ww.x;
+          return uint32_t(xx >> ((byte & 3u) * 8u + (bit & 7u))) & ((1u << lbw[k]) - 1u);
+        };
+        if constexpr (ECH) {   // the late filter before the list
+          if (!late_trivial) {
+            uint32_t keep = 0u, f = f16;
+            const uint32_t lf = Sp->leaf_false;
+            while (f) {
+              const uint32_t e = uint32_t(__builtin_ctz(f));
+              f &= f - 1u;
+              uint32_t T = 0u, F = 0u;
+#pragma unroll
+              for (int k = 0; k < NL; k++) {
+                const StrParam& sp = P.strp[1 + k];
+                if (!((lpres >> k) & 1u)) {
+                  F |= sp.hmask;
+                  continue;
+                }
+                const uint32_t bits = (L.llut[k][late_code(k, e)] >> 24) << sp.lbase;
+                T |= bits & sp.lmask;
+                F |= ~bits & sp.lmask;
+              }
+              const uint32_t ix = (T & ~lf) | ((F | lf) << P.nleaves);
+              keep |= ((L.ltruth[ix >> 5] >> (ix & 31)) & 1u) << e;
+            }
+            f16 = keep;
+          }
         }
         const uint32_t cnt = uint32_t(__popc(f16));
         uint32_t inc = cnt;
@@ -799,30 +909,50 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(LEAN_WAVE
           while (f) {
             const uint32_t e = uint32_t(__builtin_ctz(f));
             f &= f - 1u;
-            if (pos >= done && pos < done + take)
-              wl[(ltail + pos - done) & (LEAN_LIST - 1u)] = (rbase + e) | ((lit ? lean_code<BW>(w0, w1, w2, e) : rval) << 16);
+            if (pos >= done && pos < done + take) {
+              const uint32_t code = lit ? lean_code<BW>(w0, w1, w2, e) : rval;
+              uint32_t hi16 = code;
+              if constexpr (ECH) {   // the row's complete group term
+                hi16 = npass > 1 ? (L.lut[code] & DIM_MASK) * stride : dim_u;
+#pragma unroll
+                for (int k = 0; k < NL; k++) {
+                  const StrParam& sp = P.strp[1 + k];
+                  hi16 += ((lpres >> k) & 1u) ? (L.llut[k][late_code(k, e)] & DIM_MASK) * sp.dim_stride
+                                              : sp.dim_null * sp.dim_stride;
+                }
+              }
+              wl[(ltail + pos - done) & (LEAN_LIST - 1u)] = (rbase + e) | (hi16 << 16);
+            }
             pos++;
           }
           ltail += take;
           done += take;
           wave_sync();
-          while (ltail - lhead >= LEAN_TRIP) list_trip(LEAN_TRIP);   // uniform
+          while (ltail - lhead >= LEAN_TRIP) list_trip(ec, LEAN_TRIP);   // uniform
           wave_sync();   // the trips' entries are rewritten by later appends
         }
       }
     }
     if constexpr (NL > 0) {
-      while (ltail != lhead) list_trip(min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
+      while (ltail != lhead) list_trip(ec, min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
       wave_sync();
     }
   };
+  auto body2 = [&](auto bwc) __attribute__((always_inline)) {
+    if constexpr (NL > 0 && EARLY) {
+      if (early_late) body(bwc, std::true_type{});   // uniform
+      else body(bwc, std::false_type{});
+    } else {
+      body(bwc, std::false_type{});
+    }
+  };
   switch (bw) {   // uniform
-    case 1: body(std::integral_constant<uint32_t, 1>{}); break;
-    case 2: body(std::integral_constant<uint32_t, 2>{}); break;
-    case 3: body(std::integral_constant<uint32_t, 3>{}); break;
-    case 4: body(std::integral_constant<uint32_t, 4>{}); break;
-    case 5: body(std::integral_constant<uint32_t, 5>{}); break;
-    default: body(std::integral_constant<uint32_t, 6>{}); break;
+    case 1: body2(std::integral_constant<uint32_t, 1>{}); break;
+    case 2: body2(std::integral_constant<uint32_t, 2>{}); break;
+    case 3: body2(std::integral_constant<uint32_t, 3>{}); break;
+    case 4: body2(std::integral_constant<uint32_t, 4>{}); break;
+    case 5: body2(std::integral_constant<uint32_t, 5>{}); break;
+    default: body2(std::integral_constant<uint32_t, 6>{}); break;
   }
 
   flush();

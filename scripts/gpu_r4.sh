@@ -10,8 +10,8 @@ if [ -z "$NOTESTS" ]; then
   rc=$?; tail -5 gpurun_out/r4/tests.log; [ $rc -eq 0 ] || exit $rc
 fi
 for e in ${ENVS:--}; do
-  ee=""; [ "$e" != "-" ] && ee="$e"
-  tag=$(echo "${e}" | tr '=,' '__')
+  ee=""; [ "$e" != "-" ] && ee=$(echo "$e" | tr "+" " ")
+  tag=$(echo "${e}" | tr '=,+' '___')
   for q in ${QUERIES:-}; do
     cs=0; [ -n "$VALIDATE" ] && [ "$q" != tag ] && [ "$q" != dense ] && [ "$q" != c5 ] && [ "$q" != exemplar ] && cs=-1
     env $ee timeout -k 10 ${PER:-400} python3 bench.py --query $q --steps ${STEPS:-10} --warmup 3 --cpu-sample $cs $BENCH_ARGS > gpurun_out/r4/${q}_${tag}.json 2> gpurun_out/r4/${q}_${tag}.log || exit $?
