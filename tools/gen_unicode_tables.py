@@ -6,7 +6,11 @@ Two tables, from Python's unicodedata (Unicode 13.0 on CPython 3.10):
     (k, K, KELVIN SIGN; s, S, LONG S; sigma, final sigma, capital sigma ...).  RE2 folds `(?i)` / the 'i'
     option over exactly these orbits (CaseFolding.txt C + S entries);
   * general categories as code point ranges, for \\pL, \\p{Lu}, \\PN ... (RE2's one- and two-letter classes;
-    "C" is Cc|Cf|Co|Cs, unassigned code points belong to no class, as in RE2).
+    "C" is Cc|Cf|Co|Cs, unassigned code points belong to no class, as in RE2);
+  * Unicode scripts (\\p{Greek}, \\p{Han} ...): Python's unicodedata has no script property, so each script's
+    code points are read off RE2 itself -- pyarrow's bundled RE2 (the regex oracle of tests/test_regex.py) matches
+    every code point against ^\\p{<Script>}$ -- and stored as ranges.  Scripts that RE2 build does not know are
+    left out (the matcher reports them as unsupported).
 
     python3 tools/gen_unicode_tables.py > lakeside_amd/csrc/unicode_tables.inc
 """
@@ -82,6 +86,56 @@ def ranges_union(lists):
     return out
 
 
+SCRIPTS = [
+    "Adlam", "Ahom", "Anatolian_Hieroglyphs", "Arabic", "Armenian", "Avestan", "Balinese", "Bamum", "Bassa_Vah",
+    "Batak", "Bengali", "Bhaiksuki", "Bopomofo", "Brahmi", "Braille", "Buginese", "Buhid", "Canadian_Aboriginal",
+    "Carian", "Caucasian_Albanian", "Chakma", "Cham", "Cherokee", "Chorasmian", "Common", "Coptic", "Cuneiform",
+    "Cypriot", "Cypro_Minoan", "Cyrillic", "Deseret", "Devanagari", "Dives_Akuru", "Dogra", "Duployan",
+    "Egyptian_Hieroglyphs", "Elbasan", "Elymaic", "Ethiopic", "Georgian", "Glagolitic", "Gothic", "Grantha", "Greek",
+    "Gujarati", "Gunjala_Gondi", "Gurmukhi", "Han", "Hangul", "Hanifi_Rohingya", "Hanunoo", "Hatran", "Hebrew",
+    "Hiragana", "Imperial_Aramaic", "Inherited", "Inscriptional_Pahlavi", "Inscriptional_Parthian", "Javanese",
+    "Kaithi", "Kannada", "Katakana", "Kawi", "Kayah_Li", "Kharoshthi", "Khitan_Small_Script", "Khmer", "Khojki",
+    "Khudawadi", "Lao", "Latin", "Lepcha", "Limbu", "Linear_A", "Linear_B", "Lisu", "Lycian", "Lydian", "Mahajani",
+    "Makasar", "Malayalam", "Mandaic", "Manichaean", "Marchen", "Masaram_Gondi", "Medefaidrin", "Meetei_Mayek",
+    "Mende_Kikakui", "Meroitic_Cursive", "Meroitic_Hieroglyphs", "Miao", "Modi", "Mongolian", "Mro", "Multani",
+    "Myanmar", "Nabataean", "Nag_Mundari", "Nandinagari", "New_Tai_Lue", "Newa", "Nko", "Nushu",
+    "Nyiakeng_Puachue_Hmong", "Ogham", "Ol_Chiki", "Old_Hungarian", "Old_Italic", "Old_North_Arabian", "Old_Permic",
+    "Old_Persian", "Old_Sogdian", "Old_South_Arabian", "Old_Turkic", "Old_Uyghur", "Oriya", "Osage", "Osmanya",
+    "Pahawh_Hmong", "Palmyrene", "Pau_Cin_Hau", "Phags_Pa", "Phoenician", "Psalter_Pahlavi", "Rejang", "Runic",
+    "Samaritan", "Saurashtra", "Sharada", "Shavian", "Siddham", "SignWriting", "Sinhala", "Sogdian", "Sora_Sompeng",
+    "Soyombo", "Sundanese", "Syloti_Nagri", "Syriac", "Tagalog", "Tagbanwa", "Tai_Le", "Tai_Tham", "Tai_Viet",
+    "Takri", "Tamil", "Tangsa", "Tangut", "Telugu", "Thaana", "Thai", "Tibetan", "Tifinagh", "Tirhuta", "Toto",
+    "Ugaritic", "Vai", "Vithkuqi", "Wancho", "Warang_Citi", "Yezidi", "Yi", "Zanabazar_Square"]
+
+
+def scripts():
+    """Script -> code point ranges, as pyarrow's RE2 classifies every code point (surrogates excluded)."""
+    import numpy as np
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    cps = [c for c in range(MAXRUNE + 1) if not 0xD800 <= c <= 0xDFFF]
+    arr = pa.array([chr(c) for c in cps], pa.string())
+    cpa = np.array(cps, dtype=np.int64)
+    out = {}
+    for name in SCRIPTS:
+        try:
+            m = pc.match_substring_regex(arr, "^\\p{%s}$" % name).to_numpy(zero_copy_only=False)
+        except pa.ArrowInvalid:   # not a script this RE2 build knows
+            continue
+        sel = cpa[np.asarray(m, dtype=bool)]
+        rng = []
+        for c in sel.tolist():
+            if rng and rng[-1][1] == c - 1:
+                rng[-1][1] = c
+            elif rng and rng[-1][1] == 0xD7FF and c == 0xE000:   # contiguous across the surrogate gap
+                rng[-1][1] = c
+            else:
+                rng.append([c, c])
+        if rng:
+            out[name] = rng
+    return out
+
+
 def main():
     w = sys.stdout.write
     w("// GENERATED by tools/gen_unicode_tables.py from Python unicodedata %s -- do not edit.\n"
@@ -98,6 +152,10 @@ def main():
         groups[cat] = lst
     for major in "CLMNPSZ":
         groups[major] = ranges_union([v for k, v in cats.items() if k[0] == major])
+    scr = scripts()
+    w("// Scripts: %d of RE2's script names, code points as pyarrow %s's bundled RE2 classifies them.\n"
+      % (len(scr), __import__("pyarrow").__version__))
+    groups.update(scr)
     names = sorted(groups)
     for name in names:
         w("static const uint32_t kCat_%s[][2] = {" % name)
