@@ -54,6 +54,11 @@ QUERIES = {
     "exemplar": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
                              "computed": False, "dataType": "string"}, agg=None, group_bys=[], exemplar=1000,
                      desc="exemplar :eq _cardinalhq.name=metric_07, ORDER BY ts DESC LIMIT 1000 per glob"),
+    # numeric comparison leaf on the value column: scan_lean filters on the name and tests the
+    # value of every passing row (BaseExpr.scala:488-498)
+    "gt": dict(filter={"op": "and", "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
+                       "q2": {"k": "_cardinalhq.value", "v": ["1.5"], "op": "gt", "dataType": "number"}},
+               agg="sum", group_bys=[], desc=":and(:eq _cardinalhq.name=metric_07, :gt _cardinalhq.value 1.5) :sum, step 1m"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],

@@ -351,7 +351,8 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   }
   const bool numeric = !nums.empty();
   if (numeric && (sketch || ces)) throw PlanError(LK_ERR_UNSUPPORTED, "numeric comparison leaves in sketch queries");
-  if (numeric && dist) throw PlanError(LK_ERR_UNSUPPORTED, "distributed queries with numeric comparison leaves");
+  // (distributed: the numeric leaves' per-glob decisions -- a bad literal, a VARCHAR column -- come from the agreed glob
+  // unions, and the general row scan's partial tables reduce like any other)
 
   // no segments: the worker answers one sentinel row (Commons.scala:393-396)
   if (R.segments.empty()) {
@@ -804,13 +805,49 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     throw PlanError(LK_ERR_UNSUPPORTED, "cell key space beyond 64 bits");
   const uint64_t ncells = uint64_t(nslots) * nbuckets * ngroups;
 
+  // Numeric leaves on the value column alone (`:and(:eq name, :gt value 1.5)`), in conjuncts of their own: the fused
+  // kernels filter on the string conjuncts and test the value of each passing row (QParams.vl / vtab) -- the segments
+  // whose tiles all qualify for scan_lean; the other segments take the general row scan as before.
+  bool vleaf = false;
+  std::vector<uint8_t> prog_str;   // vleaf: the string conjuncts (the fused kernels' filter)
+  uint32_t vtab = 0;
+  if (numeric && !tagq && nums.size() == 1 && nums[0] == vcol && nleaves.size() <= size_t(VLEAF_MAX) &&
+      leaves.size() <= size_t(TT_MAX_LEAVES) && !getenv("LK_NO_VLEAF")) {
+    std::vector<const FilterNode*> conj;
+    conjuncts(R.filter.get(), conj);
+    std::vector<uint8_t> pn;
+    bool ok = true;
+    for (auto* c : conj) {
+      std::vector<const FilterNode*> ls;
+      collect_leaves(c, ls);
+      const size_t nn = size_t(std::count_if(ls.begin(), ls.end(), [](const FilterNode* l) { return numeric_op(l->op); }));
+      if (nn && nn != ls.size()) ok = false;   // a conjunct mixing string and numeric leaves
+      std::vector<uint8_t>& dst = nn ? pn : prog_str;
+      const bool first = dst.empty();
+      postfix(c, leaves, dst);
+      if (!first) dst.push_back(OP_AND);
+    }
+    if (ok && !pn.empty()) {
+      vleaf = true;
+      if (prog_str.empty()) prog_str.push_back(OP_TRUE);
+      // vtab bit m: the numeric conjuncts with leaf k TRUE iff bit k of m (no UNKNOWN: scan_lean tiles hold no NULL)
+      const uint32_t L = uint32_t(leaves.size()), nsl = L - uint32_t(nleaves.size());
+      const std::vector<uint32_t> tn = truth_table(pn, L);
+      for (uint32_t m = 0; m < (1u << nleaves.size()); m++) {
+        const uint32_t full = (1u << nleaves.size()) - 1u;
+        const uint32_t ix = (m << nsl) | (((~m & full) << nsl) << L);
+        if ((tn[ix >> 5] >> (ix & 31)) & 1u) vtab |= 1u << m;
+      }
+    }
+  }
   // filter truth table: bit (T | F << L) = Kleene value of the tree is TRUE (host-evaluated once per query)
-  std::vector<uint32_t> truth, truth_early, truth_late;
+  std::vector<uint32_t> truth, truth_early, truth_late, truth_x;   // truth_x: the general row scan's (vleaf)
   uint32_t late_mask = 0;
   int early = -1;   // the string column (strs index) of the single-column early conjuncts, when there is one
   if (leaves.size() <= size_t(TT_MAX_LEAVES)) {
     const uint32_t L = uint32_t(leaves.size());
-    truth = truth_table(prog, L);
+    truth = truth_table(vleaf ? prog_str : prog, L);
+    if (vleaf) truth_x = truth_table(prog, L);
     // Predicate pushdown + late materialization.  filter = C_early AND C_late where C_early is the conjuncts
     // over one "early" column (the name column when a conjunct constrains it alone).  The kernel decodes the
     // early column for every row, lists the rows where C_early is TRUE, and decodes every other string column
@@ -832,6 +869,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       return std::all_of(ls.begin(), ls.end(), [](const FilterNode* l) { return l->op == "exists" || l->op == "has"; });
     };
     bool early_weak = true;
+    if (vleaf)   // the value-leaf conjuncts are tested per passing row, outside the early / late split
+      conj.erase(std::remove_if(conj.begin(), conj.end(), [&](const FilterNode* c) { return cols_of(c) == (1u << 31); }),
+                 conj.end());
     for (auto* c : conj) {
       const uint32_t m = cols_of(c);
       if (__builtin_popcount(m) != 1) continue;
@@ -849,7 +889,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       const uint32_t m = cols_of(c);
       if (early >= 0 && m != (1u << early) && ((m >> early) & 1u)) mixed = true;
     }
-    if (early >= 0 && strs.size() >= 2 && !mixed && !numeric) {
+    if (early >= 0 && strs.size() >= 2 && !mixed && (!numeric || vleaf)) {
       std::vector<uint8_t> pe, pl;
       for (auto* c : conj) {
         std::vector<uint8_t>& dst = cols_of(c) == (1u << early) ? pe : pl;
@@ -877,6 +917,9 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     late_mask = m;
   }
   const int lead = dev_of[0] == 0 ? 0 : int(std::find(dev_of.begin(), dev_of.end(), 0) - dev_of.begin());   // strs index at device 0
+  // vleaf needs scan_lean's shape: the early column alone, or with <= 2 late columns (the launch test below)
+  const bool vleaf_shape = vleaf && !truth.empty() &&
+                           (strs.size() == 1 || (strs.size() <= 3 && late_mask == ((1u << strs.size()) - 2u)));
 
   // ---- per-segment query descriptors ----
   // `qsegs` go to the fused kernels (scan_lean / scan_tiles: INT64 timestamps, DOUBLE values); `gsegs` to the general
@@ -907,7 +950,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       q.leaf_false = g.leaf_false;
       q.win_lo = g.win_lo;
       q.win_hi = g.win_hi;
-      bool general = numeric;
+      bool general = numeric && !vleaf;
       // (column types were checked per glob above: a type the query cannot bind emptied the glob)
       auto bind = [&](int qc, const std::string& name, bool want_string) {
         int c = S.col_index(name);
@@ -935,6 +978,24 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
       for (size_t s = 0; s < strs.size(); s++) bind(2 + dev_of[s], strs[s].name, true);
       for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
+      // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
+      // name page has a small dictionary (lean_tile's test at page granularity)
+      bool seg_lean = !general;
+      if (seg_lean) {
+        const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
+        const int cn = strs.size() <= 3 ? S.col_index(strs[size_t(lead)].name) : -1;
+        seg_lean = ct >= 0 && (cv >= 0 || tagq) && cn >= 0 && !S.cols[ct].any_nulls && (tagq || !S.cols[cv].any_nulls) &&
+                   !S.cols[cn].any_nulls;
+        for (size_t s2 = 0; s2 < strs.size() && seg_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
+          if (int(s2) == lead) continue;
+          const int cl = S.col_index(strs[s2].name);
+          if (cl < 0) continue;
+          if (S.cols[cl].any_nulls || !S.cols[cl].pages_lean_late) seg_lean = false;
+        }
+        if (seg_lean && !S.cols[cn].pages_lean_name) seg_lean = false;
+      }
+      // vleaf: only scan_lean tests the value leaves -- a segment it does not take whole goes to the general row scan
+      if (vleaf && (!seg_lean || !vleaf_shape)) general = true;
       if (general) {
         q.tile_begin = total_tiles;
         seg_begin.push_back(total_tiles);
@@ -942,21 +1003,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
         gsegs.push_back(q);
         continue;
       }
-      // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
-      // name page has a small dictionary (lean_tile's test at page granularity)
-      if (all_lean) {
-        const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
-        const int cn = strs.size() <= 3 ? S.col_index(strs[size_t(lead)].name) : -1;
-        all_lean = ct >= 0 && (cv >= 0 || tagq) && cn >= 0 && !S.cols[ct].any_nulls && (tagq || !S.cols[cv].any_nulls) &&
-                   !S.cols[cn].any_nulls;
-        for (size_t s2 = 0; s2 < strs.size() && all_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
-          if (int(s2) == lead) continue;
-          const int cl = S.col_index(strs[s2].name);
-          if (cl < 0) continue;
-          if (S.cols[cl].any_nulls || !S.cols[cl].pages_lean_late) all_lean = false;
-        }
-        if (all_lean && !S.cols[cn].pages_lean_name) all_lean = false;
-      }
+      all_lean = all_lean && seg_lean;
       q.tile_begin = total_tiles;
       seg_begin.push_back(total_tiles);
       total_tiles += q.ntiles;
@@ -1037,6 +1084,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   const size_t o_segs = reserve(qsegs.size() * sizeof(QSeg));
   const size_t o_gsegs = reserve(gsegs.size() * sizeof(QSeg));
   const size_t o_truth = reserve(truth.size() * 4);
+  const size_t o_truth_x = reserve(truth_x.size() * 4);
   const size_t o_truth_e = reserve(truth_early.size() * 4);
   const size_t o_truth_l = reserve(truth_late.size() * 4);
   std::vector<size_t> o_tab(strs.size());
@@ -1095,6 +1143,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   memcpy(hbuf + o_segs, qsegs.data(), qsegs.size() * sizeof(QSeg));
   memcpy(hbuf + o_gsegs, gsegs.data(), gsegs.size() * sizeof(QSeg));
   if (!truth.empty()) memcpy(hbuf + o_truth, truth.data(), truth.size() * 4);
+  if (!truth_x.empty()) memcpy(hbuf + o_truth_x, truth_x.data(), truth_x.size() * 4);
   if (late_mask) {
     memcpy(hbuf + o_truth_e, truth_early.data(), truth_early.size() * 4);
     memcpy(hbuf + o_truth_l, truth_late.data(), truth_late.size() * 4);
@@ -1150,9 +1199,17 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       if (((late_mask >> dev_of[s]) & 1u) && !strs[s].leaves.empty()) late_leaves = true;
     P.late_chunk = (late_leaves && ngroups <= 65536u && !getenv("LK_NO_LATE_CHUNK")) ? 1u : 0u;
   }
-  P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && !numeric && !getenv("LK_NO_LEAN_SPLIT"))
+  P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
-  if (numeric) P.lean = 0;   // the general row scan accumulates every table field
+  if (numeric && !(vleaf && gsegs.empty())) P.lean = 0;   // the general row scan accumulates every table field
+  if (vleaf && !qsegs.empty()) {   // scan_lean tests the value leaves of every row its string conjuncts pass
+    P.nvl = uint32_t(nleaves.size());
+    P.vtab = vtab;
+    for (size_t k = 0; k < nleaves.size(); k++) {
+      const NumLeaf& nl = nleaves[k];
+      P.vl[k] = VLeaf{nl.dlo, nl.dhi, nl.lo_incl, nl.hi_incl, nl.nan_pass, 0u};
+    }
+  }
   // scan_lean: a dense table whose group space fits LDS for the few buckets a tile spans is aggregated in the tile's
   // direct table (lean_kernel.hpp) instead of the LDS hash table: dir_span = the most buckets it holds
   if (P.lean_split && !hash_mode && !getenv("LK_NO_DIRECT")) {
@@ -1266,7 +1323,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       XG.nleaves = P.nleaves;
       XG.nprog = P.nprog;
       memcpy(XG.prog, P.prog, sizeof(XG.prog));
-      XG.truth = P.truth;
+      XG.truth = truth_x.empty() ? P.truth : reinterpret_cast<const uint32_t*>(dbuf + o_truth_x);
       XG.mode = XMODE_AGG;
       XG.nnum = uint32_t(nums.size());
       XG.nnl = uint32_t(nleaves.size());

@@ -121,6 +121,11 @@ struct StrParam {           // per string column of a query (device array; read 
   uint32_t pad;
 };
 
+constexpr int VLEAF_MAX = 5;
+struct VLeaf {                       // value in (lo, hi) with inclusive ends per flag; NaN (greatest) passes iff nan_pass
+  double lo, hi;
+  uint32_t lo_incl, hi_incl, nan_pass, pad;
+};
 struct QParams {
   const QSeg* segs;
   uint32_t nsegs;
@@ -180,6 +185,12 @@ struct QParams {
   uint32_t rows_only;                // COUNT(*) (tag queries): no value column bound; lean tiles take none
   uint32_t late_chunk;               // scan_lean NL > 0: late columns decoded per 16-row chunk in the main loop (the
                                      // list then carries each row's group term; lean_kernel.hpp)
+  // Numeric comparison leaves on the value column (`value > 1.5`, BaseExpr.scala:488-498) in the fused kernel: a row
+  // whose string conjuncts pass is kept iff vtab bit (its leaves' outcomes, bit k = leaf k) is set -- the numeric
+  // conjuncts' value.  scan_lean tiles hold no NULL value, so no leaf is UNKNOWN there.
+  uint32_t nvl;
+  uint32_t vtab;
+  VLeaf vl[VLEAF_MAX];
 };
 // scan_lean's direct table: LDS words by late-column count NL (the hash table's 8 KB for NL >= 1, so the kernels keep
 // their occupancy), at most LEAN_DIR_MAXSPAN buckets

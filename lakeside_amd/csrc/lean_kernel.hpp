@@ -435,6 +435,16 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   };
   // one passing row: bucket (BaseExpr.scala:159-165 window, 163-165 / 376-394 bucket), cell, register cell
   auto row = [&](int64_t ts, double v, uint32_t dim) __attribute__((always_inline)) {
+    if (P.nvl) {   // numeric leaves on the value column (uniform)
+      uint32_t bits = 0;
+      for (uint32_t k = 0; k < P.nvl; k++) {
+        const VLeaf& vl = P.vl[k];
+        const bool pass = v != v ? vl.nan_pass != 0u
+                                 : ((v > vl.lo || (vl.lo_incl && v == vl.lo)) && (v < vl.hi || (vl.hi_incl && v == vl.hi)));
+        bits |= uint32_t(pass) << k;
+      }
+      if (!((P.vtab >> bits) & 1u)) return;
+    }
     bool ok = true;
     int64_t b = tile_b;
     if (!one_bucket) {
@@ -500,7 +510,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
 #pragma unroll
       for (int u = 0; u < N; u++) {
         if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, p[u] ? (vb0 + rr[u]) * 8u : OOB, 0, 0);
-        if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, p[u] ? (vb1 + rr[u]) * 8u : OOB, 0, 0);
+        if (AGG != AGG_COUNT || P.nvl) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, p[u] ? (vb1 + rr[u]) * 8u : OOB, 0, 0);
       }
     };
     if constexpr (NL > 0 && !LATE_DONE) {
@@ -587,7 +597,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
       for (int u = 0; u < N; u++) {
         if (!p[u]) continue;
         if (!one_bucket) mark(L.lines_t, (vb0 + rr[u]) * 8u, line_t0);
-        if (AGG != AGG_COUNT) mark(L.lines_v, (vb1 + rr[u]) * 8u, line_v0);
+        if (AGG != AGG_COUNT || P.nvl) mark(L.lines_v, (vb1 + rr[u]) * 8u, line_v0);
       }
     }
 #pragma unroll
@@ -792,7 +802,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
               tt[u] = v2u{0u, 0u};
               xx[u] = v2u{0u, 0u};
               if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, pp[u] ? (vb0 + r) * 8u : OOB, 0, 0);
-              if (AGG != AGG_COUNT) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, pp[u] ? (vb1 + r) * 8u : OOB, 0, 0);
+              if (AGG != AGG_COUNT || P.nvl) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, pp[u] ? (vb1 + r) * 8u : OOB, 0, 0);
               dd[u] = dim_u;
               if (npass > 1) {   // uniform
                 const uint32_t a0 = uint32_t(__shfl(int(c0), src));
@@ -805,7 +815,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
                   const uint32_t l = (((vb0 + r) * 8u) >> 7) - line_t0;
                   atomicOr(&L.lines_t[l >> 5], 1u << (l & 31u));
                 }
-                if (AGG != AGG_COUNT) {
+                if (AGG != AGG_COUNT || P.nvl) {
                   const uint32_t l = (((vb1 + r) * 8u) >> 7) - line_v0;
                   atomicOr(&L.lines_v[l >> 5], 1u << (l & 31u));
                 }

@@ -69,8 +69,13 @@ def plan_text(pr: dx.PushDownRequest, glob_size: int) -> Tuple[str, List[str], L
     be = pr.baseExpr
     dx.check_hot_path(pr)
     leaves = _leaves(be.filter, [])
+    vcol = dx.value_column(be)
     strcols = [dx.NAME]
     for l in leaves:
+        if l.op in dx.NUMERIC_OPS:   # numeric comparison leaves: on the value column only (BaseExpr.scala:488-498)
+            if l.k != vcol:
+                raise NotImplementedError("lkcpu: numeric comparison leaves on a column other than the value column")
+            continue
         if l.k not in strcols:
             strcols.append(l.k)
     gbs = []
@@ -90,7 +95,10 @@ def plan_text(pr: dx.PushDownRequest, glob_size: int) -> Tuple[str, List[str], L
     t += [str(len(gbs))] + [str(strcols.index(g)) for g in gbs]
     t += [str(len(leaves))]
     for l in leaves:
-        t += [str(strcols.index(l.k)), l.op, str(len(l.v))] + list(l.v)
+        if l.op in dx.NUMERIC_OPS:   # column -1 = the value column; the literal normalized (BaseExpr.scala:450-459)
+            t += ["-1", l.op, "1", repr(dx.normalized_value(l))]
+        else:
+            t += [str(strcols.index(l.k)), l.op, str(len(l.v))] + list(l.v)
     prog = _postfix(be.filter, leaves, [])
     t += [str(len(prog))] + [str(x) for x in prog]
     fs = sorted(dx.field_set(be))

@@ -401,7 +401,8 @@ void decode_chunk(const uint8_t* f, size_t fsize, const ColMeta& m, bool optiona
 // plan
 // ---------------------------------------------------------------------------------------------------------
 struct Leaf {
-  int col;                       // string column index
+  int col;                       // string column index (-1: a numeric comparison on the value column)
+  double c = 0;                  // numeric leaf: the normalized literal
   std::string op;
   std::vector<std::string> v;
   std::unique_ptr<regex_t> re;   // regex / contains
@@ -599,6 +600,7 @@ Plan parse_plan(const char* text) {
     L.op = next();
     const int nv = int(num());
     for (int k = 0; k < nv; k++) L.v.push_back(next());
+    if (L.col < 0) L.c = std::stod(L.v.at(0));
     if (L.op == "regex" || L.op == "contains") {
       const std::string pat = L.op == "contains" ? ".*" + L.v[0] + ".*" : L.v[0];
       L.re.reset(new regex_t);
@@ -667,12 +669,13 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
     std::map<std::string, int> nonexist;
     for (auto& f : P.fieldset)
       if (!uni.count(f)) nonexist[f] = 1;
+    auto leaf_col = [&](const Leaf& l) -> const std::string& { return l.col < 0 ? P.vcol : P.strcols[size_t(l.col)]; };
     for (size_t l = 0; l < P.leaves.size(); l++)
-      if (nonexist.count(P.strcols[size_t(P.leaves[l].col)])) leaf_false[g] |= 1u << l;
+      if (nonexist.count(leaf_col(P.leaves[l]))) leaf_false[g] |= 1u << l;
     // DuckDB Binder Error: a referenced column no file of the glob has (leaf columns not compiled to false,
     // timestamp, name, value)
     for (auto& l : P.leaves)
-      if (!nonexist.count(P.strcols[size_t(l.col)]) && !uni.count(P.strcols[size_t(l.col)])) skip[g] = 1;
+      if (!nonexist.count(leaf_col(l)) && !uni.count(leaf_col(l))) skip[g] = 1;
     if (!uni.count("_cardinalhq.timestamp") || !uni.count("_cardinalhq.name") || !uni.count(P.vcol)) skip[g] = 1;
     keycols[g].push_back(0);
     for (int c : P.gby)
@@ -726,7 +729,11 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
       std::vector<std::vector<uint32_t>> tbits(static_cast<size_t>(nstr));
       std::vector<std::vector<int32_t>> gidmap(static_cast<size_t>(nstr));
       std::vector<uint32_t> colmask(static_cast<size_t>(nstr), 0);
-      for (size_t l = 0; l < P.leaves.size(); l++) colmask[size_t(P.leaves[l].col)] |= 1u << l;
+      uint32_t nummask = 0;   // numeric leaves on the value column
+      for (size_t l = 0; l < P.leaves.size(); l++) {
+        if (P.leaves[l].col < 0) nummask |= 1u << l;
+        else colmask[size_t(P.leaves[l].col)] |= 1u << l;
+      }
       for (int c = 0; c < nstr; c++) {
         has_s[size_t(c)] = load(P.strcols[size_t(c)], true, sc[size_t(c)]);
         const auto& dict = sc[size_t(c)].dict;
@@ -761,6 +768,17 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
           const uint32_t b = tbits[size_t(c)][size_t(code)];
           T |= b & m;
           F |= ~b & m;
+        }
+        if (nummask && has_v && vc.valid[size_t(r)]) {   // value NULL: the comparison is NULL (neither bit)
+          const double x = vc.f64[size_t(r)];
+          for (size_t l = 0; l < P.leaves.size(); l++) {
+            if (!((nummask >> l) & 1u)) continue;
+            const Leaf& L = P.leaves[l];
+            const bool up = L.op == "gt" || L.op == "ge";
+            const bool pass = std::isnan(x) ? up   // NaN sorts greatest (DuckDB)
+                              : L.op == "gt" ? x > L.c : L.op == "ge" ? x >= L.c : L.op == "lt" ? x < L.c : x <= L.c;
+            (pass ? T : F) |= 1u << l;
+          }
         }
         T &= ~lf;
         F |= lf;

@@ -430,3 +430,53 @@ def _worker_fault(rank, world, port):
 def test_dist_injected_device_fault_fails_every_rank():
     import torch.multiprocessing as mp
     mp.spawn(_worker_fault, args=(2, _free_port()), nprocs=2, join=True)
+
+
+def _worker_numeric(rank, world, port, paths):
+    """numeric comparison leaves through the distributed path (host transport, world 2): the
+    general row scan's partial tables reduce on rank 0; rows equal the oracle's over every file."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd import synth
+    from lakeside_amd.evaluator import Engine
+    from oracle import dataexpr as dx
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        segs = [synth.segment_request(i, hour=0) for i in range(len(paths))]
+        num = lambda k, op, v: {"k": k, "v": [v], "op": op, "dataType": "number"}   # noqa: E731
+        for filt, agg, gbs in [({"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"),
+                                 "q2": num("attr.dur", "gt", "1000000")}, "sum", ["resource.service.name"]),
+                               ({"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_02"),
+                                 "q2": num("_cardinalhq.value", "ge", "1.5")}, "max", []),
+                               ({"op": "or", "q1": num("attr.size", "lt", "100"),
+                                 "q2": synth.leaf("resource.service.name", "eq", "svc-3")}, "count",
+                                ["resource.service.name"])]:
+            req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+            try:
+                res = eng.eval_pushdown_dist(req, paths, None, 2)
+            except Exception as e:   # both ranks' failures in the log (spawn reports only one)
+                print(f"rank {rank}: {agg} failed: {e}", flush=True)
+                raise
+            if rank == 0:
+                want = dx.evaluate_merged(dx.parse_pushdown(req), paths, 2)
+                assert_rows_equal(res.rows(), want, agg, f"dist numeric {agg}")
+                assert res.stats["general_segments"] > 0, res.stats
+            else:
+                assert len(res) == 0
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dist_numeric_leaves_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    from tests.test_gpu_numeric import _files
+    paths, _ = _files(tmp_path)
+    mp.spawn(_worker_numeric, args=(2, _free_port(), paths), nprocs=2, join=True)

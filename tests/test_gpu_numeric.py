@@ -122,3 +122,37 @@ def test_numeric_leaves_tag_and_exemplar(engine, tmp_path):
     assert len(rows) == len(want) > 0
     for g, w in zip(rows, want):
         assert (g[0], g[3], g[2]) == (w[0], w[3], w[2])
+
+
+@pytest.mark.parametrize("mixed", [False, True])
+def test_value_leaf_on_scan_lean(engine, mixed):
+    """numeric leaves on the value column run inside scan_lean (string conjuncts early, the value
+    tested per passing row), with the general row scan taking only segments scan_lean cannot take whole (mixed: one
+    segment with NULL values).  GPU == oracle per glob and merged."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    keys, blobs = [], []
+    for i in range(4):
+        nf = 0.05 if (mixed and i == 2) else 0.0
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 17, null_frac=nf, rg_rows=1 << 16, page_rows=1 << 14))
+        blobs.append(s.bytes())
+        engine.put_segment_ptr(f"vleaf/{mixed}/{i}", s.ptr, s.size)
+        s.free()
+        keys.append(f"vleaf/{mixed}/{i}")
+    segs = [synth.segment_request(i) for i in range(4)]
+    v = lambda op, x: _num(dx.VALUE, op, x)   # noqa: E731
+    for filt, agg, gbs in [({"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"), "q2": v("gt", "1.5")}, "sum", []),
+                           ({"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_07"),
+                             "q2": {"op": "or", "q1": v("le", "0.25"), "q2": v("gt", "100")}}, "count", [SVC]),
+                           ({"op": "and", "q1": {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_03"),
+                                                 "q2": synth.leaf(SVC, "regex", "^svc-0[0-4]")},
+                             "q2": {"not": v("ge", "2")}}, "max", [SVC]),
+                           ({"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_05"), "q2": v("lt", "1e3")}, "avg", [])]:
+        req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        got = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert_rows_equal(got.rows(), dx.evaluate_merged(pr, keys, 2, sources=blobs), agg, f"vleaf {agg} merged")
+        assert got.stats["general_segments"] == (1 if mixed else 0), got.stats
+        pg = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS).per_glob(2)
+        for gi, (g, w) in enumerate(zip(pg, dx.evaluate_per_glob(pr, keys, 2, sources=blobs))):
+            assert_rows_equal(g, w, agg, f"vleaf {agg} glob {gi}")

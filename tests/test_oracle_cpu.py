@@ -63,3 +63,26 @@ def test_cpu_restatement_synthetic(agg, gbs, null_frac, value_mode):
         assert_rows_equal(g, w, agg, f"glob {gi}")
     assert_rows_equal(cpu.evaluate_merged(pr, blobs, 2, threads=8), dx.evaluate_merged(pr, keys, 2, sources=blobs), agg,
                       "merged")
+
+
+@pytest.mark.parametrize("op,lit,agg", [("gt", "1.5", "sum"), ("le", "0.25", "count"), ("ge", "3", "max")])
+def test_cpu_restatement_value_leaf(op, lit, agg):
+    """Numeric comparison leaves on the value column (the bench's `gt` query) in the C++ restatement == the Python
+    oracle, with NULL values (UNKNOWN) and NaN (sorts greatest)."""
+    import numpy as np  # noqa: F401
+    from lakeside_amd import synth
+    from oracle import cpu, dataexpr as dx
+    blobs = []
+    for i in range(4):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 16, null_frac=0.05, rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        s.free()
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_07"),
+            "q2": {"op": "or", "q1": {"k": dx.VALUE, "v": [lit], "op": op, "dataType": "number"},
+                   "q2": {"k": dx.VALUE, "v": ["100"], "op": "gt", "dataType": "number"}}}
+    segs = [synth.segment_request(i) for i in range(4)]
+    req = json.dumps(synth.pushdown(filt, segs, agg, [synth.SERVICE]))
+    pr = dx.parse_pushdown(req)
+    want = dx.evaluate_merged(pr, [f"s{i}" for i in range(4)], 2, sources=blobs)
+    assert want
+    assert_rows_equal(cpu.evaluate_merged(pr, blobs, 2, threads=4), want, agg, f"cpu value leaf {op} {lit}")
