@@ -255,8 +255,10 @@ const std::vector<const char*>* lk_result::tag_dictionary(size_t c) const {
   }
   if (t.local.empty() && !t.order && t.engine && t.dict_keep && !t.null_value && t.dim_null == t.dict_n &&
       t.ndim == t.dict_n + 1) {
-    bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n, t.dict_keep);   // dim id = engine global id: the shared table
-    return bulk[c].get();
+    if (const auto alive = t.engine_life.lock()) {   // the engine still exists: its cached table
+      bulk[c] = t.engine->dict_ptrs(t.col, t.dict_n, t.dict_keep);   // dim id = engine global id: the shared table
+      return bulk[c].get();
+    }
   }
   auto v = std::make_shared<std::vector<const char*>>(size_t(t.ndim), nullptr);
   if (t.shared) {
@@ -1284,6 +1286,7 @@ Engine::Engine(int dev) : device(dev) {
 }
 
 Engine::~Engine() {
+  life.reset();   // results' weak references expire first
   (void)hipSetDevice(device);
   comm_destroy();
   ctx_free.clear();

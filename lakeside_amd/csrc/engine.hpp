@@ -260,6 +260,9 @@ struct Engine {
   // distributed group-dim unions, latest per column (DimUnion); used under comm_mu
   std::unordered_map<std::string, std::shared_ptr<DimUnion>> unions;
 
+  // Lifetime token: results hold a weak reference, so a result read after its engine was destroyed builds its own
+  // pointer tables instead of dereferencing the engine.
+  std::shared_ptr<const char> life = std::make_shared<const char>('\0');
   explicit Engine(int dev);
   ~Engine();
   GlobalDict& dict(const std::string& col);
@@ -314,6 +317,7 @@ struct lk_result {
     const char* null_value = nullptr;            // the tag's value for dim_null (nullptr: tag dropped)
     lk::Engine* engine = nullptr;                // bulk export of an engine-dictionary column: its name and the
     std::string col;                             //   dictionary size of this evaluation
+    std::weak_ptr<const char> engine_life;       // expires with the engine: the export then builds its own table
     size_t dict_n = 0;
   };
   std::vector<TagCol> tcols;

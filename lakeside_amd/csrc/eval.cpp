@@ -236,21 +236,33 @@ struct MinNanApart {};
 enum Redo : unsigned { REDO_METRICS_RAW = 1u, REDO_MIN_APART = 2u };
 }  // namespace
 
-static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
-                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo);
+static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
+                         int glob_size, unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo);
+static int evaluate_mixed_steps(Engine& E, const std::string& json, const Request& R, const char* const* paths,
+                                size_t n_paths, int glob_size, unsigned flags, const int32_t* shard, bool dist,
+                                lk_result* res);
 
-// Metrics: the worker groups by the raw timestamp (`GROUP BY "_cardinalhq.timestamp"`, BaseExpr.scala:376-394); the
-// segment index picks segments whose frequency equals the step (`metric_seg.frequency_ms = ?`,
-// QueryEngineV2.scala:746-752), so timestamps normally sit on the step grid and a bucket per step is exact.  When a
-// row's timestamp is off that grid (the kernel flags it; every rank sees the flag), the evaluation runs again with
-// one bucket per millisecond: the cell key is then the raw timestamp (a sparse key space: the hash table).
-int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
-             unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
+// Globs whose head segment requests carry different steps (Commons.scala:232, 376-378: each glob's SQL is generated
+// from pushDownRequest.copy(segmentRequests = group), i.e. with that glob's head stepInMillis).
+static bool mixed_steps(const Request& R, int glob_size) {
+  if (R.is_tag_query || !R.has_chart || glob_size <= 0) return false;
+  int64_t step = 0;
+  for (size_t i = 0; i < R.segments.size(); i += size_t(glob_size)) {
+    const int64_t s = R.segments[i].step;
+    if (s <= 0) return false;   // (the single-step path reports it)
+    if (step && s != step) return true;
+    step = s;
+  }
+  return false;
+}
+
+static int evaluate_req(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
+                        int glob_size, unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
   // Both re-runs are thrown before anything is written to *res, and every rank throws them together (agreed flags).
   unsigned redo = 0;
   for (;;) {
     try {
-      return evaluate_once(E, json, paths, n_paths, glob_size, flags, shard, dist, res, redo);
+      return evaluate_once(E, Rp, paths, n_paths, glob_size, flags, shard, dist, res, redo);
     } catch (const MetricsUnaligned&) {
       if (redo & REDO_METRICS_RAW) throw PlanError(LK_ERR_DEVICE, "internal: metrics re-run flagged again");
       redo |= REDO_METRICS_RAW;
@@ -261,8 +273,145 @@ int evaluate(Engine& E, const std::string& json, const char* const* paths, size_
   }
 }
 
-static int evaluate_once(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
-                         unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo) {
+// Metrics: the worker groups by the raw timestamp (`GROUP BY "_cardinalhq.timestamp"`, BaseExpr.scala:376-394); the
+// segment index picks segments whose frequency equals the step (`metric_seg.frequency_ms = ?`,
+// QueryEngineV2.scala:746-752), so timestamps normally sit on the step grid and a bucket per step is exact.  When a
+// row's timestamp is off that grid (the kernel flags it; every rank sees the flag), the evaluation runs again with
+// one bucket per millisecond: the cell key is then the raw timestamp (a sparse key space: the hash table).
+int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
+             unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
+  const std::shared_ptr<const Request> Rp = E.parse_cached(json);
+  if (n_paths == Rp->segments.size() && mixed_steps(*Rp, glob_size <= 0 ? 10 : glob_size))
+    return evaluate_mixed_steps(E, json, *Rp, paths, n_paths, glob_size <= 0 ? 10 : glob_size, flags, shard, dist, res);
+  return evaluate_req(E, Rp, paths, n_paths, glob_size, flags, shard, dist, res);
+}
+
+// Globs of different steps: one evaluation per step over its globs (each glob keeps its own step, as each glob's SQL
+// does), then the rows combined as query-api combines the globs' streams: per glob as they are, or merged per
+// (timestamp, tag map) -- sum / count added, min / max by java.lang.Math.min / max (NaN absorbs, -0.0 < +0.0), avg as
+// the merged sum over the merged count (two evaluations per step: sum and count).  Tags are materialized per row.
+static int evaluate_mixed_steps(Engine& E, const std::string& json, const Request& R, const char* const* paths,
+                                size_t n_paths, int glob_size, unsigned flags, const int32_t* shard, bool dist,
+                                lk_result* res) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
+  const std::string& agg = R.aggregation;
+  if (agg != "sum" && agg != "min" && agg != "max" && agg != "count" && agg != "avg")
+    throw PlanError(LK_ERR_UNSUPPORTED, "globs with different steps under aggregation " + agg);
+  const size_t G = size_t(glob_size), ng = (n_paths + G - 1) / G;
+  std::vector<std::pair<int64_t, std::vector<size_t>>> groups;   // step -> its globs, in order of first appearance
+  for (size_t g = 0; g < ng; g++) {
+    const int64_t s = R.segments[g * G].step;
+    auto it = std::find_if(groups.begin(), groups.end(), [&](const auto& p) { return p.first == s; });
+    if (it == groups.end()) groups.emplace_back(s, std::vector<size_t>{g});
+    else it->second.push_back(g);
+  }
+  struct Out {
+    int64_t ts;
+    uint32_t glob;
+    double v, v2;   // value (avg merged: sum) / avg merged: count
+    std::vector<std::pair<std::string, std::string>> tags;   // the row's tag map, sorted by name
+  };
+  std::vector<Out> rows;
+  std::vector<std::string> names;   // tag names, first-seen order
+  double scan_ms = 0;
+  const bool avg_merged = agg == "avg" && !per_glob_rows;
+  for (auto& grp : groups) {
+    std::vector<const char*> sp;
+    std::vector<int32_t> ssh;
+    std::vector<SegmentReq> ss;
+    for (size_t g : grp.second)
+      for (size_t i = g * G; i < std::min(n_paths, (g + 1) * G); i++) {
+        sp.push_back(paths[i]);
+        ss.push_back(R.segments[i]);
+        if (shard) ssh.push_back(shard[i]);
+      }
+    for (int pass = 0; pass < (avg_merged ? 2 : 1); pass++) {
+      auto sub = std::make_shared<Request>(parse_request(json));
+      sub->segments = ss;
+      if (avg_merged) sub->aggregation = pass == 0 ? "sum" : "count";
+      lk_result r;
+      evaluate_req(E, sub, sp.data(), sp.size(), glob_size, flags, shard ? ssh.data() : nullptr, dist, &r);
+      const size_t nt = r.tag_names.size();
+      for (size_t c = 0; c < nt; c++)
+        if (std::find(names.begin(), names.end(), r.tag_names[c]) == names.end()) names.push_back(r.tag_names[c]);
+      for (size_t i = 0; i < r.nrows; i++) {
+        Out o{r.ts[i], uint32_t(grp.second[r.per_glob ? r.glob[i] : 0]), r.val[i], 0.0, {}};
+        for (size_t c = 0; c < nt; c++)
+          if (const char* v = r.tag(i, c)) o.tags.emplace_back(r.tag_names[c], v);
+        std::sort(o.tags.begin(), o.tags.end());
+        if (avg_merged && pass == 1) {
+          o.v2 = o.v;
+          o.v = 0.0;
+        }
+        rows.push_back(std::move(o));
+      }
+      const char* k = strstr(r.stats.c_str(), "\"scan_ms\":");
+      if (k) scan_ms += atof(k + 10);
+    }
+  }
+  if (!per_glob_rows) {   // query-api merge per (timestamp, tag map), in first-arrival order
+    std::vector<Out> m;
+    std::map<std::pair<int64_t, std::vector<std::pair<std::string, std::string>>>, size_t> at;
+    auto jmin = [](double a, double b) {   // java.lang.Math.min
+      if (a != a) return a;
+      if (a == 0.0 && b == 0.0 && std::signbit(b)) return b;
+      return a <= b ? a : b;
+    };
+    auto jmax = [](double a, double b) {   // java.lang.Math.max
+      if (a != a) return a;
+      if (a == 0.0 && b == 0.0 && std::signbit(a)) return b;
+      return a >= b ? a : b;
+    };
+    for (auto& o : rows) {
+      auto key = std::make_pair(o.ts, o.tags);
+      auto it = at.find(key);
+      if (it == at.end()) {
+        at.emplace(std::move(key), m.size());
+        o.glob = 0;
+        m.push_back(std::move(o));
+        continue;
+      }
+      Out& x = m[it->second];
+      if (agg == "min") x.v = jmin(x.v, o.v);
+      else if (agg == "max") x.v = jmax(x.v, o.v);
+      else {
+        x.v += o.v;
+        x.v2 += o.v2;
+      }
+    }
+    if (avg_merged)
+      for (auto& o : m) o.v = o.v / o.v2;
+    rows.swap(m);
+  }
+  std::stable_sort(rows.begin(), rows.end(), [](const Out& a, const Out& b) {
+    return a.ts != b.ts ? a.ts < b.ts : a.glob < b.glob;
+  });
+  res->exemplar = true;   // tags materialized per row (ex_tags)
+  res->per_glob = per_glob_rows;
+  res->alloc_rows(rows.size());
+  res->tag_names = names;
+  res->ex_tags.assign(rows.size() * names.size(), nullptr);
+  for (size_t i = 0; i < rows.size(); i++) {
+    res->ts[i] = rows[i].ts;
+    res->val[i] = rows[i].v;
+    res->glob[i] = rows[i].glob;
+    res->gid[i] = uint32_t(i);
+    for (auto& kv : rows[i].tags) {
+      const size_t c = size_t(std::find(names.begin(), names.end(), kv.first) - names.begin());
+      res->owned.push_back(kv.second);
+      res->ex_tags[i * names.size() + c] = res->owned.back().c_str();
+    }
+  }
+  char buf[200];
+  snprintf(buf, sizeof buf, "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"step_groups\":%zu,\"table\":\"per_step\"}", scan_ms,
+           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), groups.size());
+  res->stats = buf;
+  return LK_OK;
+}
+
+static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
+                         int glob_size, unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo) {
   const bool metrics_raw = (redo & REDO_METRICS_RAW) != 0;
   auto t_start = std::chrono::steady_clock::now();
   // Distributed calls issue collectives: one at a time per engine, in the same order on every rank.  Every call
@@ -277,7 +426,6 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
   auto stage = [&](const char* what) {
     if (plan_timing) fprintf(stderr, "[lk plan] %-10s %.3f ms\n", what, ms_since(t_start));
   };
-  const std::shared_ptr<const Request> Rp = E.parse_cached(json);
   const Request& R = *Rp;
   stage("parse");
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
@@ -622,7 +770,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
     if (tagq) continue;
     if (g.step <= 0) throw PlanError(LK_ERR_ARG, "stepInMillis must be positive");
     if (step < 0) step = g.step;
-    else if (g.step != step) throw PlanError(LK_ERR_UNSUPPORTED, "globs with different steps");
+    else if (g.step != step) throw PlanError(LK_ERR_DEVICE, "internal: globs with different steps (evaluate splits them)");
   }
 
   // A tag query's single bucket: ts - ts % 2^62 = 0 for every |ts| < 2^62, so bucket_base = 0 and one bucket.
@@ -1926,6 +2074,7 @@ static int evaluate_once(Engine& E, const std::string& json, const char* const* 
       tc.dict = tc.dict_keep.get();
     }
     tc.engine = &E;
+    tc.engine_life = E.life;
     tc.col = sc.name;
     tc.dict_n = sc.dict_n;
     if (sc.exchanged) {   // the agreed union's text table, shared (no copy): 10M-value dims cost nothing here

@@ -384,10 +384,12 @@ def _worker_fault(rank, world, port):
         paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
         agg = case["request"]["baseExpr"]["chart"]["aggregation"]
         # (stage, reduce shape env): the dense gather, the key-range all-to-all legs, the hash-record gather
-        stages = [("reduce@1", {}), ("reduce@0", {}), ("gather@1", {}),
-                  ("reduce@1", {"LK_KEYRANGE_MIN_CELLS": "1"}), ("keyrange_merge@1", {"LK_KEYRANGE_MIN_CELLS": "1"}),
-                  ("keyrange_merge@0", {"LK_KEYRANGE_MIN_CELLS": "1"}), ("emit@1", {"LK_KEYRANGE_MIN_CELLS": "1"}),
-                  ("records@1", {"LK_DENSE_MAX_CELLS": "1"}), ("gather@0", {"LK_DENSE_MAX_CELLS": "1"})]
+        dense = {"LK_KEYRANGE_MIN_CELLS": str(1 << 60)}   # the dense gather to rank 0 (not the key-range path)
+        kr = {"LK_KEYRANGE_MIN_CELLS": "1"}
+        hashed = {"LK_DENSE_MAX_CELLS": "1", "LK_KEYRANGE_MIN_CELLS": str(1 << 60)}
+        stages = [("reduce@1", dense), ("reduce@0", dense), ("gather@1", dense), ("gather@0", dense),
+                  ("reduce@1", kr), ("keyrange_merge@1", kr), ("keyrange_merge@0", kr), ("emit@1", kr), ("emit@0", kr),
+                  ("records@1", hashed), ("gather@0", hashed), ("gather@1", hashed)]
         for stage, env in stages:
             for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS"):
                 os.environ.pop(k, None)
@@ -463,8 +465,12 @@ def _worker_numeric(rank, world, port, paths):
                 raise
             if rank == 0:
                 want = dx.evaluate_merged(dx.parse_pushdown(req), paths, 2)
-                assert_rows_equal(res.rows(), want, agg, f"dist numeric {agg}")
-                assert res.stats["general_segments"] > 0, res.stats
+                try:
+                    assert_rows_equal(res.rows(), want, agg, f"dist numeric {agg}")
+                    assert res.stats["general_segments"] > 0, res.stats
+                except AssertionError as e:
+                    print(f"rank 0: {agg} mismatch: {str(e)[:2000]} stats {res.stats}", flush=True)
+                    raise
             else:
                 assert len(res) == 0
         dist.barrier()

@@ -396,3 +396,22 @@ def test_lean_direct_table_planes(engine):
             assert list(hashed.ts) == list(merged.ts) and hashed.tags == merged.tags
             if agg not in ("sum", "avg"):
                 assert np.array_equal(hashed.values.view(np.uint64), merged.values.view(np.uint64))
+
+
+def test_result_outlives_engine():
+    """a result's tags (bulk export of an engine-dictionary column) are readable after its engine was
+    destroyed -- the result keeps the dictionary block and builds its own pointer table."""
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd.evaluator import Engine
+    e = Engine(0)
+    s = synth.make_segment(synth.segment_spec(3, rows=1 << 16, rg_rows=1 << 15, page_rows=1 << 13))
+    e.put_segment_ptr("outlive/0", s.ptr, s.size)
+    s.free()
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), [synth.segment_request(3)],
+                                    "sum", [synth.SERVICE]))
+    res = e.eval_pushdown(req, ["outlive/0"], 10, LK_MERGED)
+    n = len(res)
+    e.close()
+    tags = res.tags
+    assert n > 0 and len(tags) == n
+    assert sum(1 for t in tags if t.get(synth.SERVICE, "").startswith("svc-")) > n // 2

