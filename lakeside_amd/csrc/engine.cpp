@@ -1090,6 +1090,7 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
   // ---- 4. upload: the streams through the pinned staging area (filled in parallel), then the metadata blob ----
   std::lock_guard<std::mutex> dg(dev_mu);
   HIP_CHECK(hipSetDevice(device));
+  if (!load_stream) HIP_CHECK(hipStreamCreateWithFlags(&load_stream, hipStreamNonBlocking));
   HIP_CHECK(hipMalloc(&S->d_data, S->data_bytes));
   {
     // every stream, with its destination offset, cut at staging-piece boundaries
@@ -1116,15 +1117,25 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
       // the copies overlapping [lo, hi): split into ~8 MB work items
       std::vector<Copy> work;
       while (ci0 < copies.size() && copies[ci0].dst + copies[ci0].len <= lo) ci0++;
+      size_t cur = lo;   // the alignment gaps are zeroed (src == nullptr): reads past a stream's end see zeros
       for (size_t c = ci0; c < copies.size() && copies[c].dst < hi; c++) {
         size_t a = std::max(lo, copies[c].dst), b = std::min(hi, copies[c].dst + copies[c].len);
+        if (a > cur) work.push_back(Copy{nullptr, a - cur, cur - lo});
         for (size_t x = a; x < b; x += size_t(8) << 20) {
           const size_t y = std::min(b, x + (size_t(8) << 20));
           work.push_back(Copy{copies[c].src + (x - copies[c].dst), y - x, x - lo});
         }
+        cur = std::max(cur, b);
       }
-      parallel_for(work.size(), threads, [&](size_t w) { memcpy(pin + work[w].dst, work[w].src, work[w].len); });
-      HIP_CHECK(hipMemcpy(S->d_data + lo, pin, hi - lo, hipMemcpyHostToDevice));
+      if (cur < hi) work.push_back(Copy{nullptr, hi - cur, cur - lo});
+      parallel_for(work.size(), threads, [&](size_t w) {
+        if (work[w].src) memcpy(pin + work[w].dst, work[w].src, work[w].len);
+        else memset(pin + work[w].dst, 0, work[w].len);
+      });
+      // explicit stream + synchronize: a copy from pinned memory may still be reading `pin` when a plain hipMemcpy
+      // returns, and the next piece (or segment) rewrites it
+      HIP_CHECK(hipMemcpyAsync(S->d_data + lo, pin, hi - lo, hipMemcpyHostToDevice, load_stream));
+      HIP_CHECK(hipStreamSynchronize(load_stream));
     }
   }
   size_t meta = align_up(S->tiles.size() * sizeof(TileDesc));
@@ -1157,7 +1168,8 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
       if (p.kind != PAGE_DICT || p.bw > 32) c.pages_lean_late = false;
     }
   }
-  HIP_CHECK(hipMemcpy(S->d_meta, blob.data(), off, hipMemcpyHostToDevice));
+  HIP_CHECK(hipMemcpyAsync(S->d_meta, blob.data(), off, hipMemcpyHostToDevice, load_stream));
+  HIP_CHECK(hipStreamSynchronize(load_stream));   // `blob` is freed on return
   // the segment now references its chunk dictionaries' ids (released by ~Segment)
   S->engine = this;
   for (auto& c : S->cols)
@@ -1292,6 +1304,7 @@ Engine::~Engine() {
   ctx_free.clear();
   cache.clear();
   if (load_pinned) (void)hipHostFree(load_pinned);
+  if (load_stream) (void)hipStreamDestroy(load_stream);
 }
 
 std::unique_ptr<CallCtx> Engine::acquire_ctx() {

@@ -221,6 +221,7 @@ struct Engine {
   int load_thread_count() const;
   void* load_pinned = nullptr;
   size_t load_pinned_cap = 0;
+  hipStream_t load_stream = nullptr;
   double load_host_ms_total = 0, load_ms_total = 0;   // cumulative (lk_engine_stats)
   // evict LRU segments (never `keep`) until cache_bytes + extra <= budget; caller holds cache_mu
   size_t evict_lru_locked(size_t target_bytes, const std::string& keep, std::vector<std::shared_ptr<Segment>>* out);

@@ -537,7 +537,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       throw PlanError(LK_ERR_UNSUPPORTED, "column " + nm + " used both as a string and as a number");
   if (2 + strs.size() + nums.size() > size_t(MAXQCOL)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter columns");
   if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
-  if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& s) { return s.name == kTimestamp || s.name == vcol; }) != strs.end())
+  // (a tag query's tag may be the value / timestamp column: numeric, it takes the TAGNUM row scan below)
+  if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& s) {
+        return (s.name == kTimestamp || s.name == vcol) && !(tagq && s.name == R.tag_name && s.leaves.empty());
+      }) != strs.end())
     throw PlanError(LK_ERR_UNSUPPORTED, "filters / groupBys on the timestamp or value column");
   std::vector<LeafInfo> leaves;
   for (size_t s = 0; s < strs.size(); s++) {
@@ -1366,7 +1369,8 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     const uint32_t cw = (kagg == AGG_SUM ? 2u : 1u) + (rows_plane ? 1u : 0u);
     // the most replicas per cell (spreading lanes that add into the same cells over more LDS addresses) that still
     // leave room for a tile spanning two buckets
-    for (uint32_t rep = 4; rep >= 1; rep /= 2) {
+    const uint32_t rep_max = getenv("LK_DIRECT_REPMAX") ? uint32_t(atoi(getenv("LK_DIRECT_REPMAX"))) : 4u;   // env: A/B
+    for (uint32_t rep = rep_max >= 64 ? 64u : rep_max >= 16 ? 16u : rep_max >= 8 ? 8u : 4u; rep >= 1; rep /= 2) {
       const uint64_t w = std::min<uint64_t>(LEAN_DIR_MAXSPAN, words / (uint64_t(cw) * rep * std::max<uint64_t>(ngroups, 1)));
       if (w >= 2 || (rep == 1 && w >= 1)) {
         P.dir_span = uint32_t(w);

@@ -238,7 +238,8 @@ __global__ __launch_bounds__(BLOCK) void ex_scan(XParams X) {
         const bool w8 = h.kind == PAGE_PLAIN64;
         const bool bl = h.kind == PAGE_BOOL && uint32_t(qc) == X.tag_qc;   // BOOLEAN: a numeric tag only
         if (!w8 && h.kind != PAGE_PLAIN32 && !bl) ok = false;
-        const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len);
+        // (BOOLEAN: bit-packed bytes read as whole dwords -- the slack keeps the stream's last dword in range)
+        const __amdgpu_buffer_rsrc_t rs = make_rsrc(h.vals, h.vals_len + (bl ? 4u : 0u));
         uint64_t raw = 0;
         if (w8) {
           const v2u w = __builtin_amdgcn_raw_buffer_load_b64(rs, ok ? vi * 8u : OOB, 0, 0);

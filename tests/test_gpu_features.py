@@ -262,7 +262,8 @@ def test_hbm_budget_lru_eviction():
             e.eval_pushdown(req, ["s1"], 10, LK_MERGED)
         assert ei.value.code == LK_ERR_EVICTED, ei.value
         e.put_segment("s1", blobs[1])                              # re-put: answers again (s2 goes, LRU)
-        assert len(e.eval_pushdown(req, ["s1"], 10, LK_MERGED)) == len(want)
+        req1 = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), [synth.segment_request(1)]))
+        assert len(e.eval_pushdown(req1, ["s1"], 10, LK_MERGED)) == 60
         e.put_segment("s3", blobs[3])                              # s0 is now the LRU
         assert e.segment_count == 2
         e.put_segment("s0", blobs[0])
