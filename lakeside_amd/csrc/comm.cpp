@@ -207,28 +207,35 @@ struct HostComm final : Comm {
   void gather_to_root(Engine& E, CallCtx& X, const void* send, void* recv, const std::vector<size_t>& bytes,
                       const std::vector<size_t>& off) override {
     if (world == 1) return;
-    // each rank's block travels behind an 8-byte status: a rank whose device copy failed still takes part in the
-    // all-gather, and every rank then throws that failure (none is left inside the collective)
+    // each rank's block travels behind a fixed header -- 8-byte status + the first bytes of its message: a rank whose
+    // device copy failed still takes part in the all-gather, and every rank then throws that failure (none is left
+    // inside the collective)
+    constexpr size_t H = 128;
     size_t mx = 1;
     for (size_t b : bytes) mx = std::max(mx, b);
-    std::vector<uint8_t> mine(8 + mx, 0), all(size_t(world) * (8 + mx));
+    std::vector<uint8_t> mine(H + mx, 0), all(size_t(world) * (H + mx));
     uint64_t status = 0;
     comm_local(X, [&] {
       fault_point(E, "gather");
       HIP_TRY2(hipSetDevice(E.device));
       if (bytes[size_t(rank)]) {
-        HIP_TRY2(hipMemcpyAsync(mine.data() + 8, send, bytes[size_t(rank)], hipMemcpyDeviceToHost, X.stream));
+        HIP_TRY2(hipMemcpyAsync(mine.data() + H, send, bytes[size_t(rank)], hipMemcpyDeviceToHost, X.stream));
         HIP_TRY2(hipStreamSynchronize(X.stream));
       }
     });
-    if (X.pend_code) status = uint64_t(uint32_t(X.pend_code));
+    if (X.pend_code) {
+      status = uint64_t(uint32_t(X.pend_code));
+      memcpy(mine.data() + 8, X.pend_msg.data(), std::min(X.pend_msg.size(), H - 9));
+    }
     memcpy(mine.data(), &status, 8);
-    allgather(mine.data(), 8 + mx, all.data());
+    allgather(mine.data(), H + mx, all.data());
     for (int r = 0; r < world; r++) {
       uint64_t st;
-      memcpy(&st, all.data() + size_t(r) * (8 + mx), 8);
+      const uint8_t* blk = all.data() + size_t(r) * (H + mx);
+      memcpy(&st, blk, 8);
       if (st) {
-        const std::string m = r == rank ? X.pend_msg : "rank " + std::to_string(r) + ": device copy of its table failed";
+        const std::string m = r == rank ? X.pend_msg
+                                        : "rank " + std::to_string(r) + ": " + reinterpret_cast<const char*>(blk + 8);
         X.pend_code = 0;
         X.pend_msg.clear();
         throw PlanError(int(st), m);
@@ -237,7 +244,7 @@ struct HostComm final : Comm {
     if (rank == 0) {   // the last step of the gather: rank 0 alone
       for (int r = 1; r < world; r++)
         if (bytes[size_t(r)])
-          HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * (8 + mx) + 8,
+          HIP_TRY2(hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[size_t(r)], all.data() + size_t(r) * (H + mx) + H,
                                   bytes[size_t(r)], hipMemcpyHostToDevice, X.stream));
       HIP_TRY2(hipStreamSynchronize(X.stream));   // `all` is freed on return
     }

@@ -438,7 +438,9 @@ struct ChunkOut {
                                           // `runs`; d.remap: index into `dict`
   std::vector<RunDesc> runs;
   std::vector<std::string> dict;          // strings: the dictionary page's values, then every PLAIN page's own values
-  std::deque<std::vector<uint8_t>> plain; // decompressed / re-encoded pages (streams and zone maps read them)
+  // decompressed / re-encoded pages (streams, zone maps and dictionary views point into them): heap-held so the
+  // buffers stay put when the ChunkOut moves
+  std::vector<std::unique_ptr<std::vector<uint8_t>>> plain;
   uint64_t compressed = 0;
   int code = 0;                           // LK_ERR_IO: the file is corrupt; LK_ERR_UNSUPPORTED: this column's shape
   std::string msg;
@@ -449,6 +451,10 @@ struct ChunkOut {
     return off;
   }
 };
+
+// A vector<ChunkOut> that reallocates must move its elements (a copy would re-allocate `plain` and leave every
+// StreamRef / host_vals / dictionary view pointing at freed buffers).
+static_assert(std::is_nothrow_move_constructible<ChunkOut>::value, "ChunkOut must move without copying");
 
 PageStreams split_page(const pq::PageHeader& h, const uint8_t* data, size_t n, bool nullable) {
   PageStreams s;
@@ -519,8 +525,8 @@ void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32
       if (h.uncompressed < 0 || lv > n || lv > size_t(h.uncompressed))
         throw PlanError(LK_ERR_IO, "parquet: bad page sizes");
       if (h.type != pq::DATA_PAGE_V2 || h.v2_compressed) {
-        C.plain.emplace_back(size_t(h.uncompressed));
-        std::vector<uint8_t>& out = C.plain.back();
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>(size_t(h.uncompressed)));
+        std::vector<uint8_t>& out = *C.plain.back();
         if (lv) memcpy(out.data(), data, lv);
         pq::decompress(m.codec, data + lv, n - lv, out.data() + lv, out.size() - lv);
         data = out.data();
@@ -626,8 +632,8 @@ void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32
         int pbw = 1;
         while (pbw < 32 && (1ull << pbw) < page_dict_n) pbw++;
         const size_t ngroups = (size_t(nvals) + 7) / 8;
-        C.plain.emplace_back();
-        std::vector<uint8_t>& enc = C.plain.back();
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>());
+        std::vector<uint8_t>& enc = *C.plain.back();
         enc.push_back(uint8_t(pbw));
         for (uint64_t hdr = (uint64_t(ngroups) << 1) | 1u;; hdr >>= 7) {   // literal-run header (ULEB128)
           enc.push_back(uint8_t((hdr & 0x7f) | (hdr >= 0x80 ? 0x80 : 0)));
@@ -682,8 +688,8 @@ void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32
         if (bw > 32) throw PlanError(LK_ERR_IO, "parquet: bad dictionary index bit width");
         std::vector<uint32_t> idx(nvals);
         pq::hybrid_decode(st.vals_len ? st.vals + 1 : st.vals, st.vals_len ? st.vals_len - 1 : 0, bw, nvals, idx.data());
-        C.plain.emplace_back(size_t(nvals) * width);
-        std::vector<uint8_t>& out = C.plain.back();
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>(size_t(nvals) * width));
+        std::vector<uint8_t>& out = *C.plain.back();
         for (uint32_t i = 0; i < nvals; i++) {
           if (idx[i] >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
           memcpy(out.data() + size_t(i) * width, ndict.data() + size_t(idx[i]) * width, width);
@@ -1002,6 +1008,7 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
   {   // drop unloaded columns (and their chunks) from the index
     std::vector<HostCol> kept;
     std::vector<ChunkOut> kept_chunks;
+    kept_chunks.reserve(chunks.size());
     S->by_name.clear();
     for (size_t ci = 0; ci < ncol; ci++) {
       if (!keep[ci]) continue;

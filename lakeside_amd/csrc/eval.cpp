@@ -539,7 +539,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   if (all_leaves.size() > size_t(MAXLEAF)) throw PlanError(LK_ERR_UNSUPPORTED, "too many filter leaves");
   // (a tag query's tag may be the value / timestamp column: numeric, it takes the TAGNUM row scan below)
   if (std::find_if(strs.begin(), strs.end(), [&](const StrCol& s) {
-        return (s.name == kTimestamp || s.name == vcol) && !(tagq && s.name == R.tag_name && s.leaves.empty());
+        return (s.name == kTimestamp || s.name == vcol) && !(tagq && s.name == R.tag_name);
       }) != strs.end())
     throw PlanError(LK_ERR_UNSUPPORTED, "filters / groupBys on the timestamp or value column");
   std::vector<LeafInfo> leaves;
