@@ -1059,8 +1059,8 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // query even when the leading group dim -- a tag query's tag, a :by column -- is not the filter's early column.
   std::vector<int> dev_of(strs.size());
   for (size_t i = 0; i < strs.size(); i++) dev_of[i] = int(i);
-  // (opt-in until its GPU run: LK_EARLY_FIRST=1)
-  if (late_mask && early > 0 && strs.size() <= 3 && getenv("LK_EARLY_FIRST")) {
+  // (LK_NO_EARLY_FIRST=1: the r03 order, for A/B)
+  if (late_mask && early > 0 && strs.size() <= 3 && !getenv("LK_NO_EARLY_FIRST")) {
     std::swap(dev_of[0], dev_of[size_t(early)]);
     uint32_t m = 0;
     for (size_t i = 0; i < strs.size(); i++)
