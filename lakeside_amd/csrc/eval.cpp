@@ -1681,14 +1681,16 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
             wst = LK_ERR_DEVICE;
         }
         if (hipStreamSynchronize(st) != hipSuccess) wst = LK_ERR_DEVICE;
+        std::string wmsg = "shared result block: mapping or write failed";
         if (!wst && getenv("LK_FAULT")) {   // tests only: an injected failure of the row write
           try {
             fault_point(E, "emit");
-          } catch (const PlanError&) {
+          } catch (const PlanError& e) {
             wst = LK_ERR_DEVICE;
+            wmsg = e.what();
           }
         }
-        comm_agree(E, *X, wst, "shared result block: mapping or write failed");   // every range written
+        comm_agree(E, *X, wst, wmsg);   // every range written
         comm_emit_end(E);   // every rank holds its mapping: the block names can go
         if (rank == 0) {
           nrows_out = uint32_t(total_rows);

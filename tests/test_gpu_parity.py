@@ -527,5 +527,5 @@ def test_numeric_tag_high_cardinality_regrowth(engine):
         os.environ.pop("LK_TAGNUM_INIT_SLOTS")
     assert res.stats["attempts"] > 1 and res.stats["table"] == "tagnum", res.stats
     want = dx.evaluate_tag_merged(dx.parse_pushdown(text), tag, keys, 10, sources=blobs)
-    assert len(want) > 1000
+    assert len(want) >= 1000   # (synthetic values: 1000 distinct integers)
     assert sorted(res.tags, key=_tag_key) == sorted(want, key=_tag_key)
