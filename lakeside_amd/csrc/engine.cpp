@@ -1022,10 +1022,15 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
   const size_t nc = S->cols.size();
 
   // ---- 2. per column, in row-group order: intern dictionaries, concatenate runs and pages, place streams ----
-  std::vector<size_t> chunk_base(chunks.size());   // byte offset of each chunk's stream area in the segment
+  // Byte offset of each chunk's stream area in the segment: row-group major (a row group's columns side by side, as
+  // in the file), so the streams one tile reads lie close together (column-major placement measured ~1.8x slower
+  // scans; LK_COLMAJOR=1 keeps it for A/B).
+  std::vector<size_t> chunk_base(chunks.size());
   {
+    const bool colmajor = getenv("LK_COLMAJOR") != nullptr;
     size_t off = 0;
-    for (size_t k = 0; k < chunks.size(); k++) {
+    for (size_t i = 0; i < chunks.size(); i++) {
+      const size_t k = colmajor || nrg == 0 ? i : (i % nc) * nrg + i / nc;   // i = rg * nc + column
       off = (off + 127) / 128 * 128;
       chunk_base[k] = off;
       off += chunks[k].bytes;
@@ -1109,6 +1114,8 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     std::vector<Copy> copies;
     for (size_t k = 0; k < chunks.size(); k++)
       for (const StreamRef& r : chunks[k].streams) copies.push_back(Copy{r.src, r.len, chunk_base[k] + r.off});
+    // (the piece walk below needs them in destination order)
+    std::sort(copies.begin(), copies.end(), [](const Copy& a, const Copy& b) { return a.dst < b.dst; });
     const size_t piece = std::min<size_t>(S->data_bytes, size_t(1) << 30);
     if (load_pinned_cap < piece) {
       if (load_pinned) HIP_CHECK(hipHostFree(load_pinned));

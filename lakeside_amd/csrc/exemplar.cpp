@@ -926,33 +926,47 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
   res->tag_names = out_cols;
   res->ex_tags.assign(nsel * ncols, nullptr);
   const size_t vcol = size_t(std::find(out_cols.begin(), out_cols.end(), std::string(kValue)) - out_cols.begin());
-  std::set<const void*> kept;   // dictionary blocks already held by the result
   for (size_t i = 0; i < nsel; i++) {
     const Cand& c = *stream[i];
-    const XGlob& g = globs[qseg_glob[c.qseg]];
-    const Segment& S = *qseg_seg[c.qseg];
     res->ts[i] = c.ts;
     res->glob[i] = qseg_glob[c.qseg];
     res->gid[i] = uint32_t(i);
     res->val[i] = 0.0;
-    for (size_t k = 0; k < ncols; k++) {
-      if (!gok[i * ncols + k]) continue;
-      const std::string& name = out_cols[k];
+  }
+  // column by column: each (segment, column)'s physical / union type looked up once, each dictionary locked once
+  std::vector<const HostCol*> qcol(qsegs.size());
+  std::vector<int> qut(qsegs.size());
+  for (size_t k = 0; k < ncols; k++) {
+    const std::string& name = out_cols[k];
+    bool any_string = false;
+    for (size_t q = 0; q < qsegs.size(); q++) {
+      const Segment& S = *qseg_seg[q];
       const int ci = S.col_index(name);
-      const HostCol& hc = S.cols[ci];
-      const unsigned long long raw = gval[i * ncols + k];
+      qcol[q] = ci < 0 ? nullptr : &S.cols[size_t(ci)];
+      if (!qcol[q]) continue;
+      const XGlob& g = globs[qseg_glob[q]];
       const auto ut = g.types.find(name);
-      const int utype = ut == g.types.end() ? hc.ptype : ut->second;
+      qut[q] = ut == g.types.end() ? qcol[q]->ptype : ut->second;
+      any_string = any_string || qcol[q]->is_string;
+    }
+    GlobalDict* gd = any_string ? &E.dict(name) : nullptr;
+    std::unique_lock<std::mutex> dl;
+    if (gd) {
+      dl = std::unique_lock<std::mutex>(gd->mu);
+      res->keep.push_back(gd->vals);   // tag text outlives a compaction
+    }
+    for (size_t i = 0; i < nsel; i++) {
+      if (!gok[i * ncols + k]) continue;
+      const uint32_t q = stream[i]->qseg;
+      const HostCol& hc = *qcol[q];
+      const unsigned long long raw = gval[i * ncols + k];
       if (k == vcol) res->val[i] = value_double(raw, hc.ptype);
       if (hc.is_string) {
-        if (utype != pq::BYTE_ARRAY) throw PlanError(LK_ERR_UNSUPPORTED, "union_by_name over string and numeric " + name);
-        GlobalDict& gd = E.dict(name);
-        std::lock_guard<std::mutex> dg(gd.mu);
-        if (kept.insert(gd.vals.get()).second) res->keep.push_back(gd.vals);   // tag text outlives a compaction
-        const std::string& s = gd[size_t(raw)];
+        if (qut[q] != pq::BYTE_ARRAY) throw PlanError(LK_ERR_UNSUPPORTED, "union_by_name over string and numeric " + name);
+        const std::string& s = (*gd)[size_t(raw)];
         if (!null_like(s)) res->ex_tags[i * ncols + k] = s.c_str();   // Commons.scala:433
       } else {
-        res->owned.push_back(value_text(raw, hc.ptype, utype));
+        res->owned.push_back(value_text(raw, hc.ptype, qut[q]));
         res->ex_tags[i * ncols + k] = res->owned.back().c_str();
       }
     }

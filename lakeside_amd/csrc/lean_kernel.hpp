@@ -437,8 +437,12 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   auto row = [&](int64_t ts, double v, uint32_t dim) __attribute__((always_inline)) {
     if (P.nvl) {   // numeric leaves on the value column (uniform)
       uint32_t bits = 0;
+      // read through the kernarg segment pointer (P is the kernel's only argument): a runtime index into the by-value
+      // argument would copy it to scratch, and an unrolled loop holds every leaf's bounds in SGPRs
+      const VLeaf* vls = static_cast<const QParams*>((const void*)__builtin_amdgcn_kernarg_segment_ptr())->vl;
+#pragma unroll 1
       for (uint32_t k = 0; k < P.nvl; k++) {
-        const VLeaf& vl = P.vl[k];
+        const VLeaf vl = vls[k];
         const bool pass = v != v ? vl.nan_pass != 0u
                                  : ((v > vl.lo || (vl.lo_incl && v == vl.lo)) && (v < vl.hi || (vl.hi_incl && v == vl.hi)));
         bits |= uint32_t(pass) << k;

@@ -166,10 +166,14 @@ def test_c3_shape_and_regex_by2_max_with_nulls(engine):
     _synth_case(engine, 4, 1 << 19, 1, 0.05, filt, "max", [synth.SERVICE, synth.NAMESPACE])
 
 
-def test_late_materialization_paths(engine):
+@pytest.mark.parametrize("late_chunk", [False, True], ids=["per_row", "late_chunk"])
+def test_late_materialization_paths(engine, late_chunk, monkeypatch):
     """NULL-free tiles take the late path: the early column (a conjunct on one column alone, name first) is
-    decoded for every row, every other string column only for rows the early conjuncts pass."""
+    decoded for every row, every other string column only for rows the early conjuncts pass -- per listed row
+    (default) or per 16-row chunk (LK_LATE_CHUNK=1: scan_lean<..., EARLY>)."""
     from lakeside_amd import synth
+    if late_chunk:
+        monkeypatch.setenv("LK_LATE_CHUNK", "1")
     c3 = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_07"),
           "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
     _synth_case(engine, 3, 1 << 19, 1, 0.0, c3, "max", [synth.SERVICE, synth.NAMESPACE])          # C3 shape
