@@ -266,7 +266,7 @@ def main():
     # alone), committed under profiles/ -- read here only when it profiled this query at this size.
     traffic, traffic_src = None, None
     pmc_file = None
-    for rnd in ("r03", "r02"):   # the newest committed PMC summary of this query
+    for rnd in ("r04", "r03", "r02"):   # the newest committed PMC summary of this query
         cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.query}.json")
         if os.path.exists(cand):
             pmc_file = cand
