@@ -112,6 +112,8 @@ struct Comm {
 
 namespace {
 
+constexpr size_t kCommPinBytes = size_t(64) << 10;
+
 struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
   ~RcclComm() override {
@@ -122,14 +124,44 @@ struct RcclComm final : Comm {
     if (!active()) return {mine};
     HIP_TRY2(hipSetDevice(E.device));
     hipStream_t st = X.stream;
-    uint64_t* dsz = static_cast<uint64_t*>(X.workspace("comm_sizes", size_t(world) * 8));
     std::vector<uint64_t> sz(size_t(world), 0);
-    sz[size_t(rank)] = mine.size();
-    HIP_TRY2(hipMemcpyAsync(dsz + rank, &sz[size_t(rank)], 8, hipMemcpyHostToDevice, st));
-    NCCL_TRY(ncclAllGather(dsz + rank, dsz, 1, ncclUint64, comm, st));
-    cnt.allgathers++;
-    HIP_TRY2(hipMemcpyAsync(sz.data(), dsz, size_t(world) * 8, hipMemcpyDeviceToHost, st));
-    HIP_TRY2(hipStreamSynchronize(st));
+    // One all-gather of fixed slots ([length | bytes], through pinned host memory) carries every rank's blob when
+    // each fits its slot -- the agreement points' status blobs always do; a larger blob takes a second all-gather
+    // sized by the lengths the first one delivered.
+    constexpr size_t SLOT = 512;
+    if (size_t(world + 1) * SLOT <= kCommPinBytes) {
+      if (!X.comm_pin) HIP_TRY2(hipHostMalloc(&X.comm_pin, kCommPinBytes));
+      uint8_t* h = static_cast<uint8_t*>(X.comm_pin);
+      uint8_t* d = static_cast<uint8_t*>(X.workspace("comm_slots", size_t(world) * SLOT));
+      const uint64_t n = mine.size();
+      memcpy(h, &n, 8);
+      if (n <= SLOT - 8 && n) memcpy(h + 8, mine.data(), n);
+      HIP_TRY2(hipMemcpyAsync(d + size_t(rank) * SLOT, h, SLOT, hipMemcpyHostToDevice, st));
+      NCCL_TRY(ncclAllGather(d + size_t(rank) * SLOT, d, SLOT, ncclUint8, comm, st));
+      cnt.allgathers++;
+      cnt.allgather_bytes += uint64_t(world) * SLOT;
+      HIP_TRY2(hipMemcpyAsync(h + SLOT, d, size_t(world) * SLOT, hipMemcpyDeviceToHost, st));
+      HIP_TRY2(hipStreamSynchronize(st));
+      bool fits = true;
+      for (int r = 0; r < world; r++) {
+        memcpy(&sz[size_t(r)], h + SLOT * size_t(r + 1), 8);
+        fits = fits && sz[size_t(r)] <= SLOT - 8;
+      }
+      if (fits) {
+        std::vector<std::string> out(static_cast<size_t>(world));
+        for (int r = 0; r < world; r++)
+          out[size_t(r)].assign(reinterpret_cast<const char*>(h + SLOT * size_t(r + 1) + 8), size_t(sz[size_t(r)]));
+        return out;
+      }
+    } else {
+      uint64_t* dsz = static_cast<uint64_t*>(X.workspace("comm_sizes", size_t(world) * 8));
+      sz[size_t(rank)] = mine.size();
+      HIP_TRY2(hipMemcpyAsync(dsz + rank, &sz[size_t(rank)], 8, hipMemcpyHostToDevice, st));
+      NCCL_TRY(ncclAllGather(dsz + rank, dsz, 1, ncclUint64, comm, st));
+      cnt.allgathers++;
+      HIP_TRY2(hipMemcpyAsync(sz.data(), dsz, size_t(world) * 8, hipMemcpyDeviceToHost, st));
+      HIP_TRY2(hipStreamSynchronize(st));
+    }
     uint64_t mx = 1;
     for (uint64_t x : sz) mx = std::max(mx, x);
     uint8_t* d = static_cast<uint8_t*>(X.workspace("comm_blobs", size_t(world) * mx));

@@ -1382,6 +1382,7 @@ CallCtx::~CallCtx() {
   for (auto& w : ws)
     if (w.second.p) (void)hipFree(w.second.p);
   if (pinned) (void)hipHostFree(pinned);
+  if (comm_pin) (void)hipHostFree(comm_pin);
   if (ev_scan0) (void)hipEventDestroy(ev_scan0);
   if (ev_scan1) (void)hipEventDestroy(ev_scan1);
   if (stream) (void)hipStreamDestroy(stream);

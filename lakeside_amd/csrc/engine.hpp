@@ -125,6 +125,7 @@ struct CallCtx {
   std::map<std::string, Workspace> ws;
   void* pinned = nullptr;
   size_t pinned_cap = 0;
+  void* comm_pin = nullptr;   // distributed calls: pinned slots of the small all-gathers (comm.cpp, kCommPinBytes)
   // Distributed calls: a rank-local failure met after a collective step, held until the next agreement point (an
   // all-gather every rank takes) so that every rank fails together instead of leaving peers inside a collective.
   int pend_code = 0;
