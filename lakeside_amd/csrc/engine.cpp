@@ -69,6 +69,38 @@ struct DeviceError : std::runtime_error {
 static constexpr size_t kAlign = 256;
 static inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) / a * a; }
 
+// fn(0..n-1) on up to `threads` threads (the calling thread among them); the first exception is rethrown
+template <class F>
+static void parallel_for(size_t n, int threads, F&& fn) {
+  const size_t T = std::max<size_t>(1, std::min<size_t>(size_t(threads), n));
+  if (T <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex err_mu;
+  auto work = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      try {
+        fn(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!err) err = std::current_exception();
+        next.store(n);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < T; t++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
+}
+
+
 // ------------------------------------------------------------------------------------------------
 // engine-global dictionaries: one per column name; chunk dictionaries remap into them at load
 // ------------------------------------------------------------------------------------------------
@@ -187,11 +219,37 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   o->n = n;
   o->keys.resize(n);
   o->perm.resize(n);
-  for (size_t i = 0; i < n; i++) {
-    o->keys[i] = value_key(*v[i]);
-    o->perm[i] = uint32_t(i);
+  const int T = n >= (size_t(1) << 16) ? load_thread_count() : 1;
+  const size_t hb = (n + size_t(T) * 4 - 1) / (size_t(T) * 4);
+  parallel_for(n ? (n + hb - 1) / hb : 0, T, [&](size_t b) {
+    for (size_t i = b * hb; i < std::min(n, (b + 1) * hb); i++) {
+      o->keys[i] = value_key(*v[i]);
+      o->perm[i] = uint32_t(i);
+    }
+  });
+  if (T > 1) {
+    // uniform 128-bit hash keys: one scatter into 2^16 buckets by the top bits of `hi`, then every bucket sorted on
+    // its own (in parallel) -- instead of the radix sort's 8 scatter passes
+    std::vector<size_t> cnt(65537, 0);
+    for (size_t i = 0; i < n; i++) cnt[(o->keys[i].hi >> 48) + 1]++;
+    for (size_t d = 1; d <= 65536; d++) cnt[d] += cnt[d - 1];
+    std::vector<std::pair<Key128, uint32_t>> kv(n);
+    {
+      std::vector<size_t> pos(cnt.begin(), cnt.end() - 1);
+      for (size_t i = 0; i < n; i++) kv[pos[o->keys[i].hi >> 48]++] = {o->keys[i], o->perm[i]};
+    }
+    parallel_for(256, T, [&](size_t g) {
+      for (size_t d = g * 256; d < (g + 1) * 256; d++)
+        std::sort(kv.begin() + long(cnt[d]), kv.begin() + long(cnt[d + 1]),
+                  [](const std::pair<Key128, uint32_t>& a, const std::pair<Key128, uint32_t>& b) { return a.first < b.first; });
+    });
+    for (size_t i = 0; i < n; i++) {
+      o->keys[i] = kv[i].first;
+      o->perm[i] = kv[i].second;
+    }
+  } else {
+    radix_sort_keys(o->keys, o->perm);
   }
-  radix_sort_keys(o->keys, o->perm);
   for (size_t i = 1; i < n; i++)   // two distinct values of one dictionary on one 128-bit key: refuse, never merge
     if (o->keys[i] == o->keys[i - 1])
       throw PlanError(LK_ERR_UNSUPPORTED, "dictionary of " + col + ": 128-bit value-key collision");
@@ -839,35 +897,6 @@ void build_tiles_rg(const Segment& S, const std::vector<std::vector<HostPage>>& 
 
 // Runs fn(i) for i in [0, n) on up to `threads` threads (the calling thread included); the first exception is
 // rethrown after every worker has finished.
-template <class F>
-void parallel_for(size_t n, int threads, F&& fn) {
-  const size_t T = std::max<size_t>(1, std::min<size_t>(size_t(threads), n));
-  if (T <= 1) {
-    for (size_t i = 0; i < n; i++) fn(i);
-    return;
-  }
-  std::atomic<size_t> next{0};
-  std::exception_ptr err;
-  std::mutex err_mu;
-  auto work = [&]() {
-    for (;;) {
-      const size_t i = next.fetch_add(1);
-      if (i >= n) return;
-      try {
-        fn(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(err_mu);
-        if (!err) err = std::current_exception();
-        next.store(n);
-      }
-    }
-  };
-  std::vector<std::thread> pool;
-  for (size_t t = 1; t < T; t++) pool.emplace_back(work);
-  work();
-  for (auto& th : pool) th.join();
-  if (err) std::rethrow_exception(err);
-}
 
 }  // namespace
 
@@ -1053,8 +1082,24 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     if (col.is_string && ndict) {
       GlobalDict& gd = dict(col.name);
       std::lock_guard<std::mutex> g(gd.mu);
+      std::vector<const std::string*> sv;
+      sv.reserve(ndict);
       for (size_t rg = 0; rg < nrg; rg++)
-        for (const std::string& v : chunks[ci * nrg + rg].dict) col.remap.push_back(gd.intern(v));
+        for (const std::string& v : chunks[ci * nrg + rg].dict) sv.push_back(&v);
+      col.remap.assign(ndict, UINT32_MAX);
+      if (ndict >= (size_t(1) << 16) && threads > 1) {
+        // large dictionaries (a 10M-value group column): values already known are looked up in parallel -- reads
+        // only, under this thread's lock -- and only the new ones interned below, in order (ids stay deterministic)
+        const size_t blk = (ndict + size_t(threads) * 4 - 1) / (size_t(threads) * 4);
+        parallel_for((ndict + blk - 1) / blk, threads, [&](size_t b) {
+          for (size_t i = b * blk; i < std::min(ndict, (b + 1) * blk); i++) {
+            auto it = gd.ids.find(*sv[i]);
+            if (it != gd.ids.end()) col.remap[i] = it->second;
+          }
+        });
+      }
+      for (size_t i = 0; i < ndict; i++)
+        if (col.remap[i] == UINT32_MAX) col.remap[i] = gd.intern(*sv[i]);
     }
     uint32_t remap_base = 0;
     for (size_t rg = 0; rg < nrg; rg++) {
