@@ -1355,6 +1355,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric && !(vleaf && gsegs.empty())) P.lean = 0;   // the general row scan accumulates every table field
+  if (P.lean && getenv("LK_NO_DENSE_DIRECT")) P.lean |= LEAN_NO_DENSE_DIRECT;   // env: A/B only
   if (vleaf && !qsegs.empty()) {   // scan_lean tests the value leaves of every row its string conjuncts pass
     P.nvl = uint32_t(nleaves.size());
     P.vtab = vtab;

@@ -224,6 +224,8 @@ constexpr uint32_t LEAN_NO_CNT = 1u, LEAN_NO_ROWS = 2u;
 // "hi != -0.0" says the cell exists and `rows` needs no atomic either: one scattered atomic per flushed cell instead
 // of two or three (fixup_table restores rows / cnt and hi = +0.0 of empty cells).
 constexpr uint32_t LEAN_SUM_EXISTS = 4u;
+// LEAN_NO_DENSE_DIRECT (env LK_NO_DENSE_DIRECT, A/B only): dense blocks accumulate through the register cell too
+constexpr uint32_t LEAN_NO_DENSE_DIRECT = 8u;
 constexpr unsigned long long NEG_ZERO_BITS = 0x8000000000000000ull;
 
 }  // namespace lk

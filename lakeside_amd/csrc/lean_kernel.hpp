@@ -389,6 +389,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   const uint32_t step32 = uint32_t(P.step);
   // dense-block test only where a quarter or more of the chunk dictionary's codes pass (uniform; C2's 1 of 16 skips it)
   const bool dense_codes = NL == 0 && 4u * npass >= dict_n;
+  // dense blocks over several passing codes: rows straight into the direct table (`row`'s `direct`)
+  const bool dense_direct = dense_codes && npass > 1 && !(P.lean & LEAN_NO_DENSE_DIRECT);
   bool late_trivial = true;   // no filter leaf on a late column: the late stage only adds group terms (uniform)
 #pragma unroll
   for (int k = 0; k < NL; k++) late_trivial = late_trivial && P.strp[1 + k].lmask == 0u;
@@ -784,6 +786,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         const bool contig = live && valid == 0xffffu && v0 == v0l + 16u * uint32_t(lane);
         if (__ballot(contig) == ~0ull && __popcll(__ballot(__popc(f16) >= 2u)) >= 48) {
           const uint32_t rb0 = uni(rbase);
+          // several passing codes over one bucket's direct table: rows go straight to their cell (uniform)
+          const uint64_t jt = uint64_t(tile_b - tbl);
+          const bool ddir = dense_direct && one_bucket && !P.nvl && tspan && jt < tspan;
+          const uint32_t dbase = ddir ? uint32_t(jt) * ngr * rep + myrep : 0u;
           // The owner lane's 16 codes as 16 BW-bit fields in (c0, c1, c2) -- an RLE chunk's code replicated -- with
           // the pass bits in the spare high bits (BW <= 5), so a reader takes its code and pass bit with 1-3 cross-lane
           // reads instead of six.
@@ -826,10 +832,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
               }
             }
 #pragma unroll
-            for (int u = 0; u < 4; u++)
-              if (pp[u])
-                row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x),
-                    __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x)), dd[u]);
+            for (int u = 0; u < 4; u++) {
+              if (!pp[u]) continue;
+              const double v = __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x));
+              if (ddir) {   // uniform: straight into the direct-table cell (neighbouring rows rarely share it)
+                const uint32_t x = dbase + dd[u] * rep;
+                min_nan_check<AGG>(P, true, v);
+                if (AGG == AGG_SUM) {
+                  const double h = v + 0.0;   // never -0.0 (the empty marker)
+                  const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
+                  double s, e;
+                  two_sum(old, h, s, e);
+                  if (e != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), e);
+                } else if (AGG == AGG_MIN) {
+                  atomicMin(rv + x, dbl_order(v));
+                } else if (AGG == AGG_MAX) {
+                  atomicMax(rv + x, dbl_order(v));
+                } else {
+                  atomicAdd(rv + x, 1ull);
+                }
+                if (rrows_on) atomicAdd(rrows + x, 1ull);
+              } else {
+                row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), v, dd[u]);
+              }
+            }
           }
           m = 0;
         }
