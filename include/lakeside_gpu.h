@@ -49,13 +49,16 @@ enum {
 #define LK_PLAN_BYTES 4u      /* optional, with either: the scan kernel counts the bytes its plan reads
                                  (lk_result_stats "plan_bytes"; measurement only, costs ~5% of scan time) */
 
-/* options_json: {"device": 0, "hbm_budget_bytes": N, "max_calls": 4, "dict_compact_min_dead": 1024}; NULL = defaults.
+/* options_json: {"device": 0, "hbm_budget_bytes": N, "max_calls": 4, "dict_compact_min_dead": 1024,
+ *                "load_threads": 0}; NULL = defaults.
  * hbm_budget_bytes: weight bound of the HBM segment cache (the worker's Caffeine cache weight,
  * query-worker/.../WorkerApi.scala:53-64): inserting past it evicts least-recently-used segments; 0 (default) = no
  * bound, eviction only when HBM runs out.  max_calls: evaluations in flight (one stream each).
  * dict_compact_min_dead: engine dictionaries (one per column, value -> id) count the cached segments' references to
  * every id; once evictions leave at least max(live ids, this) ids unreferenced, the next load or evaluation renumbers
  * the live ids densely first, so group-dim spaces track the cached segments (results keep their strings).
+ * load_threads: host threads of a segment load (page walk, decompression, staging copies); 0 (default) = the
+ * process's OMP_NUM_THREADS share of the host's cores, at most 16.
  * Replaces DuckDbConnectionFactory (core/.../utils/DuckDbConnectionFactory.scala:76-114). */
 int lk_engine_create(const char* options_json, lk_engine** out);
 void lk_engine_destroy(lk_engine* e);

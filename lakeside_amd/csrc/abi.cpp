@@ -67,6 +67,8 @@ int lk_engine_create(const char* options_json, lk_engine** out) {
         if (const lk::Json* c = o.get("max_calls")) e->e->max_calls = size_t(std::max<int64_t>(1, c->as_i64()));
         if (const lk::Json* d = o.get("dict_compact_min_dead"))
           e->e->compact_min_dead = size_t(std::max<int64_t>(1, d->as_i64()));
+        if (const lk::Json* t = o.get("load_threads"))
+          e->e->load_threads = int(std::min<int64_t>(64, std::max<int64_t>(0, t->as_i64())));
       }
     } catch (...) {
       delete e;

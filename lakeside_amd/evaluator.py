@@ -132,12 +132,15 @@ class Result:
 class Engine:
     """One per process per GPU: HIP device, stream, HBM segment cache, optional RCCL communicator."""
 
-    def __init__(self, device: int = 0, hbm_budget_bytes: int = 0, max_calls: int = 4, dict_compact_min_dead: int = 0):
+    def __init__(self, device: int = 0, hbm_budget_bytes: int = 0, max_calls: int = 4, dict_compact_min_dead: int = 0,
+                 load_threads: int = 0):
         L = _lib.lib()
         h = ctypes.c_void_p()
         opts = {"device": device, "hbm_budget_bytes": int(hbm_budget_bytes), "max_calls": int(max_calls)}
         if dict_compact_min_dead:
             opts["dict_compact_min_dead"] = int(dict_compact_min_dead)
+        if load_threads:
+            opts["load_threads"] = int(load_threads)
         check(L.lk_engine_create(json.dumps(opts).encode(), ctypes.byref(h)))
         self._h = h
         self.device = device

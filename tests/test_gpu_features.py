@@ -272,6 +272,35 @@ def test_hbm_budget_lru_eviction():
         e.close()
 
 
+def test_load_threads_identical_segments(tmp_path):
+    """The parallel ingest (lk_engine_create load_threads) builds the same segment as a single-threaded load: a
+    multi-row-group, compressed, multi-page file answers identically (rows, values, tags) with 1 and 8 threads."""
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, synth
+    from lakeside_amd.evaluator import Engine
+    s = synth.make_segment(synth.segment_spec(0, rows=1 << 18, rg_rows=1 << 15, page_rows=1 << 12))
+    raw = tmp_path / "raw.parquet"
+    raw.write_bytes(s.bytes())
+    s.free()
+    t = pq.read_table(str(raw))
+    path = str(tmp_path / "zstd.parquet")
+    strings = [c for c in t.column_names if str(t.schema.field(c).type) == "string"]
+    pq.write_table(t, path, compression="zstd", use_dictionary=strings, row_group_size=1 << 15, data_page_size=8192)
+    req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "in", "metric_03", "metric_07"), [synth.segment_request(0)],
+                                    group_bys=[synth.SERVICE]))
+    out = []
+    for threads in (1, 8):
+        e = Engine(0, load_threads=threads)
+        try:
+            e.load_segment(path)
+            r = e.eval_pushdown(req, [path], 10, LK_MERGED)
+            out.append((r.rows(), r.stats.get("tiles")))
+        finally:
+            e.close()
+    assert len(out[0][0]) > 0 and out[0][1] == out[1][1]
+    assert_rows_equal(out[1][0], out[0][0], "sum", "load_threads 8 vs 1")
+
+
 def test_lean_kernel_late_columns(engine):
     """scan_lean with late string columns (name early; the others decoded per listed row): a group dim only
     (every listed row passes, loads issued together), a late regex filter + 2 group dims, a high-cardinality late
