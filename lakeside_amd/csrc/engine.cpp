@@ -495,7 +495,9 @@ struct ChunkOut {
   std::vector<HostPage> pages;            // d.vals / d.defs: offsets in the chunk's area; run_lo / drun_lo: indices into
                                           // `runs`; d.remap: index into `dict`
   std::vector<RunDesc> runs;
-  std::vector<std::string> dict;          // strings: the dictionary page's values, then every PLAIN page's own values
+  // strings: the dictionary page's values, then every PLAIN page's own values -- views into the file bytes or `plain`
+  // (both outlive the load), so a 10M-value dictionary is not copied string by string before interning
+  std::vector<std::string_view> dict;
   // decompressed / re-encoded pages (streams, zone maps and dictionary views point into them): heap-held so the
   // buffers stay put when the ChunkOut moves
   std::vector<std::unique_ptr<std::vector<uint8_t>>> plain;
@@ -1082,10 +1084,10 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
     if (col.is_string && ndict) {
       GlobalDict& gd = dict(col.name);
       std::lock_guard<std::mutex> g(gd.mu);
-      std::vector<const std::string*> sv;
+      std::vector<const std::string_view*> sv;
       sv.reserve(ndict);
       for (size_t rg = 0; rg < nrg; rg++)
-        for (const std::string& v : chunks[ci * nrg + rg].dict) sv.push_back(&v);
+        for (const std::string_view& v : chunks[ci * nrg + rg].dict) sv.push_back(&v);
       col.remap.assign(ndict, UINT32_MAX);
       if (ndict >= (size_t(1) << 16) && threads > 1) {
         // large dictionaries (a 10M-value group column): values already known are looked up in parallel -- reads
@@ -1093,13 +1095,13 @@ std::shared_ptr<Segment> Engine::build_segment(const std::string& key, const uin
         const size_t blk = (ndict + size_t(threads) * 4 - 1) / (size_t(threads) * 4);
         parallel_for((ndict + blk - 1) / blk, threads, [&](size_t b) {
           for (size_t i = b * blk; i < std::min(ndict, (b + 1) * blk); i++) {
-            auto it = gd.ids.find(*sv[i]);
+            auto it = gd.ids.find(std::string(*sv[i]));
             if (it != gd.ids.end()) col.remap[i] = it->second;
           }
         });
       }
       for (size_t i = 0; i < ndict; i++)
-        if (col.remap[i] == UINT32_MAX) col.remap[i] = gd.intern(*sv[i]);
+        if (col.remap[i] == UINT32_MAX) col.remap[i] = gd.intern(std::string(*sv[i]));
     }
     uint32_t remap_base = 0;
     for (size_t rg = 0; rg < nrg; rg++) {
