@@ -189,6 +189,8 @@ def main():
     cold = step()
     cold_ms = (time.perf_counter() - tc) * 1e3
     cold_total_ms = cold.stats.get("total_ms")
+    cold_stages = {k: cold.stats.get(k) for k in ("plan_ms", "dims_ms", "dims_rebuilt", "scan_ms", "device_ms",
+                                                   "reduce_ms", "scan_agreed_ms") if k in cold.stats}
     del cold
     res = step()
     if world > 1:
@@ -299,7 +301,8 @@ def main():
             "cold_eval_ms": cold_ms,
             "cold_eval": {"what": "first evaluation of the request after lk_engine_drop_caches (parsed request, "
                                   "leaf outcomes, value-key orders, group-dim unions dropped; segments resident); "
-                                  "wall time of the call", "ms": cold_ms, "engine_total_ms": cold_total_ms},
+                                  "wall time of the call", "ms": cold_ms, "engine_total_ms": cold_total_ms,
+                          "stages": cold_stages},
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "definition": "achieved = plan bytes per launch (counted by the scan kernel: streams "
