@@ -18,6 +18,7 @@
 #include <chrono>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lakeside_gpu.h"
@@ -26,6 +27,24 @@
 #include "plan.hpp"
 
 namespace lk {
+
+namespace {
+// fn(a, b) over [0, n) cut into ranges on up to `threads` threads (the calling thread among them); small n inline
+template <class F>
+void par_ranges(size_t n, int threads, F&& fn) {
+  const size_t T = n < (size_t(1) << 16) ? 1 : size_t(std::max(1, threads));
+  if (T <= 1) {
+    fn(size_t(0), n);
+    return;
+  }
+  const size_t per = (n + T - 1) / T;
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < T; t++)
+    if (t * per < n) pool.emplace_back([&, t] { fn(t * per, std::min(n, (t + 1) * per)); });
+  fn(size_t(0), std::min(n, per));
+  for (auto& th : pool) th.join();
+}
+}  // namespace
 
 namespace {
 
@@ -118,7 +137,12 @@ std::shared_ptr<DimUnion> agree_dim_union(Engine& E, CallCtx& X, const std::stri
     // every rank holds the same value set: U = this rank's sorted keys, nothing to exchange
     u->size = dict_n;
     u->text = std::make_shared<std::vector<const char*>>(size_t(dict_n) + 1, nullptr);
-    for (uint32_t d = 0; d < dict_n; d++) (*u->text)[d] = text_of(own[order->perm[d]]);
+    // (10M values: one cache miss per string, so the walk runs on the load threads)
+    std::vector<const char*>& text = *u->text;
+    const DictOrder& o = *order;
+    par_ranges(dict_n, E.load_thread_count(), [&](size_t a, size_t b) {
+      for (size_t d = a; d < b; d++) text[d] = text_of(own[o.perm[d]]);
+    });
     *dim_of_gid = order->rank;
   } else {
     // 3. all-gather the sorted key sets, merge them into U
@@ -136,11 +160,19 @@ std::shared_ptr<DimUnion> agree_dim_union(Engine& E, CallCtx& X, const std::stri
     u->text = std::make_shared<std::vector<const char*>>(U.size() + 1, nullptr);
     // 4. this rank's global ids -> U positions (merge walk: both sorted); its own values' text
     std::vector<uint32_t> pos_of_key(order->keys.size());
-    for (size_t i = 0, j = 0; i < order->keys.size(); i++) {
-      while (U[j] < order->keys[i]) j++;
-      pos_of_key[i] = uint32_t(j);
-      (*dim_of_gid)[order->perm[i]] = uint32_t(j);
-      (*u->text)[j] = text_of(own[order->perm[i]]);
+    {
+      const DictOrder& o = *order;
+      std::vector<uint32_t>& dg = *dim_of_gid;
+      std::vector<const char*>& text = *u->text;
+      par_ranges(o.keys.size(), E.load_thread_count(), [&](size_t a, size_t b) {   // each range: its own merge walk
+        size_t j = a < b ? size_t(std::lower_bound(U.begin(), U.end(), o.keys[a]) - U.begin()) : 0;
+        for (size_t i = a; i < b; i++) {
+          while (U[j] < o.keys[i]) j++;
+          pos_of_key[i] = uint32_t(j);
+          dg[o.perm[i]] = uint32_t(j);
+          text[j] = text_of(own[o.perm[i]]);
+        }
+      });
     }
     // 5. the values rank 0 lacks, each shipped once by its lowest holder: (position, length, bytes) records
     std::string ship;
