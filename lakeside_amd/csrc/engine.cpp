@@ -230,23 +230,38 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
   if (T > 1) {
     // uniform 128-bit hash keys: one scatter into 2^16 buckets by the top bits of `hi`, then every bucket sorted on
     // its own (in parallel) -- instead of the radix sort's 8 scatter passes
+    // per-range bucket counts, then each range scatters into its own slice of every bucket (parallel, stable)
+    const size_t R = size_t(T), per = (n + R - 1) / R;
+    std::vector<std::vector<size_t>> rc(R, std::vector<size_t>(65536, 0));
+    parallel_for(R, T, [&](size_t r) {
+      for (size_t i = r * per; i < std::min(n, (r + 1) * per); i++) rc[r][o->keys[i].hi >> 48]++;
+    });
     std::vector<size_t> cnt(65537, 0);
-    for (size_t i = 0; i < n; i++) cnt[(o->keys[i].hi >> 48) + 1]++;
-    for (size_t d = 1; d <= 65536; d++) cnt[d] += cnt[d - 1];
-    std::vector<std::pair<Key128, uint32_t>> kv(n);
-    {
-      std::vector<size_t> pos(cnt.begin(), cnt.end() - 1);
-      for (size_t i = 0; i < n; i++) kv[pos[o->keys[i].hi >> 48]++] = {o->keys[i], o->perm[i]};
+    for (size_t d = 0; d < 65536; d++) {
+      size_t at = cnt[d];
+      for (size_t r = 0; r < R; r++) {
+        const size_t c = rc[r][d];
+        rc[r][d] = at;   // range r's first slot in bucket d
+        at += c;
+      }
+      cnt[d + 1] = at;
     }
+    std::vector<std::pair<Key128, uint32_t>> kv(n);
+    parallel_for(R, T, [&](size_t r) {
+      std::vector<size_t>& pos = rc[r];
+      for (size_t i = r * per; i < std::min(n, (r + 1) * per); i++) kv[pos[o->keys[i].hi >> 48]++] = {o->keys[i], o->perm[i]};
+    });
     parallel_for(256, T, [&](size_t g) {
       for (size_t d = g * 256; d < (g + 1) * 256; d++)
         std::sort(kv.begin() + long(cnt[d]), kv.begin() + long(cnt[d + 1]),
                   [](const std::pair<Key128, uint32_t>& a, const std::pair<Key128, uint32_t>& b) { return a.first < b.first; });
     });
-    for (size_t i = 0; i < n; i++) {
-      o->keys[i] = kv[i].first;
-      o->perm[i] = kv[i].second;
-    }
+    parallel_for(R, T, [&](size_t r) {
+      for (size_t i = r * per; i < std::min(n, (r + 1) * per); i++) {
+        o->keys[i] = kv[i].first;
+        o->perm[i] = kv[i].second;
+      }
+    });
   } else {
     radix_sort_keys(o->keys, o->perm);
   }
@@ -254,7 +269,12 @@ std::shared_ptr<const DictOrder> Engine::dict_order(const std::string& col, size
     if (o->keys[i] == o->keys[i - 1])
       throw PlanError(LK_ERR_UNSUPPORTED, "dictionary of " + col + ": 128-bit value-key collision");
   o->rank.resize(n);
-  for (size_t d = 0; d < n; d++) o->rank[o->perm[d]] = uint32_t(d);
+  {
+    const size_t per = (n + size_t(T) - 1) / size_t(T);
+    parallel_for(size_t(T), T, [&](size_t r) {   // disjoint writes (perm is a permutation)
+      for (size_t d = r * per; d < std::min(n, (r + 1) * per); d++) o->rank[o->perm[d]] = uint32_t(d);
+    });
+  }
   // Fingerprint of the value set: MurmurHash3_x64_128 over the sorted keys, chained over 1 MiB blocks.
   uint64_t fp[2] = {uint64_t(n), 0x9e3779b97f4a7c15ull};
   const char* base = reinterpret_cast<const char*>(o->keys.data());
