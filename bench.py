@@ -7,7 +7,13 @@ call.  Weak scaling: every GPU holds `--segments` segments of `--rows` rows (C2:
 request names all N x 64 segments, each rank scans its shard and the partial tables meet on rank 0 over RCCL.
 
     python bench.py                      # N=1, C2
+    python bench.py --gpus 8             # N=8: this process starts the 8 rank processes itself (one per GPU)
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 --master-port P bench.py --gpus 8
+    python bench.py --gpus 2 --comm host # rehearsal: 2 ranks on one GPU over the host transport
+
+At N > 1 every rank times the CPU restatement on its own shard and sends its partial cells to rank 0, which folds
+them with query-api semantics and checks the merged GPU rows against them (`validated`); `cpu_baseline` is the
+whole workload's rows over the slowest rank's shard time.
 """
 import argparse
 import concurrent.futures as cf
@@ -27,6 +33,11 @@ QUERIES = {
     "c2": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
                        "computed": False, "dataType": "string"}, agg="sum", group_bys=[],
                desc=":eq _cardinalhq.name=metric_07 :sum, step 1m"),
+    # C2 at the step query-api picks for windows <= 65 min (QueryApi.scala:297-300): 10 s buckets, so nearly every
+    # 64K-row tile straddles bucket boundaries and the zone maps cannot spare the timestamp column
+    "c2s10": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                          "computed": False, "dataType": "string"}, agg="sum", group_bys=[], step=10000,
+                  desc=":eq _cardinalhq.name=metric_07 :sum, step 10s"),
     # C3 (configs[2]): :and/:re multi-tag predicate + :by 2-key group-by :max
     "c3": dict(filter={"op": "and",
                        "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
@@ -70,6 +81,77 @@ def log(msg):
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def _visible_gpus():
+    """GPUs this job can see, counted in a child process so that this launcher never initialises the GPU itself (it
+    starts the rank processes afterwards)."""
+    import subprocess
+    r = subprocess.run([sys.executable, "-c", "import torch; print(torch.cuda.device_count())"],
+                       capture_output=True, text=True, timeout=600)
+    try:
+        return int(r.stdout.strip().splitlines()[-1])
+    except (ValueError, IndexError):
+        log(f"could not count GPUs: {r.stderr.strip()[-500:]}")
+        return 0
+
+
+def launch_ranks(args):
+    """`bench.py --gpus N` without a launcher (WORLD_SIZE unset): start N rank processes of this script, one per
+    GPU (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* as torch.distributed.run sets them), before any GPU call here, and
+    exit with the worst rank status.  Fewer visible GPUs than N is an error with RCCL (one rank per device); the
+    host transport (--comm host) puts every rank on GPU 0 (a rehearsal of the N-rank protocol on one GPU)."""
+    import signal
+    import subprocess
+    n = args.gpus
+    ndev = _visible_gpus()
+    if args.comm == "rccl" and ndev < n:
+        log(f"error: --gpus {n} needs {n} visible GPUs (one rank per GPU over RCCL), {ndev} visible; "
+            f"use --comm host to rehearse {n} ranks on one GPU")
+        return 2
+    if ndev < 1:
+        log("error: no GPU visible")
+        return 2
+    if args.comm == "host" and n > 16:
+        log("error: at most 16 ranks may share one GPU")
+        return 2
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), LK_BENCH_LAUNCHED="1")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    log(f"launched {n} rank processes (pids {[p.pid for p in procs]}, comm {args.comm}, {ndev} GPUs visible)")
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                c = p.poll()
+                if c is None:
+                    continue
+                live.remove(p)
+                if c != 0:
+                    rc = rc or c
+                    log(f"rank process {p.pid} exited with {c}: stopping the others")
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            time.sleep(0.2)
+    finally:
+        for p in procs:   # our own children only, by pid
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+    return 1 if rc and rc < 0 else rc
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -79,7 +161,7 @@ def main():
     ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
     ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
     ap.add_argument("--cpu-sample", type=int, default=-1,
-                    help="segments timed on the CPU restatement (-1: all = full-size validation; 0: skip)")
+                    help="segments per rank timed on the CPU restatement (-1: all = full-size validation; 0: skip)")
     ap.add_argument("--gen-workers", type=int, default=4)
     ap.add_argument("--comm", default="rccl", choices=["rccl", "host"],
                     help="N > 1 exchange: RCCL over xGMI (default), or the host transport over gloo (rehearsal of the "
@@ -90,11 +172,14 @@ def main():
                          "ncclSend/ncclRecv of the table reduce or the key-range all-to-all) runs on this GPU")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+        log(f"error: --gpus {args.gpus} but WORLD_SIZE={world} (the launcher started a different number of ranks)")
+        sys.exit(2)
 
     import torch
     import torch.distributed as dist
@@ -108,6 +193,10 @@ def main():
         log("note: --dist-loopback applies at N=1 only; ignored")
     if loopback:
         os.environ["LK_COMM_LOOPBACK"] = "1"   # read by lk_comm_init
+    if args.comm == "rccl" and local_rank >= torch.cuda.device_count():
+        log(f"error: rank {rank} (local rank {local_rank}) has no GPU of its own: "
+            f"{torch.cuda.device_count()} visible")
+        sys.exit(2)
     device = local_rank if args.comm == "rccl" else 0
     torch.cuda.set_device(device)
     eng = Engine(device)
@@ -120,6 +209,9 @@ def main():
     elif loopback:
         eng.comm_init(Engine.unique_id(), 1, 0)
     use_dist = world > 1 or loopback
+    comm_desc = eng.stats.get("comm") if use_dist else None
+    if use_dist:
+        log(f"rank {rank}: communicator {comm_desc}")
 
     # ---- segments of this rank (weak scaling: rank r owns global segments [r*S, (r+1)*S)) ----
     q = QUERIES[args.query]
@@ -134,8 +226,8 @@ def main():
         return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour,
                                                         highcard_n=highcard))
 
-    # The CPU baseline / validator (rank 0 at N=1) reads the same Parquet bytes: keep them in host memory.
-    keep_cpu = rank == 0 and world == 1 and args.cpu_sample != 0
+    # The CPU baseline / validator reads the same Parquet bytes: every rank keeps its shard in host memory.
+    keep_cpu = args.cpu_sample != 0 and not q.get("tag") and not q.get("exemplar")
     kept = {}
     t0 = time.time()
     bytes_loaded = 0
@@ -158,11 +250,15 @@ def main():
         f"{load_s / S * 1e3:.0f} ms/segment; synthesis + load {time.time() - t0:.0f}s)")
 
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(total)]
-    if q.get("exemplar"):
-        req = json.dumps({"baseExpr": {"id": "A", "dataset": "logs", "filter": q["filter"], "limit": q["exemplar"]},
-                          "segmentRequests": segs})
-    else:
-        req = json.dumps(synth.pushdown(q["filter"], segs, q["agg"], q["group_bys"], tag=q.get("tag")))
+
+    def request(seg_reqs):
+        if q.get("exemplar"):
+            return json.dumps({"baseExpr": {"id": "A", "dataset": "logs", "filter": q["filter"],
+                                            "limit": q["exemplar"]}, "segmentRequests": seg_reqs})
+        return json.dumps(synth.pushdown(q["filter"], seg_reqs, q["agg"], q["group_bys"], tag=q.get("tag")))
+
+    req = request(segs)
+    local_req = request([segs[i] for i in mine])   # this rank's shard alone
 
     def step(extra=0):
         if use_dist:
@@ -170,14 +266,10 @@ def main():
         return eng.eval_pushdown(req, keys, 10, LK_MERGED | extra)
 
     # Plan bytes (the roofline numerator) are a property of the query and the data: counted by the kernel in one
-    # untimed call (LK_PLAN_BYTES costs ~5% of scan time), then the timed steps run without the counter.
-    if world == 1:
-        pbytes = float(eng.eval_pushdown(req, keys, 10, LK_MERGED | LK_PLAN_BYTES).stats.get("plan_bytes", 0))
-    else:   # per GPU: this rank's shard alone (the same scan work it does inside the distributed call)
-        local = json.dumps(synth.pushdown(q["filter"], [segs[i] for i in mine], q["agg"], q["group_bys"],
-                                          tag=q.get("tag")))
-        pbytes = float(eng.eval_pushdown(local, [keys[i] for i in mine], 10, LK_MERGED | LK_PLAN_BYTES)
-                       .stats.get("plan_bytes", 0))
+    # untimed call (LK_PLAN_BYTES costs ~5% of scan time), then the timed steps run without the counter.  Per GPU:
+    # this rank's shard alone (the same scan work it does inside the distributed call).
+    pbytes = float(eng.eval_pushdown(local_req, [keys[i] for i in mine], 10, LK_MERGED | LK_PLAN_BYTES)
+                   .stats.get("plan_bytes", 0))
     for _ in range(args.warmup):
         res = step()
     # Cold evaluation: the request as if never seen -- parse, leaf-outcome, value-key-order and group-dim caches
@@ -218,6 +310,11 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    avg = lambda xs: sum(xs) / len(xs)   # noqa: E731
+    per_rank = {"rank": rank, "device": device, "segments": S, "scan_kernel_ms": avg(scan_ms),
+                "eval_ms": elapsed * 1e3 / args.steps, "dims_ms": avg(dims_ms), "reduce_ms": avg(reduce_ms),
+                "scan_agreed_ms": avg(agreed_ms), "plan_bytes": pbytes, "comm": comm_desc}
+    ranks_info = [per_rank]
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -225,10 +322,12 @@ def main():
         o = torch.tensor([out_rows], dtype=torch.int64)
         dist.all_reduce(o, op=dist.ReduceOp.MAX)
         out_rows = int(o.item())
+        ranks_info = [None] * world
+        dist.all_gather_object(ranks_info, per_rank)
     ms_per_step = elapsed * 1e3 / args.steps
     rows_total = total * args.rows
     value = rows_total / (ms_per_step / 1e3)
-    scan_avg = sum(scan_ms) / len(scan_ms)
+    scan_avg = avg(scan_ms)
     # Roofline numerator: the bytes the late-materialized plan must read, counted by the scan kernel (streams it
     # decodes in full + distinct 128-B lines of its per-row gathers + tile metadata), per launch.
     achieved = pbytes / (scan_avg / 1e3) / 1e9
@@ -236,10 +335,9 @@ def main():
     log(f"rank {rank}: scan kernel {scan_avg:.3f} ms avg (min {min(scan_ms):.3f}), eval {ms_per_step:.3f} ms/step, "
         f"plan bytes {pbytes / 1e9:.2f} GB/launch -> {achieved:.0f} GB/s ({achieved / HBM_PEAK_GBS:.3f} of peak); "
         f"SURVEY algorithmic {alg_bytes / 1e9:.2f} GB -> {alg_gbs:.0f} GB/s; {out_rows} output rows; in the call: "
-        f"plan {sum(plan_ms) / len(plan_ms):.2f} ms, device {sum(device_ms) / len(device_ms):.2f} ms, "
-        f"total {sum(total_ms) / len(total_ms):.2f} ms" +
-        (f"; group-dim agreement {sum(dims_ms) / len(dims_ms):.2f} ms, reduce {res.stats.get('reduce')}, "
-         f"emit {res.stats.get('emit')}, reduce stage {sum(reduce_ms) / len(reduce_ms):.3f} ms, "
+        f"plan {avg(plan_ms):.2f} ms, device {avg(device_ms):.2f} ms, total {avg(total_ms):.2f} ms" +
+        (f"; group-dim agreement {avg(dims_ms):.2f} ms, reduce {res.stats.get('reduce')}, "
+         f"emit {res.stats.get('emit')}, reduce stage {avg(reduce_ms):.3f} ms, "
          f"collectives {res.stats.get('collectives')}" if use_dist else "") + f"; cold eval {cold_ms:.2f} ms")
 
     # measured device-to-device copy rate on this GPU (a stream-copy peak beside the spec peak)
@@ -258,17 +356,18 @@ def main():
         del a, b
 
     cpu, validated = None, None
-    if keep_cpu and not q.get("tag") and not q.get("exemplar"):
-        cpu, validated = cpu_baseline_and_validate(args, q, req, [kept[i] for i in mine], res)
+    if keep_cpu:
+        cpu, validated = cpu_baseline_and_validate(args, q, local_req, [kept[i] for i in mine], res, world, rank,
+                                                   dist if world > 1 else None)
     for sgm in kept.values():
         sgm.free()
 
     # HBM traffic of the scan kernel(s) per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same bench
-    # command (scripts/gpu_bench_prof.sh -> scripts/pmc_traffic.py; separate runs, as counters must be collected
+    # command (scripts/gpu_bench_prof.sh -> scripts/pmc_summary.py; separate runs, as counters must be collected
     # alone), committed under profiles/ -- read here only when it profiled this query at this size.
     traffic, traffic_src = None, None
     pmc_file = None
-    for rnd in ("r04", "r03", "r02"):   # the newest committed PMC summary of this query
+    for rnd in ("r05", "r04", "r03", "r02"):   # the newest committed PMC summary of this query
         cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.query}.json")
         if os.path.exists(cand):
             pmc_file = cand
@@ -289,7 +388,7 @@ def main():
             "data": f"synthetic sealed Parquet (tools/synth.cpp, seed 20240101+i), {S} x {args.rows} rows per GPU",
             "config": {"workload": f"{args.query.upper()}: {total} segments x {args.rows} rows, {q['desc']}",
                        "segments_per_gpu": S, "rows_per_segment": args.rows, "glob_size": 10,
-                       "parallelism": f"segment-sharded x{world}" + ((", RCCL table reduce" if args.comm == "rccl" else ", host-transport table reduce (rehearsal)") if world > 1 else "")},
+                       "parallelism": f"segment-sharded x{world}" + ((", RCCL table reduce" if args.comm == "rccl" else ", host-transport table reduce (rehearsal: every rank on GPU 0)") if world > 1 else "")},
             "datapoints_per_sec": out_rows / (ms_per_step / 1e3),
             "load": {"what": "Parquet bytes -> HBM segment cache (lk_segment_put: footer, page walk, run tables, "
                              "dictionary remap, upload), synthetic generation excluded; not in value",
@@ -307,7 +406,8 @@ def main():
                          "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "definition": "achieved = plan bytes per launch (counted by the scan kernel: streams "
                                        "decoded in full + distinct 128-B lines of every per-row gather + tile "
-                                       "metadata) / scan-kernel time (HIP events on the call's stream). `value` "
+                                       "metadata) / scan-kernel time (HIP events on the call's stream), rank 0's "
+                                       "shard at N > 1. `value` "
                                        "counts every row of the workload as scanned, including rows of tiles whose "
                                        "load-time zone map (timestamp min/max per tile) pins them to a single "
                                        "bucket: their timestamps are never read, and value lines with no passing "
@@ -321,14 +421,17 @@ def main():
             "cpu_baseline": cpu,
         }
         if use_dist:   # the distributed call's own stages (rank 0): group-dim agreement, table reduce, row emission
-            line["dist"] = {"dims_ms": sum(dims_ms) / len(dims_ms), "reduce": res.stats.get("reduce"),
+            line["comm_world"] = (comm_desc or {}).get("world")
+            line["dist"] = {"dims_ms": avg(dims_ms), "reduce": res.stats.get("reduce"),
                             "emit": res.stats.get("emit"), "comm": args.comm,
+                            "communicator": comm_desc,
                             "loopback": loopback,
-                            "scan_agreed_ms": sum(agreed_ms) / len(agreed_ms),
-                            "reduce_ms": sum(reduce_ms) / len(reduce_ms),
+                            "scan_agreed_ms": avg(agreed_ms),
+                            "reduce_ms": avg(reduce_ms),
                             "collectives_per_query": res.stats.get("collectives"),
                             "allgathers": res.stats.get("allgathers"), "allgather_bytes": res.stats.get("allgather_bytes"),
-                            "p2p_groups": res.stats.get("p2p_groups"), "p2p_bytes": res.stats.get("p2p_bytes")}
+                            "p2p_groups": res.stats.get("p2p_groups"), "p2p_bytes": res.stats.get("p2p_bytes"),
+                            "ranks": ranks_info}
             if loopback:
                 line["config"]["parallelism"] = ("segment-sharded x1 through lk_eval_pushdown_dist on a world-1 RCCL "
                                                  "communicator in loopback (every collective of the N>1 path runs)")
@@ -348,13 +451,20 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline_and_validate(args, q, req, segs, gpu_res):
-    """The CPU restatement (oracle/cpu: C++17 + OpenMP over the same in-memory Parquet bytes, every host core of
-    this job) timed on the workload, and the GPU's merged rows checked against its rows.  A reported baseline,
-    not the target (the reference's JVM + DuckDB cannot run here)."""
+def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0, dist=None):
+    """The CPU restatement (oracle/cpu: C++17 + OpenMP over the same in-memory Parquet bytes, the job's CPU share)
+    timed on this rank's shard, and the GPU's merged rows checked against it.  A reported baseline, not the target
+    (the reference's JVM + DuckDB cannot run here).
+
+    N > 1: every rank evaluates its own shard (concurrently over RCCL -- one rank per GPU, each with its own CPU share
+    -- or one rank after another when the ranks share one GPU's CPU share, --comm host) and sends its per-glob partial
+    cells to rank 0, which folds them with query-api semantics (TimeGroupedSketchAggregator.scala:74-92: add, min, max
+    per (timestamp, tags)) and compares the result with the distributed call's merged rows.  Columnar throughout
+    (oracle.cpu.evaluate_cell_table / merge_cell_table, tests.parity.result_columns), so millions of rows (C5) check
+    in seconds."""
     from oracle import cpu as lkcpu
     from oracle import dataexpr as dx
-    from tests.parity import assert_rows_equal
+    from tests.parity import result_columns
     # The job's CPU share: the affinity mask, capped by OMP_NUM_THREADS where the pool sets it (the GPU box allots
     # 16 host cores per GPU and sets OMP_NUM_THREADS=16; os.cpu_count() there is the whole host).
     affinity = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
@@ -362,34 +472,68 @@ def cpu_baseline_and_validate(args, q, req, segs, gpu_res):
     threads = min(affinity, int(omp)) if omp else affinity
     n = len(segs) if args.cpu_sample < 0 else min(len(segs), args.cpu_sample)
     blobs = [(s.ptr, s.size) for s in segs[:n]]
-    pr = dx.parse_pushdown(req)
-    if n < len(segs):   # a sample: the request over the sampled segments only
-        body = json.loads(req)
-        body["segmentRequests"] = body["segmentRequests"][:n]
-        pr = dx.parse_pushdown(json.dumps(body))
-    lkcpu.evaluate_merged(pr, blobs, 10, threads)   # warm (page-in, thread pool)
-    times = []
-    for _ in range(3):
-        t = time.perf_counter()
-        rows = lkcpu.evaluate_merged(pr, blobs, 10, threads)
-        times.append(time.perf_counter() - t)
-    dt = sorted(times)[1]
-    log(f"cpu baseline: {n} segments x {args.rows} rows in {dt:.2f}s (median of 3) on {threads} threads "
+    body = json.loads(local_req)
+    body["segmentRequests"] = body["segmentRequests"][:n]
+    pr = dx.parse_pushdown(json.dumps(body))
+    agg = q["agg"]
+    concurrent = world == 1 or args.comm == "rccl"
+
+    def run():
+        lkcpu.evaluate_cell_table(pr, 10, blobs, threads)   # warm (page-in, thread pool)
+        times, table = [], None
+        for _ in range(3):
+            t = []
+            table = lkcpu.evaluate_cell_table(pr, 10, blobs, threads, timing=t)
+            times.append(t[0])
+        return sorted(times)[1], table
+
+    if concurrent:
+        dt, table = run()
+    else:   # ranks sharing one GPU's CPU share take turns, so each is timed on the full share
+        for r in range(world):
+            if r == rank:
+                dt, table = run()
+            dist.barrier()
+    log(f"rank {rank}: cpu baseline {n} segments x {args.rows} rows in {dt:.3f}s (median of 3) on {threads} threads "
         f"({_cpu_model()}, {os.cpu_count()} CPUs visible)")
+    full = n == len(segs)
+    if world > 1:   # every rank's shard time and cells -> rank 0
+        times = [None] * world
+        dist.all_gather_object(times, (dt, full))
+        parts = [None] * world if rank == 0 else None
+        dist.gather_object(table.to_dict() if full else None, parts, dst=0)
+        if rank != 0:
+            return None, None
+        full = all(f for _, f in times)
+        dts = [t for t, _ in times]
+        table = lkcpu.CellTable.concat([lkcpu.CellTable(**p) for p in parts]) if full else None
+    else:
+        dts = [dt]
     validated = None
-    if n == len(segs):
+    if full:
+        has_gb = bool(q["group_bys"])
+        want = lkcpu.merge_cell_table(table, agg, has_gb)
         try:
-            assert_rows_equal(gpu_res.rows(), rows, q["agg"], "bench GPU rows vs CPU restatement")
-            validated = {"ok": True, "rows": len(rows), "against": "oracle/cpu (C++ restatement), full workload"}
+            lkcpu.assert_columns_equal(result_columns(gpu_res), want, agg, "bench GPU rows vs CPU restatement")
+            validated = {"ok": True, "rows": int(len(want[0])),
+                         "against": "oracle/cpu (C++ restatement), full workload" +
+                                    (f": {world} ranks' shard cells folded on rank 0 with query-api semantics"
+                                     if world > 1 else "")}
         except AssertionError as e:
-            validated = {"ok": False, "rows": len(rows), "error": str(e)[:500]}
+            validated = {"ok": False, "rows": int(len(want[0])), "error": str(e)[:500]}
         log(f"validation: {validated}")
-    return ({"value": n * args.rows / dt, "unit": "rows/s", "cores": threads, "kind": "port",
+    slowest = max(dts)
+    rows_cpu = n * args.rows * world
+    return ({"value": rows_cpu / slowest, "unit": "rows/s", "cores": threads * world, "kind": "port",
              "cpu_model": _cpu_model(), "nproc": os.cpu_count(), "affinity_cpus": affinity,
-             "core_limit": (f"OMP_NUM_THREADS={omp} (the job's CPU share on this box; {affinity} CPUs in the affinity "
-                            f"mask, {os.cpu_count()} on the host)") if omp else f"all {affinity} CPUs of the affinity mask",
-             "sample": f"{n} of the workload's {len(segs)} segments ({n * args.rows} rows), same query, "
-                       f"oracle/cpu/lkcpu.cpp (C++17 + OpenMP restatement, {threads} threads, median of 3)"},
+             "core_limit": (f"OMP_NUM_THREADS={omp} per rank (the job's CPU share on this box; {affinity} CPUs in the "
+                            f"affinity mask, {os.cpu_count()} on the host)") if omp else f"all {affinity} CPUs of the affinity mask",
+             "per_rank_seconds": dts,
+             "sample": (f"{n} of each rank's {len(segs)} segments ({rows_cpu} rows over {world} rank(s)), same query, "
+                        f"oracle/cpu/lkcpu.cpp (C++17 + OpenMP restatement, {threads} threads per rank, median of 3 of "
+                        f"the C++ evaluation)" +
+                        (f"; ranks {'concurrently' if concurrent else 'one after another'}, value = all rows / the "
+                         f"slowest rank's shard time" if world > 1 else ""))},
             validated)
 
 

@@ -6,6 +6,7 @@
 #include <string>
 
 #include "../../include/lakeside_gpu.h"
+#include "comm.hpp"
 #include "engine.hpp"
 #include "json.hpp"
 #include "plan.hpp"
@@ -147,7 +148,9 @@ const char* lk_engine_stats(lk_engine* e) {
            std::to_string(kv.second->live) + ",\"generation\":" + std::to_string(kv.second->gen) + "}";
     }
   }
-  o += "}}";
+  o += "}";
+  o += ",\"comm\":" + lk::comm_describe(E);   // set once by lk_comm_init*; not under comm_mu (a call may hold it)
+  o += "}";
   t_err.clear();
   static thread_local std::string t_stats;
   t_stats = o;

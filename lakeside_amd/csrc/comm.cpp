@@ -108,6 +108,9 @@ struct Comm {
                               const std::vector<size_t>& off) = 0;
   // pieces to / from other ranks (comm_exchange)
   virtual void exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) = 0;
+  // the transport's own view of the communicator (lk_engine_stats): RCCL reports what ncclCommCount /
+  // ncclCommUserRank / ncclCommCuDevice return, not what the caller passed to lk_comm_init
+  virtual std::string describe() const = 0;
 };
 
 namespace {
@@ -118,6 +121,17 @@ struct RcclComm final : Comm {
   ncclComm_t comm = nullptr;
   ~RcclComm() override {
     if (comm) ncclCommDestroy(comm);
+  }
+
+  std::string describe() const override {
+    int n = -1, r = -1, dev = -1;
+    if (comm) {
+      if (ncclCommCount(comm, &n) != ncclSuccess) n = -1;
+      if (ncclCommUserRank(comm, &r) != ncclSuccess) r = -1;
+      if (ncclCommCuDevice(comm, &dev) != ncclSuccess) dev = -1;
+    }
+    return "{\"transport\":\"rccl\",\"world\":" + std::to_string(n) + ",\"rank\":" + std::to_string(r) +
+           ",\"device\":" + std::to_string(dev) + ",\"loopback\":" + (loopback ? "true" : "false") + "}";
   }
 
   std::vector<std::string> allgather_bytes(Engine& E, CallCtx& X, const std::string& mine) override {
@@ -213,6 +227,11 @@ struct RcclComm final : Comm {
 struct HostComm final : Comm {
   lk_allgather_fn fn = nullptr;
   void* user = nullptr;
+
+  std::string describe() const override {
+    return "{\"transport\":\"host\",\"world\":" + std::to_string(world) + ",\"rank\":" + std::to_string(rank) +
+           ",\"loopback\":false}";
+  }
 
   void allgather(const void* send, size_t bytes, void* recv) {
     cnt.allgathers++;
@@ -337,6 +356,7 @@ struct HostComm final : Comm {
 }  // namespace
 
 int comm_world(const Engine& E) { return E.comm ? E.comm->world : 1; }
+std::string comm_describe(const Engine& E) { return E.comm ? E.comm->describe() : std::string("null"); }
 CommCounters comm_counters(const Engine& E) { return E.comm ? E.comm->cnt : CommCounters{}; }
 bool comm_loopback(const Engine& E) { return E.comm && E.comm->loopback; }
 int comm_rank(const Engine& E) { return E.comm ? E.comm->rank : 0; }
@@ -416,17 +436,20 @@ void comm_throw_pending(CallCtx& X) {
   throw PlanError(c, m);
 }
 
-void fault_point(const Engine& E, const char* stage) {
+bool fault_hit(const Engine& E, const char* stage) {
   const char* f = getenv("LK_FAULT");
-  if (!f || !*f) return;
+  if (!f || !*f) return false;
   const std::string spec(f);
   const size_t at = spec.find('@');
   const bool hit = spec.substr(0, at) == stage &&
                    (at == std::string::npos || atoi(spec.c_str() + at + 1) == comm_rank(E));
   if (getenv("LK_FAULT_TRACE"))
     fprintf(stderr, "[lk fault] rank %d stage %s spec %s -> %s\n", comm_rank(E), stage, f, hit ? "inject" : "pass");
-  if (!hit) return;
-  throw PlanError(LK_ERR_DEVICE, std::string("injected fault at stage '") + stage + "' (LK_FAULT)");
+  return hit;
+}
+
+void fault_point(const Engine& E, const char* stage) {
+  if (fault_hit(E, stage)) throw PlanError(LK_ERR_DEVICE, std::string("injected fault at stage '") + stage + "' (LK_FAULT)");
 }
 
 void comm_exchange(Engine& E, CallCtx& X, const std::vector<Piece>& sends, const std::vector<Piece>& recvs) {
@@ -633,7 +656,8 @@ EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes) {
   if (C.rank != 0 && (!m.blk || m.gen != hdr[3])) {
     m.release();
     const std::string name = "/lakeside-" + std::to_string(hdr[1]) + "-" + std::to_string(b) + "-" + std::to_string(hdr[3]);
-    m.blk = map_block(name, size_t(hdr[4]), false);
+    // tests only (LK_FAULT=emit_map@rank): this rank fails to map the generation
+    m.blk = fault_hit(E, "emit_map") ? nullptr : map_block(name, size_t(hdr[4]), false);
     m.gen = hdr[3];
   }
   // a rank that could not map the block reports it with its rows (the caller's agreement fails the call everywhere)
@@ -643,15 +667,26 @@ EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes) {
   T.dev = m.blk ? static_cast<uint8_t*>(m.blk->dev) : nullptr;
   T.cap = m.cap();
   T.lease = lease;
+  T.block = b;
+  T.gen = hdr[3];
   return T;
 }
 
-void comm_emit_end(Engine& E) {
+void comm_emit_end(Engine& E, const EmitTarget& T, bool agreed) {
   Comm& C = need_comm(E);
-  if (C.rank != 0) return;
-  // every rank has mapped this generation (the caller's agreement follows their writes): the names can go
-  for (auto& kv : C.shm)
-    if (kv.second.blk) kv.second.blk->unlink();
+  if (C.rank != 0 || !T.ok) return;
+  auto it = C.shm.find(T.block);
+  if (it == C.shm.end() || !it->second.blk || it->second.gen != T.gen) return;
+  if (agreed) {
+    // every rank has mapped this call's block generation (the agreement follows their writes): its name can go.
+    // Only this block: another block's generation may not have been mapped by every rank yet.
+    it->second.blk->unlink();
+  } else {
+    // the emit agreement failed -- possibly because a rank could not map this generation: drop the block from the
+    // pool, so the next call that needs one creates a new generation that every rank maps afresh, instead of
+    // re-offering a name that may already be gone (the mapping itself lives on while a lease holds it)
+    it->second.release();
+  }
 }
 
 }  // namespace lk

@@ -13,6 +13,8 @@
 namespace lk {
 
 int comm_world(const Engine& E);
+// JSON object describing the communicator as its transport sees it ("null" without one): lk_engine_stats' "comm".
+std::string comm_describe(const Engine& E);
 // Collectives this rank has issued on the communicator (cumulative; a call's stats report the difference).  RCCL: one
 // ncclAllGather per all-gather, one grouped ncclSend/ncclRecv set per point-to-point group; host transport: one
 // callback all-gather each.
@@ -56,6 +58,8 @@ void comm_throw_pending(CallCtx& X);
 // Tests only (env LK_FAULT=<stage>[@rank]): throws an injected LK_ERR_DEVICE at that stage on that rank (any rank
 // without @rank), so the multi-rank failure paths can be exercised on hardware that does not fail.
 void fault_point(const Engine& E, const char* stage);
+// The same test as fault_point without throwing (a stage whose failure is a result, not an exception).
+bool fault_hit(const Engine& E, const char* stage);
 // comm_agree and an element-wise max of a small host byte array (glob column unions, NULL flags) in one all-gather.
 void comm_agree_max_u8(Engine& E, CallCtx& X, int code, const std::string& msg, uint8_t* host, size_t n);
 // Dense mode: reduce the partial aggregation table (P.rows/cnt/hi/lo/ext, nc cells) onto rank 0: counts by
@@ -92,11 +96,14 @@ struct EmitTarget {
   uint8_t* dev = nullptr;
   size_t cap = 0;
   std::shared_ptr<void> lease;
+  int block = -1;      // rank 0's pool index and generation of the offered block
+  uint64_t gen = 0;
 };
 EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes);
-// After the agreement that follows every rank's writes (so every rank holds its mapping): rank 0 unlinks the block
-// names, so a crash leaves no block behind in /dev/shm.
-void comm_emit_end(Engine& E);
+// After the agreement that follows every rank's writes.  agreed: every rank holds its mapping, so rank 0 unlinks this
+// call's block name (a crash then leaves nothing in /dev/shm).  Not agreed (some rank failed to map or write): rank 0
+// drops the block from its pool, so a later call creates a new generation rather than re-offering this one.
+void comm_emit_end(Engine& E, const EmitTarget& T, bool agreed);
 
 // Agreed dim space of an unrestricted group dimension over the ranks (dims.cpp; collective: every rank calls it in
 // the same order).  The cached union is reused while no rank's dictionary changed (one all-gather); `rebuilt` says a

@@ -1693,8 +1693,13 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
             wmsg = e.what();
           }
         }
-        comm_agree(E, *X, wst, wmsg);   // every range written
-        comm_emit_end(E);   // every rank holds its mapping: the block names can go
+        try {
+          comm_agree(E, *X, wst, wmsg);   // every range written
+        } catch (...) {
+          comm_emit_end(E, ET, false);     // rank 0: retire the block (a rank may not have mapped it)
+          throw;
+        }
+        comm_emit_end(E, ET, true);   // every rank holds its mapping: this block's name can go
         if (rank == 0) {
           nrows_out = uint32_t(total_rows);
           res->adopt_rows(ET.host, N, ET.lease);

@@ -8,6 +8,7 @@ Only tests/, bench.py and __graft_entry__.smoke() may import it; the product pat
 import ctypes
 import math
 import os
+import time
 from typing import Dict, List, Optional, Sequence, Tuple
 from urllib.parse import quote
 
@@ -234,6 +235,209 @@ def merge_glob_cells(pr: dx.PushDownRequest, glob_cells) -> List[Tuple[int, floa
 
 def evaluate_merged(pr: dx.PushDownRequest, blobs: Sequence, glob_size: int = 10, threads: int = 0):
     return merge_glob_cells(pr, evaluate_glob_cells(pr, glob_size, blobs, threads))
+
+
+# ---------------------------------------------------------------------------------------------------------------
+# Columnar form (bench validation at full size: millions of cells, and partial tables of several ranks).  A row's tag
+# map is one canonical byte string, `tag_key(tags)`: its items sorted by key, key and value joined by 0x1e, items by
+# 0x1f -- equal maps give equal keys, so the query-api merge and the comparison run on numpy arrays.
+# ---------------------------------------------------------------------------------------------------------------
+def tag_key(tags: Dict[str, str]) -> bytes:
+    return "\x1f".join(f"{k}\x1e{v}" for k, v in sorted(tags.items())).encode()
+
+
+def tags_of_key(key: bytes) -> Dict[str, str]:
+    if not key:
+        return {}
+    return dict(item.split("\x1e", 1) for item in key.decode().split("\x1f"))
+
+
+def join_tag_columns(names: Sequence[str], cols: Sequence[np.ndarray], fallback: np.ndarray) -> np.ndarray:
+    """Per-row canonical tag keys from per-column value arrays (bytes; b"" = the tag is dropped, S15) in any column
+    order; rows with no tag left take `fallback` (their queryTags key, Commons.scala:450-452)."""
+    order = sorted(range(len(names)), key=lambda c: names[c])
+    n = len(fallback)
+    out = np.full(n, b"", dtype=object)
+    for c in order:
+        v = np.asarray(cols[c], dtype=object)
+        has = v != b""
+        piece = np.full(n, b"", dtype=object)
+        if has.any():
+            piece[has] = names[c].encode() + b"\x1e" + v[has]
+        both = has & (out != b"")
+        out[both] = out[both] + b"\x1f"
+        out = out + piece
+    empty = out == b""
+    out[empty] = fallback[empty]
+    return out
+
+
+class CellTable:
+    """Per-glob (bucket, group) cells as numpy columns: ts, glob, count, hi, lo, vmin, vmax (count == 0: no value),
+    key (canonical tag key, object array of bytes)."""
+
+    FIELDS = ("ts", "glob", "count", "hi", "lo", "vmin", "vmax", "key")
+
+    def __init__(self, **cols):
+        for f in self.FIELDS:
+            setattr(self, f, cols[f])
+
+    def __len__(self):
+        return len(self.ts)
+
+    def to_dict(self):
+        return {f: getattr(self, f) for f in self.FIELDS}
+
+    @staticmethod
+    def concat(tables: Sequence["CellTable"]) -> "CellTable":
+        return CellTable(**{f: np.concatenate([getattr(t, f) for t in tables]) if tables else np.zeros(0)
+                            for f in CellTable.FIELDS})
+
+
+def evaluate_cell_table(pr: dx.PushDownRequest, glob_size: int, blobs: Sequence, threads: int = 0,
+                        timing: Optional[list] = None) -> CellTable:
+    """evaluate_glob_cells in columnar form: the same cells, tags already materialized per S15 into canonical keys.
+    `timing` (a list) receives the C++ evaluation's wall time in seconds (the CPU baseline's timed part)."""
+    text, strcols, gbs = plan_text(pr, glob_size)
+    n = len(blobs)
+    ptrs = (ctypes.c_void_p * max(1, n))()
+    sizes = (ctypes.c_size_t * max(1, n))()
+    keep = []
+    for i, b in enumerate(blobs):
+        if isinstance(b, (bytes, bytearray)):
+            buf = ctypes.create_string_buffer(bytes(b), len(b))
+            keep.append(buf)
+            ptrs[i], sizes[i] = ctypes.cast(buf, ctypes.c_void_p), len(b)
+        else:
+            ptrs[i], sizes[i] = ctypes.cast(b[0], ctypes.c_void_p), b[1]
+    L = lib()
+    t0 = time.perf_counter()
+    h = L.lkcpu_eval(text.encode(), ptrs, sizes, n, threads)
+    if timing is not None:
+        timing.append(time.perf_counter() - t0)
+    if not h:
+        raise RuntimeError(L.lkcpu_error().decode())
+    try:
+        m = L.lkcpu_ncells(h)
+        nc = L.lkcpu_ncols(h)
+        glob = np.zeros(m, np.int32)
+        ts = np.zeros(m, np.int64)
+        rows = np.zeros(m, np.uint64)
+        cnt = np.zeros(m, np.uint64)
+        hi = np.zeros(m, np.float64)
+        lo = np.zeros(m, np.float64)
+        mn = np.zeros(m, np.float64)
+        mx = np.zeros(m, np.float64)
+        nanf = np.zeros(m, np.uint8)
+        keys = np.zeros(max(1, m * nc), np.int32)
+        L.lkcpu_cells(h, *[a.ctypes.data for a in (glob, ts, rows, cnt, hi, lo, mn, mx, nanf, keys)])
+        keys = keys[:m * nc].reshape(m, nc)
+        names = ["name"] + gbs
+        cols = []
+        for j in range(nc):
+            uniq, inv = np.unique(keys[:, j], return_inverse=True)
+            text_u = []
+            for u in uniq.tolist():
+                v = L.lkcpu_key_string(h, j, int(u)) if u >= 0 else None
+                text_u.append(b"" if v is None or v in (b"null", b"") else v)   # Commons.scala:433 (S15)
+            cols.append(np.array(text_u, dtype=object)[inv] if m else np.zeros(0, object))
+        globs = dx.globs_of(pr, glob_size)
+        qkeys = np.array([tag_key({k: (v if isinstance(v, str) else str(v))
+                                   for k, v in pr.segmentRequests[g[0]].queryTags.items()}) for g in globs] or [b""],
+                         dtype=object)
+        key = join_tag_columns(names, cols, qkeys[glob] if m else np.zeros(0, object))
+        vmin = np.where(nanf & 2, mn, np.nan)
+        vmax = np.where(nanf & 1, np.nan, mx)
+        return CellTable(ts=ts, glob=glob, count=cnt, hi=hi, lo=lo, vmin=vmin, vmax=vmax, key=key)
+    finally:
+        L.lkcpu_free(h)
+
+
+def _two_sum(a, b):
+    s = a + b
+    bb = s - a
+    return s, (a - (s - bb)) + (b - bb)
+
+
+def merge_cell_table(t: CellTable, agg: str, has_group_bys: bool):
+    """query-api merge (S19) of cells (any number of globs and ranks) -> (ts, value, key) arrays sorted by (ts, key):
+    with groupBys one row per (ts, tag map), else one per ts with the smallest tag map (deterministic stand-in for
+    the first arrival, as merge_glob_cells).  sum: hi / lo parts accumulated in double-double, rounded once (within
+    1 ulp of the correctly rounded sum, the test bar); min / max: java.lang.Math semantics, a NaN absorbs."""
+    n = len(t)
+    if n == 0:
+        return np.zeros(0, np.int64), np.zeros(0), np.zeros(0, object)
+    kid_u, kid = np.unique(t.key.astype(bytes), return_inverse=True)
+    if has_group_bys:
+        order = np.lexsort((kid, t.ts))
+        ts_s, k_s = t.ts[order], kid[order]
+        start = np.ones(n, bool)
+        start[1:] = (ts_s[1:] != ts_s[:-1]) | (k_s[1:] != k_s[:-1])
+    else:
+        order = np.lexsort((kid, t.ts))
+        ts_s, k_s = t.ts[order], kid[order]
+        start = np.ones(n, bool)
+        start[1:] = ts_s[1:] != ts_s[:-1]
+    g = np.cumsum(start) - 1
+    G = int(g[-1]) + 1
+    first = np.nonzero(start)[0]
+    pos = np.arange(n) - first[g]
+    out_ts = ts_s[first]
+    out_key = kid_u[k_s[first]].astype(object)   # (sorted by key within a ts: the first is the smallest map)
+    cnt = t.count[order]
+    total = np.zeros(G, np.uint64)
+    np.add.at(total, g, cnt)
+    if agg in (dx.SUM, dx.AVG):
+        hi, lo = t.hi[order], t.lo[order]
+        acc_hi, acc_lo = np.zeros(G), np.zeros(G)
+        for k in range(int(pos.max()) + 1):
+            sel = pos == k
+            idx = g[sel]
+            for x in (hi[sel], lo[sel]):
+                s, e = _two_sum(acc_hi[idx], x)
+                acc_hi[idx] = s
+                acc_lo[idx] += e
+        with np.errstate(invalid="ignore"):
+            ssum = np.where(np.isfinite(acc_hi), acc_hi + acc_lo, acc_hi)
+        if agg == dx.SUM:
+            val = np.where(total > 0, ssum, 0.0)
+        else:
+            with np.errstate(invalid="ignore", divide="ignore"):
+                val = np.where(total > 0, ssum / np.maximum(total, 1).astype(np.float64), np.nan)
+    elif agg == dx.COUNT:
+        val = total.astype(np.float64)
+    else:
+        src = (t.vmin if agg == dx.MIN else t.vmax)[order]
+        cell = np.where(cnt > 0, src, 0.0)   # a cell without values reads 0.0 (S15 getDouble of NULL)
+        val = np.full(G, np.inf if agg == dx.MIN else -np.inf)
+        (np.minimum if agg == dx.MIN else np.maximum).at(val, g, cell)
+    return out_ts, val, out_key
+
+
+def assert_columns_equal(got, want, agg: str, label: str = ""):
+    """(ts, value, key) arrays, each side in any order: the same rows; count / min / max bit-exact, sum / avg within
+    1 ulp (tests/parity.py's bar, vectorized)."""
+    def srt(cols):
+        ts, val, key = cols
+        key = np.asarray(key, dtype=object).astype(bytes)
+        o = np.lexsort((key, ts))
+        return ts[o], val[o], key[o]
+    gt, gv, gk = srt(got)
+    wt, wv, wk = srt(want)
+    assert len(gt) == len(wt), f"{label}: {len(gt)} rows vs expected {len(wt)}"
+    bad = np.nonzero(gt != wt)[0]
+    assert not len(bad), f"{label}: row {bad[0]} ts {gt[bad[0]]} vs {wt[bad[0]]}"
+    bad = np.nonzero(gk != wk)[0]
+    assert not len(bad), f"{label}: row {bad[0]} tags {tags_of_key(gk[bad[0]])} vs {tags_of_key(wk[bad[0]])}"
+    both_nan = np.isnan(gv) & np.isnan(wv)
+    if agg in (dx.SUM, dx.AVG):
+        with np.errstate(invalid="ignore"):
+            ok = (gv == wv) | both_nan | (np.abs(gv - wv) <= np.spacing(np.abs(wv)))
+    else:
+        ok = ((gv == wv) & (np.signbit(gv) == np.signbit(wv))) | both_nan
+    bad = np.nonzero(~ok)[0]
+    assert not len(bad), (f"{label}: row {bad[0]} at ts={gt[bad[0]]} tags={tags_of_key(gk[bad[0]])}: value "
+                          f"{gv[bad[0]]!r} vs expected {wv[bad[0]]!r} (agg {agg})")
 
 
 def evaluate_per_glob(pr: dx.PushDownRequest, blobs: Sequence, glob_size: int = 10, threads: int = 0):

@@ -30,3 +30,46 @@ def assert_rows_equal(got, want, agg, label=""):
 
 def from_jsonable(rows):
     return [(int(t), float.fromhex(v), dict(tags)) for t, v, tags in rows]
+
+
+def result_columns(res):
+    """A GPU Result as (ts, value, canonical tag key) arrays (oracle.cpu.tag_key), built column-wise from the bulk
+    export (lk_result_group_ids + lk_result_tag_dictionary) -- the full-size bench validation compares millions of
+    rows this way; rows whose group tags are all dropped take their per-row tags (the queryTags fallback)."""
+    import ctypes
+
+    import numpy as np
+
+    from lakeside_amd import _lib
+    from lakeside_amd.evaluator import _View
+    from oracle.cpu import join_tag_columns, tag_key
+
+    L = _lib.lib()
+    h = res._owner.h
+    n = len(res.ts)
+    ng = L.lk_result_num_group_columns(h) if n else 0
+    names, cols = [], []
+    if ng:
+        gid = np.asarray(_View(res._owner, L.lk_result_group_ids(h), n, "<u4")).astype(np.uint64)
+        for c in range(ng):
+            stride, nd = ctypes.c_uint64(), ctypes.c_uint64()
+            p = L.lk_result_tag_dictionary(h, c, ctypes.byref(stride), ctypes.byref(nd))
+            if not p or nd.value == 0:
+                continue
+            d = (gid // np.uint64(stride.value)) % np.uint64(nd.value)
+            uniq, inv = np.unique(d, return_inverse=True)
+            text = [ctypes.string_at(p[int(u)]) if p[int(u)] else b"" for u in uniq]
+            names.append(res.tag_names[c])
+            cols.append(np.array(text, dtype=object)[inv])
+    fallback = np.full(n, b"", dtype=object)
+    if len(res.tag_names) > ng:   # rows without own tags: their tag map from the library, row by row (few)
+        own = join_tag_columns(names, cols, fallback) if names else fallback
+        for r in np.nonzero(own == b"")[0].tolist():
+            m = {}
+            for c in range(ng, len(res.tag_names)):
+                v = L.lk_result_tag_value(h, r, c)
+                if v is not None:
+                    m[res.tag_names[c]] = v.decode()
+            fallback[r] = tag_key(m)
+    key = join_tag_columns(names, cols, fallback) if names else fallback
+    return np.array(res.ts, dtype=np.int64), np.array(res.values, dtype=np.float64), key

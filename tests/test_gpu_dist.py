@@ -422,6 +422,30 @@ def _worker_fault(rank, world, port):
         res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
         if rank == 0:
             assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, "after numeric tag refusal")
+        del res
+        # a rank that fails to map a shared result block generation must not turn into a permanent
+        # failure once another call unlinks names.  Block 0 is held by a live result, call A creates block 1 and rank
+        # 1 cannot map it (LK_FAULT=emit_map@1); once block 0 is free again call C uses it (and, before the fix,
+        # unlinked every name in the pool), then call D -- block 0 held again -- needs block 1 and must succeed.
+        os.environ.update(kr)
+        held = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])   # block 0
+        os.environ["LK_FAULT"] = "emit_map@1"
+        try:
+            eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # A: block 1
+            raise AssertionError("emit_map fault did not fail the call")
+        except LakesideError as e:
+            assert e.code == LK_ERR_DEVICE, str(e)
+        os.environ.pop("LK_FAULT")
+        if rank == 0:
+            assert held.stats["emit"] == "shared_host_block", held.stats
+        del held
+        c = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # C: block 0
+        d = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # D: block 1
+        if rank == 0:
+            for r_, nm in ((c, "C"), (d, "D")):
+                assert r_.stats["emit"] == "shared_host_block", r_.stats
+                assert_rows_equal(r_.rows(), from_jsonable(case["expected_merged"]), agg, f"after emit_map fault {nm}")
+        del c, d
         dist.barrier()
     finally:
         for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS", "LK_FAULT"):

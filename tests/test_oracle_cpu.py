@@ -86,3 +86,72 @@ def test_cpu_restatement_value_leaf(op, lit, agg):
     want = dx.evaluate_merged(pr, [f"s{i}" for i in range(4)], 2, sources=blobs)
     assert want
     assert_rows_equal(cpu.evaluate_merged(pr, blobs, 2, threads=4), want, agg, f"cpu value leaf {op} {lit}")
+
+
+def _rows_as_columns(rows):
+    import numpy as np
+
+    from oracle.cpu import tag_key
+    return (np.array([r[0] for r in rows], dtype=np.int64), np.array([r[1] for r in rows], dtype=np.float64),
+            np.array([tag_key(r[2]) for r in rows], dtype=object))
+
+
+@pytest.mark.parametrize("case", [c for c in _cases() if c["expected_merged"] is not None], ids=lambda c: c["name"])
+def test_columnar_merge_golden(case):
+    """The bench's columnar validator (evaluate_cell_table + merge_cell_table, numpy) == the golden merged rows, both
+    over the whole request and folded from two shards' cell tables (the N > 1 bench: every rank's CPU cells meet on
+    rank 0)."""
+    from oracle import cpu, dataexpr as dx
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    blobs = [open(p, "rb").read() for p in paths]
+    req = case["request"]
+    pr = dx.parse_pushdown(json.dumps(req))
+    agg = req["baseExpr"]["chart"]["aggregation"]
+    has_gb = bool(pr.baseExpr.chart.groupBys)
+    want = _rows_as_columns(from_jsonable(case["expected_merged"]))
+    try:
+        whole = cpu.evaluate_cell_table(pr, case["glob_size"], blobs, threads=3)
+    except RuntimeError as e:
+        if "compressed" in str(e):
+            pytest.skip("compressed fixture")
+        raise
+    cpu.assert_columns_equal(cpu.merge_cell_table(whole, agg, has_gb), want, agg, f"columnar {case['name']}")
+    # two shards: only valid where every glob carries one window, step and queryTags (the bench's requests)
+    segs = req["segmentRequests"]
+    if len({(s["startTs"], s["endTs"], s["stepInMillis"], json.dumps(s.get("queryTags"), sort_keys=True))
+            for s in segs}) != 1 or len(segs) < 2:
+        return
+    parts = []
+    for sh in (range(0, len(segs), 2), range(1, len(segs), 2)):
+        sub = dict(req)
+        sub["segmentRequests"] = [segs[i] for i in sh]
+        parts.append(cpu.evaluate_cell_table(dx.parse_pushdown(json.dumps(sub)), case["glob_size"],
+                                             [blobs[i] for i in sh], threads=2))
+    cpu.assert_columns_equal(cpu.merge_cell_table(cpu.CellTable.concat(parts), agg, has_gb), want, agg,
+                             f"columnar 2 shards {case['name']}")
+
+
+@pytest.mark.parametrize("agg,gbs", [("sum", []), ("max", ["svc", "ns"]), ("avg", ["ns"]), ("min", [])])
+def test_columnar_merge_synthetic_shards(agg, gbs):
+    from lakeside_amd import synth
+    from oracle import cpu, dataexpr as dx
+    col = {"svc": synth.SERVICE, "ns": synth.NAMESPACE}
+    blobs = []
+    for i in range(6):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 16, value_mode=1, null_frac=0.05,
+                                                  rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        s.free()
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_07"),
+            "q2": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}
+    segs = [synth.segment_request(i) for i in range(6)]
+    req = synth.pushdown(filt, segs, agg, [col[g] for g in gbs])
+    pr = dx.parse_pushdown(json.dumps(req))
+    want = _rows_as_columns(dx.evaluate_merged(pr, [f"s{i}" for i in range(6)], 2, sources=blobs))
+    parts = []
+    for r in range(3):   # three "ranks", contiguous blocks of two segments
+        sub = dict(req)
+        sub["segmentRequests"] = segs[2 * r:2 * r + 2]
+        parts.append(cpu.evaluate_cell_table(dx.parse_pushdown(json.dumps(sub)), 10, blobs[2 * r:2 * r + 2], threads=2))
+    cpu.assert_columns_equal(cpu.merge_cell_table(cpu.CellTable.concat(parts), agg, bool(gbs)), want, agg,
+                             f"columnar shards {agg} {gbs}")
