@@ -17,6 +17,8 @@ HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/jdtoa.cpp $(SRC)/ddske
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
+# device code includes only these (host-only header edits do not rebuild the kernels)
+DEV_HDRS = $(SRC)/device_common.hpp $(SRC)/kernels.hpp $(SRC)/layout.hpp $(SRC)/scan_inst.hpp $(SRC)/scan_kernel.hpp $(SRC)/lean_kernel.hpp
 
 all: $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
 
@@ -24,7 +26,7 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(CXXFLAGS_HOST) -x c++ -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include -c $< -o $@
 
-$(OBJDIR)/%.o: $(SRC)/%.hip $(HDRS)
+$(OBJDIR)/%.o: $(SRC)/%.hip $(DEV_HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
 

@@ -653,11 +653,13 @@ EmitTarget comm_emit_begin(Engine& E, CallCtx& X, size_t bytes) {
   if (!hdr[0]) return T;   // no block on rank 0: every rank takes the gather path
   const int b = int(hdr[2]);
   ShmMap& m = C.shm[b];
-  if (C.rank != 0 && (!m.blk || m.gen != hdr[3])) {
+  if (C.rank != 0 && fault_hit(E, "emit_map")) {   // tests only (LK_FAULT=emit_map@rank): the mapping fails
+    m.release();
+    m.gen = hdr[3];
+  } else if (C.rank != 0 && (!m.blk || m.gen != hdr[3])) {
     m.release();
     const std::string name = "/lakeside-" + std::to_string(hdr[1]) + "-" + std::to_string(b) + "-" + std::to_string(hdr[3]);
-    // tests only (LK_FAULT=emit_map@rank): this rank fails to map the generation
-    m.blk = fault_hit(E, "emit_map") ? nullptr : map_block(name, size_t(hdr[4]), false);
+    m.blk = map_block(name, size_t(hdr[4]), false);
     m.gen = hdr[3];
   }
   // a rank that could not map the block reports it with its rows (the caller's agreement fails the call everywhere)

@@ -433,7 +433,8 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   if (glob_size <= 0) glob_size = 10;
   if (n_paths != R.segments.size()) throw PlanError(LK_ERR_ARG, "paths must match segmentRequests");
   // Exemplar query (no chart, not a tag query): raw rows, ORDER BY timestamp LIMIT n (BaseExpr.scala:234-239)
-  if (!R.is_tag_query && !R.has_chart) return evaluate_exemplar(E, *X, R, paths, n_paths, glob_size, flags, dist, res);
+  if (!R.is_tag_query && !R.has_chart)
+    return evaluate_exemplar(E, *X, R, paths, n_paths, glob_size, flags, dist, res, std::string(), shard);
 
   // ---- shape gate ----
   // Tag query (isTagQuery with a tagDataType): BaseExpr.generateSql (BaseExpr.scala:127-143) emits
@@ -725,8 +726,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // every rank sees every glob's union, failures and value type; a rank-local engine failure fails every rank here
   if (dist) comm_agree_max_u8(E, *X, load_err, load_msg, exists.data(), exists.size());
   const bool value_nulls = exists[vnull_at] != 0;
-  if (exists[vnull_at + 1])   // agreed: every rank fails alike
-    throw PlanError(LK_ERR_UNSUPPORTED, "distributed tag query over the numeric tag column " + R.tag_name);
+  if (exists[vnull_at + 1]) {   // agreed: a numeric tag column on some rank -- every rank takes the TAGNUM row scan
+    segs.clear();
+    return evaluate_exemplar(E, *X, R, paths, n_paths, glob_size, flags, true, res, R.tag_name, shard);
+  }
   size_t nfailed = 0;
   for (size_t gi = 0; gi < ng; gi++)
     if (gfail[gi]) {

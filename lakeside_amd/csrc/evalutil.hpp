@@ -36,8 +36,12 @@ double ms_since(std::chrono::steady_clock::time_point t0);
 // Exemplar queries (no chart): exemplar.cpp.
 // numtag: a tag query (isTagQuery) whose tag column is numeric -- the same row scan planning (filter, globs,
 // union_by_name types), counting passing rows per canonical tag value instead of selecting rows (ex_scan TAGNUM).
+// dist: every rank evaluates the segments of its shard (shard[i] == rank; default i % world) as the worker of its pod
+// would, and rank 0 folds the ranks' streams (exemplar: Akka mergeSorted in rank order, then query-api's take(limit);
+// numeric tag: counts summed per tag text).
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
-                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag = std::string());
+                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag = std::string(),
+                      const int32_t* shard = nullptr);
 // Numeric comparison leaves (numleaf.cpp): gt / ge / lt / le; the normalized literal (PlanError(LK_ERR_ARG) where the
 // reference's SQL fails); the leaf's interval on numeric filter column `col`.
 bool numeric_op(const std::string& op);

@@ -32,6 +32,7 @@
 #include <vector>
 
 #include "../../include/lakeside_gpu.h"
+#include "comm.hpp"
 #include "engine.hpp"
 #include "evalutil.hpp"
 #include "kernels.hpp"
@@ -159,12 +160,194 @@ struct PinnedTmp {
 };
 }  // namespace
 
+namespace {
+// Row streams as bytes (the ranks' exchange): tag names, then per row ts | value | present tags (column, text).
+void put_u32(std::string& b, uint32_t x) { b.append(reinterpret_cast<const char*>(&x), 4); }
+void put_str(std::string& b, const std::string& s) {
+  put_u32(b, uint32_t(s.size()));
+  b += s;
+}
+struct Reader {
+  const std::string& b;
+  size_t o = 0;
+  template <class T>
+  T get() {
+    if (o + sizeof(T) > b.size()) throw PlanError(LK_ERR_DEVICE, "internal: short exemplar stream from a rank");
+    T x;
+    memcpy(&x, b.data() + o, sizeof(T));
+    o += sizeof(T);
+    return x;
+  }
+  std::string str() {
+    const uint32_t n = get<uint32_t>();
+    if (o + n > b.size()) throw PlanError(LK_ERR_DEVICE, "internal: short exemplar stream from a rank");
+    std::string s = b.substr(o, n);
+    o += n;
+    return s;
+  }
+};
+struct XRow {
+  int64_t ts;
+  double val;
+  std::vector<std::pair<std::string, std::string>> tags;   // (column name, text), the row's present tags
+};
+}  // namespace
+
+// Distributed exemplar / numeric-tag query (VERDICT r4 missing #1-2).  Reference: query-api fans the pushdown out to
+// every worker pod holding segments of the group (SegmentSequencer.allSources), each pod evaluates its own segments
+// (globs of its own request, Commons.scala:361-392), and query-api merges the pods' streams -- exemplars:
+// flatMapMerge then take(limit) (QueryEngineV2.scala:493-535); tag queries: every pod's (tag, count) rows
+// (QueryEngineV2.scala:452-487).  Here each rank is a pod: it evaluates the segments of its shard as the worker
+// would (its exemplar stream: per-glob top `limit`, globs folded by mergeSorted; its numeric tag rows: counts per tag
+// text over its globs), one all-gather carries every rank's rows (and status: a rank-local failure fails every
+// rank), and rank 0 folds them -- exemplars: Akka mergeSorted over the ranks in rank order (the deterministic
+// stand-in for flatMapMerge's arrival order) and take(limit); numeric tags: counts summed per tag text (NULL apart),
+// in first-seen order, as the string tag query's merged table does.  Other ranks return no rows.
+static int exemplar_dist(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
+                         int glob_size, lk_result* res, const std::string& numtag, const int32_t* shard) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool tagnum = !numtag.empty();
+  const int world = comm_world(E), rank = comm_rank(E);
+  Request sub = copy_request(R);
+  sub.segments.clear();
+  std::vector<const char*> sp;
+  for (size_t i = 0; i < n_paths; i++)
+    if ((shard ? shard[i] : int32_t(i % size_t(world))) == rank) {
+      sp.push_back(paths[i]);
+      sub.segments.push_back(R.segments[i]);
+    }
+  int code = 0;
+  std::string msg, blob;
+  double scan_ms = 0;
+  uint64_t local_rows = 0;
+  if (!sp.empty()) {   // a pod with no segment of the group is not asked at all (no sentinel row)
+    try {
+      lk_result local;
+      evaluate_exemplar(E, X, sub, sp.data(), sp.size(), glob_size, tagnum ? LK_MERGED : LK_PER_GLOB_ROWS, false,
+                        &local, numtag);
+      const size_t nt = local.tag_names.size();
+      put_u32(blob, uint32_t(nt));
+      for (auto& n : local.tag_names) put_str(blob, n);
+      const uint64_t n = local.nrows;
+      blob.append(reinterpret_cast<const char*>(&n), 8);
+      for (size_t i = 0; i < local.nrows; i++) {
+        blob.append(reinterpret_cast<const char*>(&local.ts[i]), 8);
+        blob.append(reinterpret_cast<const char*>(&local.val[i]), 8);
+        uint32_t present = 0;
+        for (size_t c = 0; c < nt; c++) present += local.tag(i, c) != nullptr;
+        put_u32(blob, present);
+        for (size_t c = 0; c < nt; c++)
+          if (const char* v = local.tag(i, c)) {
+            put_u32(blob, uint32_t(c));
+            put_str(blob, v);
+          }
+      }
+      local_rows = local.nrows;
+      const char* k = strstr(local.stats.c_str(), "\"scan_ms\":");
+      if (k) scan_ms = atof(k + 10);
+    } catch (const PlanError& e) {
+      code = e.code;
+      msg = e.what();
+    } catch (const std::exception& e) {
+      code = LK_ERR_DEVICE;
+      msg = e.what();
+    }
+  }
+  const std::vector<std::string> all = comm_allgather_status(E, X, code, msg, blob);
+  res->exemplar = true;
+  res->per_glob = false;
+  std::vector<XRow> out;
+  std::vector<std::string> names;   // tag columns, first-seen order over the ranks
+  if (rank == 0) {
+    std::vector<std::vector<XRow>> streams(all.size());
+    for (size_t r = 0; r < all.size(); r++) {
+      if (all[r].empty()) continue;
+      Reader rd{all[r]};
+      const uint32_t nt = rd.get<uint32_t>();
+      std::vector<std::string> tn(nt);
+      for (auto& t : tn) t = rd.str();
+      for (auto& t : tn)
+        if (std::find(names.begin(), names.end(), t) == names.end()) names.push_back(t);
+      const uint64_t n = rd.get<uint64_t>();
+      streams[r].resize(size_t(n));
+      for (auto& row : streams[r]) {
+        row.ts = rd.get<int64_t>();
+        row.val = rd.get<double>();
+        const uint32_t np = rd.get<uint32_t>();
+        for (uint32_t j = 0; j < np; j++) {
+          const uint32_t c = rd.get<uint32_t>();
+          if (c >= nt) throw PlanError(LK_ERR_DEVICE, "internal: bad tag column in a rank's exemplar stream");
+          row.tags.emplace_back(tn[c], rd.str());
+        }
+      }
+    }
+    if (!tagnum) {
+      // Akka mergeSorted fold over the ranks' streams (left head when strictly less), then take(limit)
+      const bool rev = R.reverse_sort;
+      for (auto& v : streams) {
+        std::vector<XRow> m;
+        m.reserve(out.size() + v.size());
+        size_t i = 0, j = 0;
+        while (i < out.size() && j < v.size()) {
+          const bool lt = rev ? out[i].ts > v[j].ts : out[i].ts < v[j].ts;
+          if (lt) m.push_back(std::move(out[i++]));
+          else m.push_back(std::move(v[j++]));
+        }
+        while (i < out.size()) m.push_back(std::move(out[i++]));
+        while (j < v.size()) m.push_back(std::move(v[j++]));
+        out.swap(m);
+      }
+      if (R.limit >= 0 && out.size() > uint64_t(R.limit)) out.resize(size_t(R.limit));
+    } else {
+      // counts summed per tag text (the "count" tag rewritten), NULL / dropped tag apart, first-seen order
+      std::map<std::string, size_t> at;
+      for (auto& v : streams)
+        for (auto& row : v) {
+          std::string key = "\x01";   // the tag dropped (NULL or a null-like text)
+          for (auto& kv : row.tags)
+            if (kv.first == numtag) key = "\x02" + kv.second;
+          auto it = at.find(key);
+          if (it == at.end()) {
+            at.emplace(key, out.size());
+            out.push_back(std::move(row));
+          } else {
+            out[it->second].val += row.val;
+          }
+        }
+      for (auto& row : out)
+        for (auto& kv : row.tags)
+          if (kv.first == "count") kv.second = std::to_string((unsigned long long)row.val);
+    }
+  }
+  res->alloc_rows(out.size());
+  res->tag_names = names;
+  res->ex_tags.assign(out.size() * names.size(), nullptr);
+  for (size_t i = 0; i < out.size(); i++) {
+    res->ts[i] = out[i].ts;
+    res->val[i] = out[i].val;
+    res->glob[i] = 0;
+    res->gid[i] = uint32_t(i);
+    for (auto& kv : out[i].tags) {
+      const size_t c = size_t(std::find(names.begin(), names.end(), kv.first) - names.begin());
+      res->owned.push_back(kv.second);
+      res->ex_tags[i * names.size() + c] = res->owned.back().c_str();
+    }
+  }
+  char buf[320];
+  snprintf(buf, sizeof buf,
+           "{\"scan_ms\":%.4f,\"total_ms\":%.4f,\"rank_rows\":%llu,\"rows\":%zu,\"reduce\":\"%s\",\"table\":\"%s\"}",
+           scan_ms, ms_since(t0), (unsigned long long)local_rows, out.size(), tagnum ? "tag_counts" : "merge_sorted",
+           tagnum ? "tagnum" : "exemplar");
+  res->stats = buf;
+  return LK_OK;
+}
+
 int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const* paths, size_t n_paths,
-                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag) {
+                      int glob_size, unsigned flags, bool dist, lk_result* res, const std::string& numtag,
+                      const int32_t* shard) {
   const auto t_start = std::chrono::steady_clock::now();
   const bool tagnum = !numtag.empty();
-  if (dist) throw PlanError(LK_ERR_UNSUPPORTED, tagnum ? "distributed tag queries over a numeric tag column"
-                                                       : "distributed exemplar queries (each worker streams its own rows)");
+  if (dist) return exemplar_dist(E, X, R, paths, n_paths, glob_size <= 0 ? 10 : glob_size, res, numtag, shard);
   if (R.has_extract || R.has_compute)
     throw PlanError(LK_ERR_UNSUPPORTED, "extract / compute exemplar queries are not on the hot path");
   const bool logs = R.dataset == "logs";

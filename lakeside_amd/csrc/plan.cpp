@@ -184,4 +184,42 @@ bool restricted_values(const FilterNode* n, const std::string& col, std::vector<
   return false;
 }
 
+static std::unique_ptr<FilterNode> clone_filter(const FilterNode* n) {
+  if (!n) return nullptr;
+  auto c = std::make_unique<FilterNode>();
+  c->kind = n->kind;
+  c->k = n->k;
+  c->v = n->v;
+  c->op = n->op;
+  c->extracted = n->extracted;
+  c->computed = n->computed;
+  c->data_type = n->data_type;
+  c->a = clone_filter(n->a.get());
+  c->b = clone_filter(n->b.get());
+  return c;
+}
+
+Request copy_request(const Request& r) {
+  Request c;
+  c.expr_id = r.expr_id;
+  c.dataset = r.dataset;
+  c.filter = clone_filter(r.filter.get());
+  c.has_chart = r.has_chart;
+  c.aggregation = r.aggregation;
+  c.group_bys = r.group_bys;
+  c.chart_type = r.chart_type;
+  c.rollup = r.rollup;
+  c.field_chart = r.field_chart;
+  c.has_extract = r.has_extract;
+  c.has_compute = r.has_compute;
+  c.limit = r.limit;
+  c.order = r.order;
+  c.is_tag_query = r.is_tag_query;
+  c.reverse_sort = r.reverse_sort;
+  c.tag_name = r.tag_name;
+  c.tag_data_type = r.tag_data_type;
+  c.segments = r.segments;
+  return c;
+}
+
 }  // namespace lk

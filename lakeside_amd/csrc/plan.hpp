@@ -64,6 +64,8 @@ struct PlanError : std::runtime_error {
 };
 
 Request parse_request(const std::string& json);   // throws PlanError(LK_ERR_ARG, ...)
+// A deep copy (the filter tree cloned), e.g. to narrow `segments` to one rank's shard.
+Request copy_request(const Request& r);
 
 // Fields: BaseExpr.fieldSet (BaseExpr.scala:648-663): filter keys outside NOT + groupBys.
 std::set<std::string> field_set(const Request& r);

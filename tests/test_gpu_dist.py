@@ -408,20 +408,14 @@ def _worker_fault(rank, world, port):
             if rank == 0:
                 assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, f"after fault {stage} {env}")
             print(f"rank {rank}: {stage} {env} ok", flush=True)
-        # a tag query over a numeric tag column is refused alike on every rank (the decision is agreed), and the
-        # communicator stays usable
+        # a numeric tag query runs distributed (VERDICT r4 missing #2), and the communicator stays usable after it
         with open(os.path.join(GOLDEN, "numtag_cases.json")) as f:
             nt = json.load(f)[0]
         ntp = [os.path.join(GOLDEN, p) for p in nt["segments"]]
-        from lakeside_amd._lib import LK_ERR_UNSUPPORTED
-        try:
-            eng.eval_pushdown_dist(json.dumps(nt["request"]), ntp, None, nt["glob_size"])
-            raise AssertionError("numeric tag query accepted by the distributed path")
-        except LakesideError as e:
-            assert e.code == LK_ERR_UNSUPPORTED, str(e)
+        eng.eval_pushdown_dist(json.dumps(nt["request"]), ntp, None, nt["glob_size"])
         res = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])
         if rank == 0:
-            assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, "after numeric tag refusal")
+            assert_rows_equal(res.rows(), from_jsonable(case["expected_merged"]), agg, "after numeric tag query")
         del res
         # a rank that fails to map a shared result block generation must not turn into a permanent
         # failure once another call unlinks names.  Block 0 is held by a live result, call A creates block 1 and rank
@@ -512,3 +506,138 @@ def test_dist_numeric_leaves_world2(tmp_path):
     from tests.test_gpu_numeric import _files
     paths, _ = _files(tmp_path)
     mp.spawn(_worker_numeric, args=(2, _free_port(), paths), nprocs=2, join=True)
+
+
+# ---------------------------------------------------------------------------------------------------------
+# exemplar and numeric-tag queries through the distributed path (VERDICT r4 missing #1-2)
+# ---------------------------------------------------------------------------------------------------------
+def _rank_requests(req, paths, shard, rank):
+    """The request a pod receives: the segments of its shard, in request order (SegmentSequencer.allSources)."""
+    body = json.loads(req)
+    idx = [i for i in range(len(paths)) if shard[i] == rank]
+    body["segmentRequests"] = [body["segmentRequests"][i] for i in idx]
+    return json.dumps(body), [paths[i] for i in idx]
+
+
+def _want_exemplar_dist(req, paths, shard, world, glob_size):
+    """query-api's exemplar stream over the pods: each pod's worker stream (oracle/exemplar.py), folded with Akka
+    mergeSorted in rank order, then take(limit) (QueryEngineV2.scala:493-535)."""
+    from oracle import dataexpr as dx
+    from oracle import exemplar as ex
+    pr = dx.parse_pushdown(req)
+    streams = []
+    for r in range(world):
+        sreq, sp = _rank_requests(req, paths, shard, r)
+        if sp:
+            streams.append([(t, v, tags) for t, v, tags, _ in ex.evaluate_exemplar(dx.parse_pushdown(sreq), sp,
+                                                                                    glob_size)])
+    out = ex.merge_sorted_fold(streams, pr.reverseSort)
+    return out[:pr.baseExpr.limit] if pr.baseExpr.limit is not None else out
+
+
+def _want_numtag_dist(case, paths, shard, world):
+    """Counts per tag text over every pod's globs (each pod's globs over its own segments)."""
+    from oracle import dataexpr as dx
+    req = json.dumps(case["request"])
+    tag = case["request"]["tagDataType"]["tagName"]
+    acc = {}
+    for r in range(world):
+        sreq, sp = _rank_requests(req, paths, shard, r)
+        if not sp:
+            continue
+        for t in dx.evaluate_tag_merged(dx.parse_pushdown(sreq), tag, sp, case["glob_size"]):
+            k = t.get(tag)
+            acc[k] = acc.get(k, 0) + int(t["count"])
+    return [dx.tag_row_tags(tag, v, c) for v, c in acc.items()]
+
+
+def _check_exemplar_rows(res, want, label):
+    import math
+    rows = list(zip(res.ts.tolist(), res.values.tolist(), res.tags))
+    assert len(rows) == len(want), f"{label}: {len(rows)} rows vs {len(want)}"
+    for i, (g, w) in enumerate(zip(rows, want)):
+        assert g[0] == w[0], f"{label}: row {i} ts {g[0]} vs {w[0]}"
+        assert g[1] == w[1] or (math.isnan(g[1]) and math.isnan(w[1])), f"{label}: row {i} value {g[1]} vs {w[1]}"
+        assert g[2] == w[2], f"{label}: row {i} tags {g[2]} vs {w[2]}"
+
+
+def _exemplar_requests(n):
+    from lakeside_amd import synth
+    from oracle import dataexpr as dx
+    from tests.test_gpu_exemplar import SVC, _request
+    return [("default", _request(synth.leaf(dx.NAME, "eq", "metric_02"), n), 2),
+            ("limit37_asc_reverse", _request(synth.leaf(SVC, "regex", "^svc-a"), n, limit=37, order="asc",
+                                             reverse=True), 2),
+            ("everything", _request({"k": SVC, "v": [], "op": "exists"}, n, limit=100_000), 3)]
+
+
+def _worker_exemplar(rank, world, port, paths):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd.evaluator import Engine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        for rule in ("modulo", "block", "all_on_last"):
+            shard = _shard(rule, len(paths), world)
+            for label, req, gs in _exemplar_requests(len(paths)):
+                res = eng.eval_pushdown_dist(req, paths, shard, gs)
+                if rank == 0:
+                    _check_exemplar_rows(res, _want_exemplar_dist(req, paths, shard, world, gs), f"{rule} {label}")
+                else:
+                    assert len(res) == 0
+            with open(os.path.join(GOLDEN, "numtag_cases.json")) as f:
+                for case in json.load(f):
+                    ntp = [os.path.join(GOLDEN, p) for p in case["segments"]]
+                    sh = _shard(rule, len(ntp), world)
+                    res = eng.eval_pushdown_dist(json.dumps(case["request"]), ntp, sh, case["glob_size"])
+                    if rank == 0:
+                        key = lambda t: sorted(t.items())   # noqa: E731
+                        assert sorted(res.tags, key=key) == sorted(_want_numtag_dist(case, ntp, sh, world), key=key), \
+                            f"{rule} numtag {case['name']}"
+                        assert all(int(v) == int(t["count"]) for v, t in zip(res.values, res.tags))
+                    else:
+                        assert len(res) == 0
+            print(f"rank {rank}: exemplar / numtag {rule} ok", flush=True)
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dist_exemplar_and_numeric_tag_world2(tmp_path):
+    """Exemplar queries and numeric-tag queries through lk_eval_pushdown_dist at world 2 (host transport): each rank
+    evaluates its shard as a pod's worker would; rank 0 folds the streams (mergeSorted + take(limit) / counts per
+    tag text) and equals the oracle's per-pod evaluation folded the same way."""
+    import torch.multiprocessing as mp
+
+    from tests.test_gpu_exemplar import _logs_files
+    paths, _ = _logs_files(tmp_path)
+    mp.spawn(_worker_exemplar, args=(2, _free_port(), paths), nprocs=2, join=True)
+
+
+@pytest.mark.timeout(180)
+def test_dist_exemplar_world1_rccl_loopback(tmp_path):
+    """The same exchange through RCCL at world 1 (LK_COMM_LOOPBACK=1: the all-gather runs on the device)."""
+    from lakeside_amd.evaluator import Engine
+    from tests.test_gpu_exemplar import _logs_files
+    paths, _ = _logs_files(tmp_path)
+    saved = os.environ.get("LK_COMM_LOOPBACK")
+    os.environ["LK_COMM_LOOPBACK"] = "1"
+    eng = Engine(0)
+    try:
+        eng.comm_init(Engine.unique_id(), 1, 0)
+        shard = [0] * len(paths)
+        for label, req, gs in _exemplar_requests(len(paths)):
+            res = eng.eval_pushdown_dist(req, paths, shard, gs)
+            _check_exemplar_rows(res, _want_exemplar_dist(req, paths, shard, 1, gs), f"loopback {label}")
+    finally:
+        eng.close()
+        if saved is None:
+            os.environ.pop("LK_COMM_LOOPBACK", None)
+        else:
+            os.environ["LK_COMM_LOOPBACK"] = saved
