@@ -13,7 +13,7 @@ SYNTH   = lakeside_amd/liblakeside_synth.so
 RELIB   = lakeside_amd/liblakeside_regex.so
 TXLIB   = lakeside_amd/liblakeside_text.so
 
-HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/jdtoa.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
+HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/jdtoa.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/loader.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
 HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
@@ -68,3 +68,22 @@ exp-depth3:
 	@mkdir -p build/exp/obj lakeside_amd/exp
 	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) '-DLK_DEPTH(n)=2' -c $(SRC)/scan_$$a.hip -o build/exp/obj/scan_$$a.o & done; wait
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_d2.so $(HOST_OBJS) $(OBJDIR)/kernels.o build/exp/obj/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+
+# Host-only loader harness (no HIP): the Parquet walk, dictionary interning and staging copy of lakeside_amd/csrc/
+# loader.cpp, plain and under ASan + UBSan / TSan (`make sanitize`, tools/sanitize.sh).
+LOADCHK_SRCS = tools/load_check.cpp $(SRC)/loader.cpp $(SRC)/parquet.cpp $(SRC)/codec.cpp $(SRC)/plan.cpp
+LOADCHK_DEPS = $(LOADCHK_SRCS) $(SRC)/loader.hpp $(SRC)/segment.hpp $(SRC)/parquet.hpp $(SRC)/codec.hpp $(SRC)/layout.hpp $(SRC)/plan.hpp $(SRC)/thrift.hpp
+LOADCHK_FLAGS = -std=c++17 -g -pthread -Wall -Wextra -Wno-unused-parameter
+LOADCHK_LIBS = -lz -l:libzstd.so.1 -l:liblz4.so.1
+build/load_check: $(LOADCHK_DEPS)
+	@mkdir -p build
+	g++ -O2 $(LOADCHK_FLAGS) -o $@ $(LOADCHK_SRCS) $(LOADCHK_LIBS)
+build/load_check_asan: $(LOADCHK_DEPS)
+	@mkdir -p build
+	g++ -O1 -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all $(LOADCHK_FLAGS) -o $@ $(LOADCHK_SRCS) $(LOADCHK_LIBS)
+build/load_check_tsan: $(LOADCHK_DEPS)
+	@mkdir -p build
+	g++ -O1 -fsanitize=thread $(LOADCHK_FLAGS) -o $@ $(LOADCHK_SRCS) $(LOADCHK_LIBS)
+sanitize: build/load_check build/load_check_asan build/load_check_tsan
+	tools/sanitize.sh
+.PHONY: sanitize

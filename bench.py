@@ -227,7 +227,7 @@ def main():
                                                         highcard_n=highcard))
 
     # The CPU baseline / validator reads the same Parquet bytes: every rank keeps its shard in host memory.
-    keep_cpu = args.cpu_sample != 0 and not q.get("tag") and not q.get("exemplar")
+    keep_cpu = args.cpu_sample != 0 and not q.get("exemplar")
     kept = {}
     t0 = time.time()
     bytes_loaded = 0
@@ -476,14 +476,20 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
     body["segmentRequests"] = body["segmentRequests"][:n]
     pr = dx.parse_pushdown(json.dumps(body))
     agg = q["agg"]
+    tag = q.get("tag")
     concurrent = world == 1 or args.comm == "rccl"
 
+    def evaluate(timing=None):   # tag queries: {tag text -> COUNT(*)}; aggregates: per-glob cells
+        if tag:
+            return lkcpu.evaluate_tag_counts(pr, tag, 10, blobs, threads, timing=timing)
+        return lkcpu.evaluate_cell_table(pr, 10, blobs, threads, timing=timing)
+
     def run():
-        lkcpu.evaluate_cell_table(pr, 10, blobs, threads)   # warm (page-in, thread pool)
+        evaluate()   # warm (page-in, thread pool)
         times, table = [], None
         for _ in range(3):
             t = []
-            table = lkcpu.evaluate_cell_table(pr, 10, blobs, threads, timing=t)
+            table = evaluate(timing=t)
             times.append(t[0])
         return sorted(times)[1], table
 
@@ -501,20 +507,35 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
         times = [None] * world
         dist.all_gather_object(times, (dt, full))
         parts = [None] * world if rank == 0 else None
-        dist.gather_object(table.to_dict() if full else None, parts, dst=0)
+        dist.gather_object((table if tag else table.to_dict()) if full else None, parts, dst=0)
         if rank != 0:
             return None, None
         full = all(f for _, f in times)
         dts = [t for t, _ in times]
-        table = lkcpu.CellTable.concat([lkcpu.CellTable(**p) for p in parts]) if full else None
+        if full and tag:
+            table = {}
+            for p in parts:
+                for k, c in p.items():
+                    table[k] = table.get(k, 0) + c
+        elif full:
+            table = lkcpu.CellTable.concat([lkcpu.CellTable(**p) for p in parts])
     else:
         dts = [dt]
     validated = None
     if full:
         has_gb = bool(q["group_bys"])
-        want = lkcpu.merge_cell_table(table, agg, has_gb)
+        want = lkcpu.merge_cell_table(table, agg, has_gb) if not tag else (list(table),)
         try:
-            lkcpu.assert_columns_equal(result_columns(gpu_res), want, agg, "bench GPU rows vs CPU restatement")
+            if tag:   # the merged tag table: one row per tag text (NULL-like values together), value = COUNT(*)
+                got = {}
+                for v, t in zip(gpu_res.values.tolist(), gpu_res.tags):
+                    k = t.get(tag)
+                    assert int(t["count"]) == int(v), f"count tag {t['count']} vs value {v}"
+                    assert k not in got, f"tag value {k!r} twice in the merged rows"
+                    got[k] = int(v)
+                assert got == table, f"tag counts differ: {sorted(set(got.items()) ^ set(table.items()))[:10]}"
+            else:
+                lkcpu.assert_columns_equal(result_columns(gpu_res), want, agg, "bench GPU rows vs CPU restatement")
             validated = {"ok": True, "rows": int(len(want[0])),
                          "against": "oracle/cpu (C++ restatement), full workload" +
                                     (f": {world} ranks' shard cells folded on rank 0 with query-api semantics"

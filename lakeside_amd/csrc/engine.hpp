@@ -18,95 +18,20 @@
 
 #include "layout.hpp"
 #include "plan.hpp"
+#include "segment.hpp"
 
 namespace lk {
 
 void set_error(const std::string& m);
 
-// Append-only string array in fixed 64K-entry blocks behind a fixed block table: an element never moves, and
-// reading an element published before (under the owner's mutex) needs no lock, so results keep reading tag
-// strings while loads append to the dictionary.
-class StableStrs {
- public:
-  static constexpr uint32_t kShift = 16, kBlock = 1u << kShift, kMaxBlocks = 1u << 14;   // 2^30 entries
-  size_t size() const { return n_; }
-  const std::string& operator[](size_t i) const { return blocks_[i >> kShift][i & (kBlock - 1)]; }
-  void push_back(const std::string& s) {
-    const size_t b = n_ >> kShift;
-    if (b >= kMaxBlocks) throw std::length_error("dictionary exceeds 2^30 values");
-    if (!blocks_[b]) blocks_[b].reset(new std::string[kBlock]);
-    blocks_[b][n_ & (kBlock - 1)] = s;
-    n_++;
-  }
-  const std::string& back() const { return (*this)[n_ - 1]; }
-
- private:
-  std::unique_ptr<std::unique_ptr<std::string[]>[]> blocks_{new std::unique_ptr<std::string[]>[kMaxBlocks]};
-  size_t n_ = 0;
-};
-
-// Engine-global dictionary of one column name.  Values get dense ids in first-seen order, at stable
-// addresses (result tag values point into it).  Every id counts the chunk-dictionary entries of cached segments
-// that map to it (`refs`); when evictions have left as many dead ids as live ones, Engine::maybe_compact renumbers
-// the live values densely (old order kept), rewrites the cached segments' remaps and starts a new `vals` block --
-// results keep the block they were built from (shared ownership), so the group-dim space of a long-lived worker
-// tracks its cached segments, as the worker's bounded disk cache does (WorkerApi.scala:53-64).
-struct GlobalDict {
-  std::mutex mu;
-  std::unordered_map<std::string, uint32_t> ids;
-  std::shared_ptr<StableStrs> vals = std::make_shared<StableStrs>();
-  std::vector<uint32_t> refs;              // per id: cached chunk-dictionary entries mapping to it
-  size_t live = 0;                         // ids with refs > 0
-  uint64_t gen = 0;                        // compactions so far (ids are renumbered by each)
-  uint32_t intern(const std::string& s);   // caller holds mu
-  size_t size() const { return vals->size(); }
-  const std::string& operator[](size_t i) const { return (*vals)[i]; }
-};
-
-struct HostCol {
-  std::string name;
-  int ptype = -1;
-  bool nullable = false;
-  bool is_string = false;
-  bool unsupported = false;
-  bool any_nulls = false;
-  // page summaries (load time), so a query's lean-tile test costs O(1) per column instead of a walk over its pages:
-  bool pages_lean_name = false;           // every page: dictionary indices, chunk dictionary <= 64 values, 1..6 bits
-  bool pages_lean_late = false;           // every page: dictionary indices of <= 32 bits
-  uint64_t compressed_bytes = 0;          // Σ ColumnMetaData.total_compressed_size (algorithmic bytes)
-  std::vector<PageDesc> pages;            // host copy (planner reads dict sizes / null flags)
-  std::vector<RunDesc> runs;              // load-time only
-  std::vector<TileCol> tcols;             // load-time only
-  std::vector<uint32_t> remap;            // load-time only
-  size_t nremap = 0;                      // entries of d_remap counted in the column dictionary's refs
-  PageDesc* d_pages = nullptr;
-  RunDesc* d_runs = nullptr;
-  TileCol* d_tcols = nullptr;
-  uint32_t* d_remap = nullptr;
-};
-
-struct Segment {
-  std::string key;
-  int64_t num_rows = 0;
-  std::vector<int64_t> rg_rows;
-  std::vector<HostCol> cols;                     // loadable columns
-  std::set<std::string> all_columns;             // every column of the file (DESCRIBE, Commons.scala:214-221)
-  // columns of the file the engine does not decode (nested / repeated, INT96 / FIXED_LEN_BYTE_ARRAY, an encoding or
-  // codec outside the implemented set) -> why; a query referencing one fails with LK_ERR_UNSUPPORTED
-  std::map<std::string, std::string> unloaded;
-  double load_host_ms = 0, load_ms = 0;          // build_segment: host walk / total (stats)
-  bool from_put = false;                         // registered by lk_segment_put (its key is not a file path)
-  std::vector<std::pair<std::string, int>> schema;   // (name, Parquet physical type) in file order (SELECT *)
-  std::unordered_map<std::string, int> by_name;
-  std::vector<TileDesc> tiles;
+struct Segment : SegmentData {
   TileDesc* d_tiles = nullptr;
   uint8_t* d_data = nullptr;                     // page streams (def levels / values), 16-B aligned
-  size_t data_bytes = 0;
   void* d_meta = nullptr;
   size_t meta_bytes = 0;
+  bool from_put = false;                         // registered by lk_segment_put (its key is not a file path)
   std::atomic<uint64_t> last_use{0};             // LRU clock value of the last lookup (cache eviction)
   struct Engine* engine = nullptr;               // whose dictionaries its remaps reference (refs released at ~Segment)
-  int col_index(const std::string& name) const;
   ~Segment();
 };
 

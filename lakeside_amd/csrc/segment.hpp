@@ -1,0 +1,171 @@
+// Host-side segment model and engine dictionaries (no HIP): what the Parquet loader (loader.cpp) builds on the host
+// before a segment is uploaded (engine.cpp), so the loader can also run -- and be sanitized -- without a GPU
+// (tools/load_check.cpp, `make sanitize`).
+#pragma once
+#include <atomic>
+#include <cstdint>
+#include <exception>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "layout.hpp"
+
+namespace lk {
+
+// fn(0..n-1) on up to `threads` threads (the calling thread among them); the first exception is rethrown after every
+// worker has finished.  Not nested: a caller inside a parallel_for passes threads = 1 (the load's thread bound holds).
+template <class F>
+void parallel_for(size_t n, int threads, F&& fn) {
+  const size_t T = std::max<size_t>(1, std::min<size_t>(size_t(threads > 0 ? threads : 1), n));
+  if (T <= 1) {
+    for (size_t i = 0; i < n; i++) fn(i);
+    return;
+  }
+  std::atomic<size_t> next{0};
+  std::exception_ptr err;
+  std::mutex err_mu;
+  auto work = [&]() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      try {
+        fn(i);
+      } catch (...) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (!err) err = std::current_exception();
+        next.store(n);
+      }
+    }
+  };
+  std::vector<std::thread> pool;
+  for (size_t t = 1; t < T; t++) pool.emplace_back(work);
+  work();
+  for (auto& th : pool) th.join();
+  if (err) std::rethrow_exception(err);
+}
+
+// Append-only string array in fixed 64K-entry blocks behind a fixed block table: an element never moves, and
+// reading an element published before (under the owner's mutex) needs no lock, so results keep reading tag
+// strings while loads append to the dictionary.
+class StableStrs {
+ public:
+  static constexpr uint32_t kShift = 16, kBlock = 1u << kShift, kMaxBlocks = 1u << 14;   // 2^30 entries
+  size_t size() const { return n_; }
+  const std::string& operator[](size_t i) const { return blocks_[i >> kShift][i & (kBlock - 1)]; }
+  void push_back(const std::string& s) {
+    grow(n_ + 1);
+    blocks_[(n_ - 1) >> kShift][(n_ - 1) & (kBlock - 1)] = s;
+  }
+  // n entries (new ones empty), then `slot` fills them -- distinct slots from several threads at once
+  void grow(size_t n) {
+    if (n <= n_) return;
+    if (((n - 1) >> kShift) >= kMaxBlocks) throw std::length_error("dictionary exceeds 2^30 values");
+    for (size_t b = n_ >> kShift; b <= ((n - 1) >> kShift); b++)
+      if (!blocks_[b]) blocks_[b].reset(new std::string[kBlock]);
+    n_ = n;
+  }
+  std::string& slot(size_t i) { return blocks_[i >> kShift][i & (kBlock - 1)]; }
+  const std::string& back() const { return (*this)[n_ - 1]; }
+
+ private:
+  std::unique_ptr<std::unique_ptr<std::string[]>[]> blocks_{new std::unique_ptr<std::string[]>[kMaxBlocks]};
+  size_t n_ = 0;
+};
+
+// value -> id, sharded by hash so a large batch of new values is inserted by several threads at once.  Keys are views
+// of the dictionary's own StableStrs entries (stable addresses), so a lookup allocates nothing.
+class IdMap {
+ public:
+  static constexpr size_t kShards = 64;
+  static size_t hash(std::string_view s) { return std::hash<std::string_view>{}(s); }
+  static size_t shard_of(size_t h) { return (h ^ (h >> 29)) & (kShards - 1); }
+  const uint32_t* find(std::string_view s) const { return find_h(s, hash(s)); }
+  const uint32_t* find_h(std::string_view s, size_t h) const {
+    const auto& m = m_[shard_of(h)];
+    auto it = m.find(s);
+    return it == m.end() ? nullptr : &it->second;
+  }
+  size_t count(std::string_view s) const { return find(s) ? 1 : 0; }
+  void emplace(std::string_view s, uint32_t id) { m_[shard_of(hash(s))].emplace(s, id); }
+  std::unordered_map<std::string_view, uint32_t>& shard(size_t k) { return m_[k]; }
+  void swap(IdMap& o) { m_.swap(o.m_); }
+  void reserve(size_t n) {
+    for (auto& m : m_) m.reserve(n / kShards + 1);
+  }
+
+ private:
+  std::vector<std::unordered_map<std::string_view, uint32_t>> m_{kShards};
+};
+
+// Engine-global dictionary of one column name.  Values get dense ids in first-seen order, at stable
+// addresses (result tag values point into it).  Every id counts the chunk-dictionary entries of cached segments
+// that map to it (`refs`); when evictions have left as many dead ids as live ones, Engine::maybe_compact renumbers
+// the live values densely (old order kept), rewrites the cached segments' remaps and starts a new `vals` block --
+// results keep the block they were built from (shared ownership), so the group-dim space of a long-lived worker
+// tracks its cached segments, as the worker's bounded disk cache does (WorkerApi.scala:53-64).
+struct GlobalDict {
+  std::mutex mu;
+  IdMap ids;                               // keys: views of `vals` entries
+  std::shared_ptr<StableStrs> vals = std::make_shared<StableStrs>();
+  std::vector<uint32_t> refs;              // per id: cached chunk-dictionary entries mapping to it
+  size_t live = 0;                         // ids with refs > 0
+  uint64_t gen = 0;                        // compactions so far (ids are renumbered by each)
+  uint32_t intern(std::string_view s);     // caller holds mu
+  // ids of values[i] in order (caller holds mu): known values looked up, new ones interned in first-occurrence order
+  // -- the ids equal those of interning the values one by one -- on up to `threads` threads.
+  void intern_all(const std::vector<std::string_view>& values, uint32_t* ids_out, int threads);
+  size_t size() const { return vals->size(); }
+  const std::string& operator[](size_t i) const { return (*vals)[i]; }
+};
+
+struct HostCol {
+  std::string name;
+  int ptype = -1;
+  bool nullable = false;
+  bool is_string = false;
+  bool unsupported = false;
+  bool any_nulls = false;
+  // page summaries (load time), so a query's lean-tile test costs O(1) per column instead of a walk over its pages:
+  bool pages_lean_name = false;           // every page: dictionary indices, chunk dictionary <= 64 values, 1..6 bits
+  bool pages_lean_late = false;           // every page: dictionary indices of <= 32 bits
+  uint64_t compressed_bytes = 0;          // Σ ColumnMetaData.total_compressed_size (algorithmic bytes)
+  std::vector<PageDesc> pages;            // host copy (planner reads dict sizes / null flags)
+  std::vector<RunDesc> runs;              // load-time only
+  std::vector<TileCol> tcols;             // load-time only
+  std::vector<uint32_t> remap;            // load-time only
+  size_t nremap = 0;                      // entries of d_remap counted in the column dictionary's refs
+  PageDesc* d_pages = nullptr;
+  RunDesc* d_runs = nullptr;
+  TileCol* d_tcols = nullptr;
+  uint32_t* d_remap = nullptr;
+};
+
+// The host part of a cached segment (the loader's output; engine.hpp's Segment adds the device copies).
+struct SegmentData {
+  std::string key;
+  int64_t num_rows = 0;
+  std::vector<int64_t> rg_rows;
+  std::vector<HostCol> cols;                     // loadable columns
+  std::set<std::string> all_columns;             // every column of the file (DESCRIBE, Commons.scala:214-221)
+  // columns of the file the engine does not decode (nested / repeated, INT96 / FIXED_LEN_BYTE_ARRAY, an encoding or
+  // codec outside the implemented set) -> why; a query referencing one fails with LK_ERR_UNSUPPORTED
+  std::map<std::string, std::string> unloaded;
+  double load_host_ms = 0, load_ms = 0;          // build_segment: host walk / total (stats)
+  std::vector<std::pair<std::string, int>> schema;   // (name, Parquet physical type) in file order (SELECT *)
+  std::unordered_map<std::string, int> by_name;
+  std::vector<TileDesc> tiles;
+  size_t data_bytes = 0;                         // the page-stream area (device: d_data)
+  int col_index(const std::string& name) const;
+};
+
+}  // namespace lk

@@ -107,6 +107,74 @@ def plan_text(pr: dx.PushDownRequest, glob_size: int) -> Tuple[str, List[str], L
     return "\n".join(quote(x, safe="") for x in t) + "\n", strcols, gbs
 
 
+def plan_text_tag(pr: dx.PushDownRequest, tag: str, glob_size: int) -> str:
+    """A tag query (isTagQuery + tagDataType, BaseExpr.scala:127-143) in lkcpu's line format: the tag is string column
+    0 and the only key; rows are counted (COUNT(*), NULL values included) in one bucket."""
+    leaves = _leaves(pr.baseExpr.filter, []) if pr.baseExpr.filter is not None else []
+    strcols = [tag]
+    for l in leaves:
+        if l.op in dx.NUMERIC_OPS:
+            raise NotImplementedError("lkcpu: numeric leaves in a tag query")
+        if l.k not in strcols:
+            strcols.append(l.k)
+    if len(strcols) > 7:
+        raise NotImplementedError("lkcpu: at most 7 string columns")
+    t = ["tag", "count", dx.VALUE, str(glob_size), str(len(pr.segmentRequests))]
+    for s in pr.segmentRequests:
+        t += [str(s.startTs), str(s.endTs), str(s.stepInMillis)]
+    t += [str(len(strcols))] + strcols + ["0"]
+    t += [str(len(leaves))]
+    for l in leaves:
+        t += [str(strcols.index(l.k)), l.op, str(len(l.v))] + list(l.v)
+    prog = _postfix(pr.baseExpr.filter, leaves, []) if leaves else []
+    t += [str(len(prog))] + [str(x) for x in prog]
+    fs = sorted(dx.field_set(pr.baseExpr))
+    t += [str(len(fs))] + fs
+    return "\n".join(quote(x, safe="") for x in t) + "\n"
+
+
+def evaluate_tag_counts(pr: dx.PushDownRequest, tag: str, glob_size: int, blobs: Sequence, threads: int = 0,
+                        timing: Optional[list] = None) -> Dict[Optional[str], int]:
+    """Tag query counts merged over the globs (the engine's LK_MERGED tag table, oracle/dataexpr.evaluate_tag_merged):
+    {tag text (None: NULL / "" / "null") -> COUNT(*)}."""
+    text = plan_text_tag(pr, tag, glob_size)
+    n = len(blobs)
+    ptrs = (ctypes.c_void_p * max(1, n))()
+    sizes = (ctypes.c_size_t * max(1, n))()
+    keep = []
+    for i, b in enumerate(blobs):
+        if isinstance(b, (bytes, bytearray)):
+            buf = ctypes.create_string_buffer(bytes(b), len(b))
+            keep.append(buf)
+            ptrs[i], sizes[i] = ctypes.cast(buf, ctypes.c_void_p), len(b)
+        else:
+            ptrs[i], sizes[i] = ctypes.cast(b[0], ctypes.c_void_p), b[1]
+    L = lib()
+    t0 = time.perf_counter()
+    h = L.lkcpu_eval(text.encode(), ptrs, sizes, n, threads)
+    if timing is not None:
+        timing.append(time.perf_counter() - t0)
+    if not h:
+        raise RuntimeError(L.lkcpu_error().decode())
+    try:
+        m = L.lkcpu_ncells(h)
+        nc = L.lkcpu_ncols(h)
+        arrs = [np.zeros(m, t) for t in (np.int32, np.int64, np.uint64, np.uint64, np.float64, np.float64, np.float64,
+                                          np.float64, np.uint8)]
+        keys = np.zeros(max(1, m * nc), np.int32)
+        L.lkcpu_cells(h, *[a.ctypes.data for a in arrs + [keys]])
+        rows = arrs[2]
+        out: Dict[Optional[str], int] = {}
+        for i in range(m):
+            kid = int(keys[i * nc])
+            v = L.lkcpu_key_string(h, 0, kid) if kid >= 0 else None
+            s = None if v is None or v in (b"", b"null") else v.decode()
+            out[s] = out.get(s, 0) + int(rows[i])
+        return out
+    finally:
+        L.lkcpu_free(h)
+
+
 def _dd(*xs):
     """Correctly rounded sum of double-double parts (IEEE propagation for non-finite values)."""
     return math.fsum(xs) if all(math.isfinite(x) for x in xs) else float(np.sum(np.array(xs)))

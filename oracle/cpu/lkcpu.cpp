@@ -18,6 +18,7 @@
 //   Kleene filter over eq / != / in / not_in / has / exists / regex   BaseExpr.scala:470-511
 //   GROUP BY bucket, groupBys present in the glob, name; NULL key     BaseExpr.scala:338-346, 400-404
 //   sum / min / max / count (NULL values ignored), avg = sum / count  BaseExpr.scala:319-405
+//   tag queries: COUNT(*) per tag value (NULL its own group)          BaseExpr.scala:127-143
 // Regex leaves use POSIX ERE (regcomp, REG_ICASE): identical to RE2 on the ASCII patterns of the bench configs
 // (the exact RE2 semantics are tested separately, tests/test_regex.py).  Pages must be uncompressed (the bench's
 // synthetic segments are); anything else is refused.
@@ -412,6 +413,7 @@ enum { OP_AND = -1, OP_OR = -2, OP_NOT = -3 };
 
 struct Plan {
   bool metrics = false;
+  bool tag = false;                        // tag query: strcols[0] is the tag, the only key; COUNT(*), one bucket
   std::string agg, vcol;
   int glob_size = 10;
   std::vector<int64_t> start, end, step;   // per segment request
@@ -579,7 +581,11 @@ Plan parse_plan(const char* text) {
   };
   auto num = [&]() { return std::stoll(next()); };
   Plan P;
-  P.metrics = next() == "metrics";
+  {
+    const std::string ds = next();
+    P.metrics = ds == "metrics";
+    P.tag = ds == "tag";
+  }
   P.agg = next();
   P.vcol = next();
   P.glob_size = int(num());
@@ -676,6 +682,11 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
     // timestamp, name, value)
     for (auto& l : P.leaves)
       if (!nonexist.count(leaf_col(l)) && !uni.count(leaf_col(l))) skip[g] = 1;
+    if (P.tag) {   // SELECT "<tag>", COUNT(*) ... GROUP BY "<tag>" (BaseExpr.scala:127-143): the tag must exist
+      if (!uni.count("_cardinalhq.timestamp") || !uni.count(P.strcols[0])) skip[g] = 1;
+      keycols[g].push_back(0);
+      continue;
+    }
     if (!uni.count("_cardinalhq.timestamp") || !uni.count("_cardinalhq.name") || !uni.count(P.vcol)) skip[g] = 1;
     keycols[g].push_back(0);
     for (int c : P.gby)
@@ -722,7 +733,7 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
       };
       Chunk tsc, vc;
       const bool has_ts = load("_cardinalhq.timestamp", false, tsc);
-      const bool has_v = load(P.vcol, false, vc);
+      const bool has_v = !P.tag && load(P.vcol, false, vc);
       std::vector<Chunk> sc(static_cast<size_t>(nstr));
       std::vector<char> has_s(static_cast<size_t>(nstr));
       // per string column: chunk code -> (leaf T bits, global id)
@@ -784,7 +795,7 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
         F |= lf;
         if (!kleene(P.prog, T, F)) continue;
         Key k;
-        k.ts = P.metrics ? t : t - int64_t(std::fmod(double(t), double(step)));
+        k.ts = P.tag ? 0 : P.metrics ? t : t - int64_t(std::fmod(double(t), double(step)));
         for (int j = 0; j < 7; j++) k.g[j] = -1;
         for (size_t j = 0; j < keycols[g].size(); j++) {
           const int c = keycols[g][j];

@@ -1,0 +1,38 @@
+"""The segment loader's host part (lakeside_amd/csrc/loader.cpp) without a GPU: tools/load_check.cpp loads the golden,
+compressed, PLAIN-fallback, numeric-dictionary, large-dictionary and truncated fixtures and prints a digest of every
+segment (staged stream bytes, pages, runs, tile columns, remaps) and of the engine dictionaries.  The digest must not
+depend on the load thread count: the parallel chunk walk, the parallel dictionary interning (GlobalDict::intern_all:
+ids in first-occurrence order) and the parallel staging copy give the one-thread result.  `make sanitize` runs the
+same harness under ASan + UBSan and TSan."""
+import glob
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def harness(tmp_path_factory):
+    subprocess.run(["make", "-C", ROOT, "build/load_check"], check=True, capture_output=True)
+    fix = str(tmp_path_factory.mktemp("load_fixtures"))
+    subprocess.run([sys.executable, os.path.join(ROOT, "tools", "make_load_fixtures.py"), fix], check=True)
+    files = sorted(glob.glob(os.path.join(ROOT, "tests", "golden", "segments", "*.parquet"))) + \
+        sorted(glob.glob(os.path.join(fix, "*.parquet")))
+    return os.path.join(ROOT, "build", "load_check"), files
+
+
+def test_loader_digest_independent_of_threads(harness):
+    exe, files = harness
+    outs = [subprocess.run([exe, str(t)] + files, check=True, capture_output=True, text=True, timeout=300).stdout
+            for t in (1, 3, 8)]
+    assert outs[0] == outs[1] == outs[2]
+    lines = outs[0].splitlines()
+    assert lines[-1] == "failures=1"                                 # the truncated fixture, and only it
+    assert any(l.startswith("truncated.parquet error") for l in lines)
+    big = [l for l in lines if l.startswith("  col resource.container.id")]
+    assert big and all(int(l.split("remap=")[1].split()[0]) >= 1 << 16 for l in big)   # the parallel intern path
+    codecs = {l.split()[5] for l in lines if l.startswith("codec_")}
+    assert len(codecs) == 1                  # every codec / page version stages the same bytes as the others

@@ -155,3 +155,27 @@ def test_columnar_merge_synthetic_shards(agg, gbs):
         parts.append(cpu.evaluate_cell_table(dx.parse_pushdown(json.dumps(sub)), 10, blobs[2 * r:2 * r + 2], threads=2))
     cpu.assert_columns_equal(cpu.merge_cell_table(cpu.CellTable.concat(parts), agg, bool(gbs)), want, agg,
                              f"columnar shards {agg} {gbs}")
+
+
+def _tag_case_list():
+    with open(os.path.join(GOLDEN, "tag_cases.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", _tag_case_list(), ids=lambda c: c["name"])
+def test_cpu_tag_counts_golden(case):
+    """The C++ restatement's tag mode (the bench's full-size tag validator) == the golden merged tag rows."""
+    from oracle import cpu, dataexpr as dx
+    paths = [os.path.join(GOLDEN, p) for p in case["segments"]]
+    blobs = [open(p, "rb").read() for p in paths]
+    text = json.dumps(case["request"])
+    tag = dx.parse_tag_data_type(text)
+    try:
+        got = cpu.evaluate_tag_counts(dx.parse_pushdown(text), tag, case["glob_size"], blobs, threads=3)
+    except RuntimeError as e:
+        if "compressed" in str(e) or "PLAIN" in str(e) or "non-" in str(e):
+            pytest.skip(str(e))
+        raise
+    rows = [dx.tag_row_tags(tag, v, c) for v, c in got.items()]
+    key = lambda t: sorted(t.items())   # noqa: E731
+    assert sorted(rows, key=key) == sorted(case["expected_merged"], key=key)
