@@ -373,7 +373,7 @@ void Engine::compact_locked(const std::string& col) {
   GlobalDict& gd = dict(col);
   std::vector<uint32_t> map;
   auto nv = std::make_shared<StableStrs>();
-  IdMap ids;
+  IdMap ids(nv.get());
   std::vector<uint32_t> refs;
   {
     std::lock_guard<std::mutex> dg(gd.mu);
@@ -386,7 +386,7 @@ void Engine::compact_locked(const std::string& col) {
       if (gd.refs[i] == 0) continue;
       map[i] = uint32_t(nv->size());
       nv->push_back(gd[i]);
-      ids.emplace(nv->back(), map[i]);
+      ids.emplace(map[i]);
       refs.push_back(gd.refs[i]);
     }
   }

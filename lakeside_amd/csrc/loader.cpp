@@ -6,6 +6,8 @@
 #include <atomic>
 #include <chrono>
 #include <climits>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -28,11 +30,13 @@ static inline size_t align_up(size_t x, size_t a = kAlign) { return (x + a - 1) 
 // engine-global dictionaries: one per column name; chunk dictionaries remap into them at load
 // ------------------------------------------------------------------------------------------------
 uint32_t GlobalDict::intern(std::string_view s) {
-  if (const uint32_t* f = ids.find(s)) return *f;
+  const uint64_t h = IdMap::hash(s);
+  const uint32_t f = ids.find_h(s, h);
+  if (f != IdMap::kNone) return f;
   const uint32_t id = uint32_t(vals->size());
   vals->push_back(std::string(s));
   refs.push_back(0);
-  ids.emplace(std::string_view((*vals)[id]), id);
+  ids.emplace_h(id, h);
   return id;
 }
 
@@ -47,27 +51,63 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
     for (size_t i = 0; i < n; i++) out[i] = intern(v[i]);
     return;
   }
+  static const bool timing = getenv("LK_LOAD_TIMING") != nullptr;
+  const auto t0 = std::chrono::steady_clock::now();
+  auto mark = [&](const char* w) {
+    if (timing) fprintf(stderr, "[lk intern] %-8s %8.1f ms (%zu values)\n", w, std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), n);
+  };
   constexpr size_t K = IdMap::kShards;
   const size_t B = std::min<size_t>(size_t(threads) * 8, (n + 4095) / 4096), bs = (n + B - 1) / B;
-  std::vector<size_t> h(n);
+  std::vector<uint64_t> h(n);
   parallel_for(B, threads, [&](size_t b) {
-    for (size_t i = b * bs; i < std::min(n, (b + 1) * bs); i++) {
+    const size_t lo = b * bs, hi = std::min(n, (b + 1) * bs);
+    constexpr size_t D = 16;   // lookups in flight: slot lines prefetched D values ahead (each lookup is a cache miss)
+    for (size_t i = lo; i < std::min(hi, lo + D); i++) {
       h[i] = IdMap::hash(v[i]);
-      const uint32_t* f = ids.find_h(v[i], h[i]);
-      out[i] = f ? *f : UINT32_MAX;
+      ids.prefetch(h[i]);
+    }
+    for (size_t i = lo; i < hi; i++) {
+      if (i + D < hi) {
+        h[i + D] = IdMap::hash(v[i + D]);
+        ids.prefetch(h[i + D]);
+      }
+      out[i] = ids.find_h(v[i], h[i]);   // kNone (UINT32_MAX) when unknown
     }
   });
+  mark("lookup");
   std::vector<std::vector<uint32_t>> lists(B * K);   // [block][shard]: positions of unknown values, ascending
   parallel_for(B, threads, [&](size_t b) {
     for (size_t i = b * bs; i < std::min(n, (b + 1) * bs); i++)
       if (out[i] == UINT32_MAX) lists[b * K + IdMap::shard_of(h[i])].push_back(uint32_t(i));
   });
+  mark("lists");
   std::vector<uint32_t> first(n, UINT32_MAX);   // unknown positions: the first position of the same value
   parallel_for(K, threads, [&](size_t k) {
-    std::unordered_map<std::string_view, uint32_t> seen;
+    // open addressing over this shard's positions (slot: hash tag | position), walked in position order
+    size_t m = 0;
+    for (size_t b = 0; b < B; b++) m += lists[b * K + k].size();
+    size_t cap = 64;
+    while (cap * 7 < m * 10) cap <<= 1;
+    std::vector<uint64_t> tab(cap, 0);
+    const size_t mask = cap - 1;
     for (size_t b = 0; b < B; b++)
-      for (uint32_t i : lists[b * K + k]) first[i] = seen.emplace(v[i], i).first->second;
+      for (uint32_t i : lists[b * K + k]) {
+        const uint64_t tag = ((h[i] >> 32) & 0x7fffffffull) | 0x80000000ull;
+        for (size_t j = size_t(h[i] >> 6) & mask;; j = (j + 1) & mask) {
+          const uint64_t x = tab[j];
+          if (!x) {
+            tab[j] = (tag << 32) | i;
+            first[i] = i;
+            break;
+          }
+          if ((x >> 32) == tag && v[uint32_t(x)] == v[i]) {
+            first[i] = uint32_t(x);
+            break;
+          }
+        }
+      }
   });
+  mark("dedup");
   std::vector<size_t> base(B + 1, 0);
   parallel_for(B, threads, [&](size_t b) {
     size_t c = 0;
@@ -75,10 +115,12 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
     base[b + 1] = c;
   });
   for (size_t b = 0; b < B; b++) base[b + 1] += base[b];
+  mark("count");
   const size_t old = vals->size(), added = base[B];
   if (old + added > size_t(UINT32_MAX)) throw std::length_error("dictionary exceeds 2^32 values");
   vals->grow(old + added);
   refs.resize(old + added, 0);
+  mark("grow");
   parallel_for(B, threads, [&](size_t b) {   // first occurrences: ids in position order, strings stored
     uint32_t id = uint32_t(old + base[b]);
     for (size_t i = b * bs; i < std::min(n, (b + 1) * bs); i++)
@@ -87,16 +129,22 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
         out[i] = id++;
       }
   });
+  mark("store");
   parallel_for(B, threads, [&](size_t b) {   // repeats (their first occurrence is final after the previous pass)
     for (size_t i = b * bs; i < std::min(n, (b + 1) * bs); i++)
       if (first[i] != UINT32_MAX && first[i] != i) out[i] = out[first[i]];
   });
+  mark("repeats");
   parallel_for(K, threads, [&](size_t k) {   // index the new values, one thread per shard
-    auto& m = ids.shard(k);
+    size_t nk = 0;
+    for (size_t b = 0; b < B; b++)
+      for (uint32_t i : lists[b * K + k]) nk += first[i] == i;
+    ids.reserve_shard(k, nk);
     for (size_t b = 0; b < B; b++)
       for (uint32_t i : lists[b * K + k])
-        if (first[i] == i) m.emplace(std::string_view((*vals)[out[i]]), out[i]);
+        if (first[i] == i) ids.emplace_h(out[i], h[i]);
   });
+  mark("index");
 }
 
 int SegmentData::col_index(const std::string& name) const {
@@ -575,6 +623,13 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
     S->rg_rows.push_back(g.num_rows);
   }
 
+  static const bool timing = getenv("LK_LOAD_TIMING") != nullptr;   // diagnostics: stage times on stderr
+  auto mark = [&](const char* what) {
+    if (timing)
+      fprintf(stderr, "[lk load] %-8s %9.1f ms  %s\n", what,
+              std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count(), key.c_str());
+  };
+  mark("footer");
   // ---- 1. every (column, row group) chunk walked in parallel ----
   const size_t ncol = S->cols.size();
   std::vector<int> leaf_of(ncol);
@@ -624,6 +679,7 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
   }
   const size_t nc = S->cols.size();
 
+  mark("walk");
   // ---- 2. per column, in row-group order: intern dictionaries, concatenate runs and pages, place streams ----
   // Byte offset of each chunk's stream area in the segment: row-group major (a row group's columns side by side, as
   // in the file), so the streams one tile reads lie close together (column-major placement measured ~1.8x slower
@@ -656,6 +712,7 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
     std::lock_guard<std::mutex> g(gd.mu);
     gd.intern_all(sv, col.remap.data(), t);
   };
+  mark("layout");
   std::vector<char> big(nc, 0);
   for (size_t ci = 0; ci < nc; ci++) {
     size_t ndict = 0;
@@ -665,6 +722,7 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
       intern_column(ci, threads);
     }
   }
+  mark("intern");
   parallel_for(nc, threads, [&](size_t ci) {
     HostCol& col = S->cols[ci];
     size_t npages = 0, nruns = 0, ndict = 0;
@@ -697,6 +755,7 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
     }
   });
 
+  mark("concat");
   // ---- 3. tiles, per row group in parallel ----
   std::vector<std::vector<TileDesc>> rg_tiles(nrg);
   std::vector<std::vector<std::vector<TileCol>>> rg_tcols(nrg);
@@ -717,6 +776,7 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
     col.pages.reserve(pages[ci].size());
     for (auto& hp : pages[ci]) col.pages.push_back(hp.d);
   }
+  mark("tiles");
   H.host_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   S->load_host_ms = H.host_ms;
   return H;

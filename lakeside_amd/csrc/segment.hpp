@@ -82,29 +82,83 @@ class StableStrs {
   size_t n_ = 0;
 };
 
-// value -> id, sharded by hash so a large batch of new values is inserted by several threads at once.  Keys are views
-// of the dictionary's own StableStrs entries (stable addresses), so a lookup allocates nothing.
+// value -> id of one dictionary: open addressing over 64 hash shards (a shard per thread when a large batch of new
+// values is indexed), each slot one word -- a 31-bit hash tag and the id -- so a lookup costs one slot read and, on a
+// tag match, one string compare against the dictionary's own entry (no node chasing, no key copies).
 class IdMap {
  public:
   static constexpr size_t kShards = 64;
-  static size_t hash(std::string_view s) { return std::hash<std::string_view>{}(s); }
-  static size_t shard_of(size_t h) { return (h ^ (h >> 29)) & (kShards - 1); }
-  const uint32_t* find(std::string_view s) const { return find_h(s, hash(s)); }
-  const uint32_t* find_h(std::string_view s, size_t h) const {
-    const auto& m = m_[shard_of(h)];
-    auto it = m.find(s);
-    return it == m.end() ? nullptr : &it->second;
+  static constexpr uint32_t kNone = UINT32_MAX;
+  explicit IdMap(const StableStrs* strs = nullptr) : strs_(strs), m_(kShards) {}
+  static uint64_t hash(std::string_view s) {   // FNV-1a 64 + a final mix (the shard takes the low bits)
+    uint64_t h = 1469598103934665603ull;
+    for (char c : s) h = (h ^ uint8_t(c)) * 1099511628211ull;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    return h ^ (h >> 29);
   }
-  size_t count(std::string_view s) const { return find(s) ? 1 : 0; }
-  void emplace(std::string_view s, uint32_t id) { m_[shard_of(hash(s))].emplace(s, id); }
-  std::unordered_map<std::string_view, uint32_t>& shard(size_t k) { return m_[k]; }
-  void swap(IdMap& o) { m_.swap(o.m_); }
+  static size_t shard_of(uint64_t h) { return size_t(h & (kShards - 1)); }
+  uint32_t find(std::string_view s) const { return find_h(s, hash(s)); }
+  uint32_t find_h(std::string_view s, uint64_t h) const {
+    const Shard& sh = m_[shard_of(h)];
+    if (sh.slots.empty()) return kNone;
+    const uint64_t tag = tag_of(h), mask = sh.slots.size() - 1;
+    for (size_t i = size_t(h >> 6) & mask;; i = (i + 1) & mask) {
+      const uint64_t v = sh.slots[i];
+      if (!v) return kNone;
+      if ((v >> 32) == tag && (*strs_)[uint32_t(v)] == s) return uint32_t(v);
+    }
+  }
+  size_t count(std::string_view s) const { return find(s) != kNone ? 1 : 0; }
+  void prefetch(uint64_t h) const {
+    const Shard& sh = m_[shard_of(h)];
+    if (!sh.slots.empty()) __builtin_prefetch(&sh.slots[size_t(h >> 6) & (sh.slots.size() - 1)]);
+  }
+  // id -> its value (*strs)[id] must not be in the map yet
+  void emplace(uint32_t id) { emplace_h(id, hash((*strs_)[id])); }
+  void emplace_h(uint32_t id, uint64_t h) {
+    Shard& sh = m_[shard_of(h)];
+    if ((sh.n + 1) * 10 > sh.slots.size() * 7) grow(sh, std::max<size_t>(64, sh.slots.size() * 2));
+    insert(sh, id, h);
+  }
+  // room for n more entries in shard k (a batch of new values indexed by one thread per shard)
+  void reserve_shard(size_t k, size_t n) {
+    Shard& sh = m_[k];
+    size_t cap = std::max<size_t>(64, sh.slots.size());
+    while ((sh.n + n) * 10 > cap * 7) cap *= 2;
+    if (cap != sh.slots.size()) grow(sh, cap);
+  }
   void reserve(size_t n) {
-    for (auto& m : m_) m.reserve(n / kShards + 1);
+    for (size_t k = 0; k < kShards; k++) reserve_shard(k, n / kShards + 1);
+  }
+  void swap(IdMap& o) {
+    std::swap(strs_, o.strs_);
+    m_.swap(o.m_);
   }
 
  private:
-  std::vector<std::unordered_map<std::string_view, uint32_t>> m_{kShards};
+  struct Shard {
+    std::vector<uint64_t> slots;   // 0: empty; else (tag | 2^31) << 32 | id
+    size_t n = 0;
+  };
+  static uint64_t tag_of(uint64_t h) { return ((h >> 32) & 0x7fffffffull) | 0x80000000ull; }
+  static void insert(Shard& sh, uint32_t id, uint64_t h) {
+    const uint64_t mask = sh.slots.size() - 1;
+    size_t i = size_t(h >> 6) & mask;
+    while (sh.slots[i]) i = (i + 1) & mask;
+    sh.slots[i] = (tag_of(h) << 32) | id;
+    sh.n++;
+  }
+  void grow(Shard& sh, size_t cap) {
+    std::vector<uint64_t> old;
+    old.swap(sh.slots);
+    sh.slots.assign(cap, 0);
+    sh.n = 0;
+    for (uint64_t v : old)
+      if (v) insert(sh, uint32_t(v), hash((*strs_)[uint32_t(v)]));
+  }
+  const StableStrs* strs_;
+  std::vector<Shard> m_;
 };
 
 // Engine-global dictionary of one column name.  Values get dense ids in first-seen order, at stable
@@ -115,8 +169,8 @@ class IdMap {
 // tracks its cached segments, as the worker's bounded disk cache does (WorkerApi.scala:53-64).
 struct GlobalDict {
   std::mutex mu;
-  IdMap ids;                               // keys: views of `vals` entries
   std::shared_ptr<StableStrs> vals = std::make_shared<StableStrs>();
+  IdMap ids{vals.get()};                   // over `vals` (a compaction swaps both)
   std::vector<uint32_t> refs;              // per id: cached chunk-dictionary entries mapping to it
   size_t live = 0;                         // ids with refs > 0
   uint64_t gen = 0;                        // compactions so far (ids are renumbered by each)

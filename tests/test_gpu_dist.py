@@ -421,8 +421,12 @@ def _worker_fault(rank, world, port):
         # failure once another call unlinks names.  Block 0 is held by a live result, call A creates block 1 and rank
         # 1 cannot map it (LK_FAULT=emit_map@1); once block 0 is free again call C uses it (and, before the fix,
         # unlinked every name in the pool), then call D -- block 0 held again -- needs block 1 and must succeed.
+        for k in ("LK_KEYRANGE_MIN_CELLS", "LK_DENSE_MAX_CELLS"):
+            os.environ.pop(k, None)
         os.environ.update(kr)
         held = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])   # block 0
+        if rank == 0:
+            assert held.stats["emit"] == "shared_host_block", held.stats
         os.environ["LK_FAULT"] = "emit_map@1"
         try:
             eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # A: block 1
@@ -430,8 +434,6 @@ def _worker_fault(rank, world, port):
         except LakesideError as e:
             assert e.code == LK_ERR_DEVICE, str(e)
         os.environ.pop("LK_FAULT")
-        if rank == 0:
-            assert held.stats["emit"] == "shared_host_block", held.stats
         del held
         c = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # C: block 0
         d = eng.eval_pushdown_dist(json.dumps(case["request"]), paths, None, case["glob_size"])      # D: block 1

@@ -95,8 +95,7 @@ int main(int argc, char** argv) {
     for (size_t i = 0; i < d.size(); i++) {
       h = fnv(h, d[i].data(), d[i].size());
       h = fnv(h, "\0", 1);
-      const uint32_t* id = d.ids.find(d[i]);
-      if (!id || *id != i) {
+      if (d.ids.find(d[i]) != i) {
         printf("dict %s: value %zu is not indexed under its id\n", kv.first.c_str(), i);
         return 1;
       }
