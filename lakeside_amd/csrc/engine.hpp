@@ -16,6 +16,8 @@
 #include <unordered_set>
 #include <vector>
 
+#include "ddsketch.hpp"
+#include "hll.hpp"
 #include "layout.hpp"
 #include "plan.hpp"
 #include "segment.hpp"
@@ -262,6 +264,11 @@ struct lk_result {
   std::vector<std::shared_ptr<const void>> keep; // dictionary blocks tag pointers point into
   std::string stats;
   std::vector<std::string> sketches;             // percentile rows: the serialized DDSketch of each row
+  // internal (evaluate_mixed_steps): the rows' sketches as objects, so rows of globs with different steps can be
+  // merged per (timestamp, tags) as query-api merges sketches (TimeGroupedSketchAggregator.scala:34-43)
+  bool keep_sketches = false;
+  std::vector<lk::dd::Sketch> dd_objs;           // percentile rows
+  std::vector<lk::hll::Sketch> hll_objs;         // cardinality rows
 
   lk_result() = default;
   lk_result(const lk_result&) = delete;

