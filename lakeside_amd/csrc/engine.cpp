@@ -632,13 +632,15 @@ std::shared_ptr<Segment> Engine::get_segment(const std::string& key, bool load_o
     }
   }
   if (!load_on_miss) return nullptr;
-  {
+  std::ifstream f(key, std::ios::binary);
+  if (!f) {
+    // an evicted lk_segment_put key that is not a readable file: the caller must put it again (LK_ERR_EVICTED); a put
+    // key that is also a real path is simply reloaded from the file below, as any cache miss
     std::lock_guard<std::mutex> g(cache_mu);
     if (evicted_puts.count(key))
       throw PlanError(LK_ERR_EVICTED, "segment " + key + " was evicted from the HBM cache (lk_segment_put it again)");
+    throw PlanError(LK_ERR_IO, "cannot open segment " + key);
   }
-  std::ifstream f(key, std::ios::binary);
-  if (!f) throw PlanError(LK_ERR_IO, "cannot open segment " + key);
   std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
   put_segment(key, buf.data(), buf.size(), false);
   std::lock_guard<std::mutex> g(cache_mu);
@@ -658,7 +660,13 @@ Engine::Engine(int dev) : device(dev) {
 }
 
 Engine::~Engine() {
-  life.reset();   // results' weak references expire first
+  // results' weak references expire first; a result still reading through the engine (lk_result_tag_dictionary holds
+  // the token while it calls dict_ptrs) finishes before anything is torn down
+  {
+    std::weak_ptr<const char> w = life;
+    life.reset();
+    while (!w.expired()) std::this_thread::yield();
+  }
   (void)hipSetDevice(device);
   comm_destroy();
   ctx_free.clear();

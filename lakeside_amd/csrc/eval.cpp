@@ -1299,12 +1299,13 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       }
   const size_t o_maps = reserve(flat.size() * 4);
   const size_t stage_bytes = off;
+  const size_t o_tail = reserve(64);   // host side only: the small-table epilogue's flags and row count (mapped)
   // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)
   uint8_t* hbuf = nullptr;
   uint8_t* dbuf = nullptr;
   try {
     HIP_TRY(hipSetDevice(E.device));
-    hbuf = static_cast<uint8_t*>(X->pinned_buf(stage_bytes));
+    hbuf = static_cast<uint8_t*>(X->pinned_buf(o_tail + 64));
     dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
   } catch (const PlanError& e) {
     if (!dist) throw;
@@ -1374,10 +1375,11 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     for (size_t s = 0; s < strs.size(); s++)
       if (((late_mask >> dev_of[s]) & 1u) && !strs[s].leaves.empty()) late_leaves = true;
     P.late_chunk = (late_leaves && ngroups <= 65536u && getenv("LK_LATE_CHUNK")) ? 1u : 0u;
-    // speculative value gather for late-filtered rows (lean_kernel.hpp rowsN): A/B via
-    // LK_SPEC_GATHER=0/1 (default: on -- see DESIGN §6 for the measurement)
+    // speculative value gather for late-filtered rows (lean_kernel.hpp rowsN): opt-in
+    // (LK_SPEC_GATHER=1) -- measured slower on C3, 2.155 vs 1.968 ms: the loads of the rows the late filter drops
+    // (half of C3's listed rows) cost more than the round trip they save (profiles/r05_bench_c3*.json)
     const char* sg = getenv("LK_SPEC_GATHER");
-    P.spec_gather = (late_leaves && !(sg && *sg == '0')) ? 1u : 0u;
+    P.spec_gather = (late_leaves && sg && *sg == '1') ? 1u : 0u;
   }
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;
@@ -1455,13 +1457,24 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     P.ext = reinterpret_cast<unsigned long long*>(tb + ncl * 32);
     P.hkeys = hashed ? reinterpret_cast<unsigned long long*>(tb + ncl * 40) : nullptr;
     P.hmask = hashed ? ncl - 1 : 0;
-    HIP_TRY(hipMemsetAsync(tb, 0, ncl * 16, st));
-    if (kagg == AGG_SUM) HIP_TRY(hipMemsetAsync(tb + ncl * 16, 0, ncl * 16, st));
-    if (kagg == AGG_SUM && (P.lean & LEAN_SUM_EXISTS))
-      HIP_TRY(launch_fill_u64(reinterpret_cast<unsigned long long*>(P.hi), ncl, NEG_ZERO_BITS, st));
-    if (kagg == AGG_MIN) HIP_TRY(hipMemsetAsync(P.ext, 0xff, ncl * 8, st));
-    if (kagg == AGG_MAX) HIP_TRY(hipMemsetAsync(P.ext, 0, ncl * 8, st));
-    if (hashed) HIP_TRY(hipMemsetAsync(P.hkeys, 0xff, ncl * 8, st));
+    // one launch: the planes this aggregate reads, and the scan flags + plan-bytes counter (4 x u32)
+    FillList F{};
+    auto add = [&](void* p, size_t n, unsigned long long v) {
+      F.p[F.count] = static_cast<unsigned long long*>(p);
+      F.n[F.count] = n;
+      F.v[F.count] = v;
+      F.count++;
+    };
+    add(tb, ncl * 2, 0ull);                                           // rows | cnt
+    if (kagg == AGG_SUM) {
+      add(P.hi, ncl, (P.lean & LEAN_SUM_EXISTS) ? NEG_ZERO_BITS : 0ull);
+      add(P.lo, ncl, 0ull);
+    }
+    if (kagg == AGG_MIN) add(P.ext, ncl, ~0ull);
+    if (kagg == AGG_MAX) add(P.ext, ncl, 0ull);
+    if (hashed) add(P.hkeys, ncl, ~0ull);
+    add(P.flags, 2, 0ull);                                            // flags + the 64-bit plan-bytes counter
+    HIP_TRY(launch_fill_many(F, st));
   };
   // Multi-GPU reduce shape (decided before the scan: its receive buffers are placed before the scan's agreement
   // point, so no rank can fail alone between that agreement and the first point-to-point transfer).
@@ -1484,8 +1497,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         comm_reduce_prepare(E, *X, nc);
       }
     }
-    zero_table(nc, hash_mode);
-    HIP_TRY(hipMemsetAsync(P.flags, 0, 16, st));   // flags + the 64-bit plan-bytes counter behind them
+    zero_table(nc, hash_mode);   // (and the flags)
     P.plan_bytes = (flags & LK_PLAN_BYTES) ? reinterpret_cast<unsigned long long*>(P.flags + 2) : nullptr;
     HIP_TRY(hipEventRecord(X->ev_scan0, st));
     const size_t nstamp = size_t(P.max_tiles) * P.nsegs * LK_NSTAMP;
@@ -1516,6 +1528,31 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       HIP_TRY(launch_ex_scan(XG, st));
     }
     HIP_TRY(hipEventRecord(X->ev_scan1, st));
+    // small dense single-GPU tables: fixup, rows and flags in one single-workgroup launch (launch_epilogue_small),
+    // read after one synchronization from mapped pinned memory -- no fixup / count / scan / write launches, no copies
+    const bool epilogue = fast_final && !fast_done && !P.stamps && nc <= kEpilogueMax && out_keys <= kEpilogueMax &&
+                          !getenv("LK_NO_EPILOGUE");
+    if (epilogue) {
+      res->alloc_rows(size_t(out_keys), per_glob_rows);
+      if (res->blk.pinned) {
+        FParams Fs{};
+        Fs.rows = P.rows;
+        Fs.cnt = P.cnt;
+        Fs.hi = P.hi;
+        Fs.lo = P.lo;
+        Fs.ext = P.ext;
+        setup_final(Fs, nslots);
+        uint32_t* tail = reinterpret_cast<uint32_t*>(hbuf + o_tail);
+        memset(tail, 0, 32);
+        HIP_TRY(launch_epilogue_small(P, Fs, nc, kagg, res->ts, res->val, res->gid, per_glob_rows ? res->glob : nullptr,
+                                      P.flags, tail, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fast_rows = tail[4];
+        fast_done = true;
+        memcpy(&plan_bytes, tail + 2, 8);
+        return tail[0];
+      }
+    }
     if (ncells) HIP_TRY(launch_fixup_table(P, nc, kagg, st));
     if (P.stamps) {
       std::vector<unsigned long long> h(nstamp);

@@ -796,6 +796,9 @@ int evaluate_exemplar(Engine& E, CallCtx& X, const Request& R, const char* const
       if (a.glob != b.glob) return a.glob < b.glob;
       if (a.null != b.null) return b.null;
       if (a.null) return false;
+      const int ut = union_of(a.glob);
+      if (ut != pq::DOUBLE && ut != pq::FLOAT)   // integers (the all-ones key is -1): exact order, not as doubles
+        return int64_t(a.key) < int64_t(b.key);  // (beyond 2^53 doubles tie and the text order is wrong)
       const double x = num_of(a), y = num_of(b);
       if (x != y && x == x && y == y) return x < y;
       return a.text < b.text;

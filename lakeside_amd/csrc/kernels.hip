@@ -533,6 +533,87 @@ __global__ __launch_bounds__(256) void fill_u64(unsigned long long* p, unsigned 
     p[i] = v;
 }
 
+__global__ __launch_bounds__(256) void fill_many(FillList L) {
+  const unsigned long long stride = (unsigned long long)gridDim.x * 256;
+  for (int k = 0; k < L.count; k++) {
+    unsigned long long* p = L.p[k];
+    const unsigned long long n = L.n[k], v = L.v[k];
+    for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) p[i] = v;
+  }
+}
+
+hipError_t launch_fill_many(const FillList& L, hipStream_t st) {
+  unsigned long long mx = 0;
+  for (int k = 0; k < L.count; k++) mx = std::max(mx, L.n[k]);
+  if (mx == 0) return hipSuccess;
+  const unsigned long long blocks = std::min<unsigned long long>((mx + 255) / 256, 8192);
+  hipLaunchKernelGGL(fill_many, dim3(uint32_t(blocks)), dim3(256), 0, st, L);
+  return hipGetLastError();
+}
+
+// One workgroup: fixup (as fixup_table) -> barrier -> rows in key order (as finalize_count / scan / write, the block
+// walking the keys 1024 at a time with a running offset) -> flags and row count to the host.  The barrier makes the
+// fixup's table writes visible to every wave of the workgroup (HIP __syncthreads semantics for global memory).
+constexpr int EB = 1024;
+__global__ __launch_bounds__(EB) void epilogue_small(QParams P, FParams F, unsigned long long nc, int agg, int64_t* out_ts,
+                                                   double* out_val, uint32_t* out_gid, uint32_t* out_glob,
+                                                   const uint32_t* dflags, uint32_t* host_tail) {
+  __shared__ uint32_t ws[EB / 64];
+  if (P.lean)
+    for (unsigned long long i = threadIdx.x; i < nc; i += EB) {
+      if (P.lean & LEAN_SUM_EXISTS) {
+        const bool e = (unsigned long long)__double_as_longlong(P.hi[i]) != NEG_ZERO_BITS;
+        P.rows[i] = e ? 1ull : 0ull;
+        P.cnt[i] = e ? 1ull : 0ull;
+        if (!e) P.hi[i] = 0.0;
+      } else if (P.lean & LEAN_NO_ROWS) {
+        const unsigned long long ident = agg == AGG_MIN ? ~0ull : 0ull;
+        const unsigned long long e = P.ext[i] != ident ? 1ull : 0ull;
+        P.rows[i] = e;
+        P.cnt[i] = e;
+      } else if (P.lean & LEAN_NO_CNT) {
+        P.cnt[i] = P.rows[i];
+      }
+    }
+  __syncthreads();
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t off = 0;
+  for (unsigned long long base = 0; base < F.nkeys; base += EB) {   // uniform trip count
+    const unsigned long long local = base + threadIdx.x;
+    const unsigned long long key = F.key_base + local;
+    OutRow r{false, 0, 0, 0};
+    if (local < F.nkeys) r = make_row(F, key);
+    const unsigned long long m = __ballot(r.exists);
+    if (lane == 0) ws[wave] = uint32_t(__popcll(m));
+    __syncthreads();
+    uint32_t wb = 0, tot = 0;
+    for (int w = 0; w < EB / 64; w++) {
+      wb += (w < wave) ? ws[w] : 0u;
+      tot += ws[w];
+    }
+    if (r.exists) {
+      const uint32_t pos = off + wb + uint32_t(__popcll(m & ((1ull << lane) - 1ull)));
+      const unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
+      out_ts[pos] = F.bucket_base + (int64_t)b * F.step;
+      out_val[pos] = r.value;
+      out_gid[pos] = uint32_t(r.gid);
+      if (out_glob) out_glob[pos] = r.glob;
+    }
+    off += tot;
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) host_tail[threadIdx.x] = dflags[threadIdx.x];
+  if (threadIdx.x == 0) host_tail[4] = off;
+}
+
+hipError_t launch_epilogue_small(const QParams& P, const FParams& F, unsigned long long nc, int agg, int64_t* ts,
+                                 double* val, uint32_t* gid, uint32_t* glob, const uint32_t* dflags,
+                                 uint32_t* host_tail, hipStream_t st) {
+  if (nc > kEpilogueMax || F.nkeys > kEpilogueMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(epilogue_small, dim3(1), dim3(EB), 0, st, P, F, nc, agg, ts, val, gid, glob, dflags, host_tail);
+  return hipGetLastError();
+}
+
 // Dictionary compaction (Engine::compact_locked): a segment's chunk remap, old engine id -> new id.
 __global__ __launch_bounds__(256) void remap_ids(uint32_t* p, unsigned long long n, const uint32_t* map) {
   for (unsigned long long i = (unsigned long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (unsigned long long)gridDim.x * 256)

@@ -197,6 +197,23 @@ hipError_t launch_remap_ids(uint32_t* p, unsigned long long n, const uint32_t* m
 hipError_t launch_fixup_table(const QParams& P, unsigned long long nc, int agg, hipStream_t stream);
 // p[0 .. n) = v (64-bit pattern fill: LEAN_SUM_EXISTS's -0.0)
 hipError_t launch_fill_u64(unsigned long long* p, unsigned long long n, unsigned long long v, hipStream_t stream);
+// Several 64-bit pattern fills in one launch (a table's planes and the scan flags before a scan).
+struct FillList {
+  static constexpr int kMax = 8;
+  unsigned long long* p[kMax];
+  unsigned long long n[kMax];
+  unsigned long long v[kMax];
+  int count;
+};
+hipError_t launch_fill_many(const FillList& L, hipStream_t stream);
+// Small dense tables (nc, out_keys <= kEpilogueMax): the whole epilogue of a single-GPU scan in one single-workgroup
+// launch -- the lean-table fixup, the output rows compacted in key order straight into the (mapped pinned) result
+// columns, and the scan's flags (flags[0..3]) plus the row count written to host_tail[0..3] / host_tail[4] (mapped
+// pinned host memory), so the host reads everything after one stream synchronization.
+constexpr unsigned long long kEpilogueMax = 1ull << 16;
+hipError_t launch_epilogue_small(const QParams& P, const FParams& F, unsigned long long nc, int agg, int64_t* ts,
+                                 double* val, uint32_t* gid, uint32_t* glob, const uint32_t* dflags,
+                                 uint32_t* host_tail, hipStream_t stream);
 // one aggregate's scan instantiations (scan_<agg>.hip)
 template <int AGG>
 void launch_scan_agg(const QParams& P, dim3 grid, hipStream_t st);

@@ -1,6 +1,7 @@
 """GPU parity of the §8(f) widenings (metrics specifics, other worker query shapes) against the oracle, through
 the C ABI on the MI355X."""
 import json
+import os
 
 import numpy as np
 import pytest
@@ -268,6 +269,18 @@ def test_hbm_budget_lru_eviction():
         assert e.segment_count == 2
         e.put_segment("s0", blobs[0])
         assert e.eval_pushdown(req, ["s0"], 10, LK_MERGED).rows() == want
+        # a put key that is also a readable file path is reloaded from the file once evicted (a cache miss
+        # like any other), not LK_ERR_EVICTED
+        import tempfile
+        with tempfile.TemporaryDirectory() as td:
+            path = os.path.join(td, "seg0.parquet")
+            with open(path, "wb") as f:
+                f.write(blobs[0])
+            e.put_segment(path, blobs[0])
+            e.put_segment("s2", blobs[2])
+            e.put_segment("s3", blobs[3])                          # the path key is evicted (LRU)
+            assert e.segment_count == 2
+            assert e.eval_pushdown(req, [path], 10, LK_MERGED).rows() == want
     finally:
         e.close()
 
