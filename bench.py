@@ -290,26 +290,29 @@ def main():
     torch.cuda.synchronize()
     scan_ms, total_ms, plan_ms, device_ms, alg_bytes, out_rows = [], [], [], [], 0, 0
     launch_ms, sync_ms, alloc_ms, copy_ms, dims_ms, reduce_ms, agreed_ms = [], [], [], [], [], [], []
+    texts = []   # each step's stats, parsed after the timed region
     t_start = time.perf_counter()
     for _ in range(args.steps):
         res = step()
-        scan_ms.append(res.stats["scan_ms"])
-        total_ms.append(res.stats["total_ms"])
-        plan_ms.append(res.stats.get("plan_ms", 0.0))
-        device_ms.append(res.stats.get("device_ms", 0.0))
-        launch_ms.append(res.stats.get("launch_ms", 0.0))
-        sync_ms.append(res.stats.get("sync_ms", 0.0))
-        alloc_ms.append(res.stats.get("alloc_ms", 0.0))
-        copy_ms.append(res.stats.get("copy_ms", 0.0))
-        dims_ms.append(res.stats.get("dims_ms", 0.0))
-        reduce_ms.append(res.stats.get("reduce_ms", 0.0))
-        agreed_ms.append(res.stats.get("scan_agreed_ms", 0.0))
-        alg_bytes = res.stats.get("algorithmic_bytes", 0)
-        out_rows = len(res)
+        texts.append(res.stats_text())
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    for st in map(json.loads, texts):
+        scan_ms.append(st["scan_ms"])
+        total_ms.append(st["total_ms"])
+        plan_ms.append(st.get("plan_ms", 0.0))
+        device_ms.append(st.get("device_ms", 0.0))
+        launch_ms.append(st.get("launch_ms", 0.0))
+        sync_ms.append(st.get("sync_ms", 0.0))
+        alloc_ms.append(st.get("alloc_ms", 0.0))
+        copy_ms.append(st.get("copy_ms", 0.0))
+        dims_ms.append(st.get("dims_ms", 0.0))
+        reduce_ms.append(st.get("reduce_ms", 0.0))
+        agreed_ms.append(st.get("scan_agreed_ms", 0.0))
+        alg_bytes = st.get("algorithmic_bytes", 0)
+    out_rows = len(res)
     avg = lambda xs: sum(xs) / len(xs)   # noqa: E731
     per_rank = {"rank": rank, "device": device, "segments": S, "scan_kernel_ms": avg(scan_ms),
                 "eval_ms": elapsed * 1e3 / args.steps, "dims_ms": avg(dims_ms), "reduce_ms": avg(reduce_ms),

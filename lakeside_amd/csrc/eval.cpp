@@ -1374,7 +1374,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     bool late_leaves = false;
     for (size_t s = 0; s < strs.size(); s++)
       if (((late_mask >> dev_of[s]) & 1u) && !strs[s].leaves.empty()) late_leaves = true;
-    P.late_chunk = (late_leaves && ngroups <= 65536u && getenv("LK_LATE_CHUNK")) ? 1u : 0u;
+    // tag queries: COUNT(*) counted in the chunk loop from the late window (A/B: LK_TAG_DIRECT=1)
+    const bool tag_direct = tagq && getenv("LK_TAG_DIRECT") && *getenv("LK_TAG_DIRECT") == '1';
+    P.late_chunk = ((late_leaves || tag_direct) && ngroups <= 65536u && (getenv("LK_LATE_CHUNK") || tag_direct)) ? 1u : 0u;
     // speculative value gather for late-filtered rows (lean_kernel.hpp rowsN): opt-in
     // (LK_SPEC_GATHER=1) -- measured slower on C3, 2.155 vs 1.968 ms: the loads of the rows the late filter drops
     // (half of C3's listed rows) cost more than the round trip they save (profiles/r05_bench_c3*.json)

