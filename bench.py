@@ -227,7 +227,7 @@ def main():
                                                         highcard_n=highcard))
 
     # The CPU baseline / validator reads the same Parquet bytes: every rank keeps its shard in host memory.
-    keep_cpu = args.cpu_sample != 0 and not q.get("exemplar")
+    keep_cpu = args.cpu_sample != 0
     kept = {}
     t0 = time.time()
     bytes_loaded = 0
@@ -482,9 +482,13 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
     tag = q.get("tag")
     concurrent = world == 1 or args.comm == "rccl"
 
-    def evaluate(timing=None):   # tag queries: {tag text -> COUNT(*)}; aggregates: per-glob cells
+    exemplar = q.get("exemplar")
+
+    def evaluate(timing=None):   # tag queries: {tag text -> COUNT(*)}; exemplars: the worker stream; else cells
         if tag:
             return lkcpu.evaluate_tag_counts(pr, tag, 10, blobs, threads, timing=timing)
+        if exemplar:
+            return lkcpu.evaluate_exemplar_rows(pr, 10, blobs, threads, timing=timing)
         return lkcpu.evaluate_cell_table(pr, 10, blobs, threads, timing=timing)
 
     def run():
@@ -510,7 +514,7 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
         times = [None] * world
         dist.all_gather_object(times, (dt, full))
         parts = [None] * world if rank == 0 else None
-        dist.gather_object((table if tag else table.to_dict()) if full else None, parts, dst=0)
+        dist.gather_object((table if tag or exemplar else table.to_dict()) if full else None, parts, dst=0)
         if rank != 0:
             return None, None
         full = all(f for _, f in times)
@@ -520,6 +524,10 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
             for p in parts:
                 for k, c in p.items():
                     table[k] = table.get(k, 0) + c
+        elif full and exemplar:   # query-api: the pods' streams merged (rank order) and take(limit)
+            from oracle import exemplar as ex
+            table = ex.merge_sorted_fold([[(t, v, k) for t, v, k, _ in p] for p in parts],
+                                         pr.reverseSort)[:pr.baseExpr.limit]
         elif full:
             table = lkcpu.CellTable.concat([lkcpu.CellTable(**p) for p in parts])
     else:
@@ -527,9 +535,17 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
     validated = None
     if full:
         has_gb = bool(q["group_bys"])
-        want = lkcpu.merge_cell_table(table, agg, has_gb) if not tag else (list(table),)
+        want = (list(table),) if tag or exemplar else lkcpu.merge_cell_table(table, agg, has_gb)
         try:
-            if tag:   # the merged tag table: one row per tag text (NULL-like values together), value = COUNT(*)
+            if exemplar:   # rows in stream order: timestamps, values (read, bit-exact), tag maps, glob (N = 1)
+                got = list(zip(gpu_res.ts.tolist(), gpu_res.values.tolist(), gpu_res.tags, gpu_res.globs.tolist()))
+                assert len(got) == len(table), f"{len(got)} rows vs {len(table)}"
+                for i, (g, w) in enumerate(zip(got, table)):
+                    assert g[0] == w[0] and g[1] == w[1], f"row {i}: (ts, value) {g[:2]} vs {w[:2]}"
+                    assert g[2] == lkcpu.tags_of_key(w[2]), f"row {i}: tags {g[2]} vs {lkcpu.tags_of_key(w[2])}"
+                    if world == 1:
+                        assert g[3] == w[3], f"row {i}: glob {g[3]} vs {w[3]}"
+            elif tag:   # the merged tag table: one row per tag text (NULL-like values together), value = COUNT(*)
                 got = {}
                 for v, t in zip(gpu_res.values.tolist(), gpu_res.tags):
                     k = t.get(tag)

@@ -175,6 +175,79 @@ def evaluate_tag_counts(pr: dx.PushDownRequest, tag: str, glob_size: int, blobs:
         L.lkcpu_free(h)
 
 
+def plan_text_exemplar(pr: dx.PushDownRequest, glob_size: int) -> str:
+    """An exemplar request (no chart, BaseExpr.scala:206-239) in lkcpu's line format: the filter's string columns,
+    no group keys."""
+    be = pr.baseExpr
+    leaves = _leaves(be.filter, []) if be.filter is not None else []
+    strcols = [dx.NAME]
+    for l in leaves:
+        if l.op in dx.NUMERIC_OPS:
+            raise NotImplementedError("lkcpu exemplar: numeric leaves")
+        if l.k not in strcols:
+            strcols.append(l.k)
+    t = [be.dataset, "sum", dx.VALUE, str(glob_size), str(len(pr.segmentRequests))]
+    for s in pr.segmentRequests:
+        t += [str(s.startTs), str(s.endTs), str(s.stepInMillis)]
+    t += [str(len(strcols))] + strcols + ["0"]
+    t += [str(len(leaves))]
+    for l in leaves:
+        t += [str(strcols.index(l.k)), l.op, str(len(l.v))] + list(l.v)
+    prog = _postfix(be.filter, leaves, []) if leaves else []
+    t += [str(len(prog))] + [str(x) for x in prog]
+    fs = sorted(dx.field_set(be))
+    t += [str(len(fs))] + fs
+    return "\n".join(quote(x, safe="") for x in t) + "\n"
+
+
+def evaluate_exemplar_rows(pr: dx.PushDownRequest, glob_size: int, blobs: Sequence, threads: int = 0,
+                           timing: Optional[list] = None):
+    """The worker's exemplar stream (per glob ORDER BY ts LIMIT n, globs folded by mergeSorted) from the C++
+    restatement: [(ts, value, canonical tag key, glob)] in stream order."""
+    text = plan_text_exemplar(pr, glob_size)
+    n = len(blobs)
+    ptrs = (ctypes.c_void_p * max(1, n))()
+    sizes = (ctypes.c_size_t * max(1, n))()
+    keep = []
+    for i, b in enumerate(blobs):
+        if isinstance(b, (bytes, bytearray)):
+            buf = ctypes.create_string_buffer(bytes(b), len(b))
+            keep.append(buf)
+            ptrs[i], sizes[i] = ctypes.cast(buf, ctypes.c_void_p), len(b)
+        else:
+            ptrs[i], sizes[i] = ctypes.cast(b[0], ctypes.c_void_p), b[1]
+    L = lib()
+    if not getattr(L, "_ex_bound", False):
+        L.lkcpu_exemplar.restype = ctypes.c_void_p
+        L.lkcpu_exemplar.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                     ctypes.c_size_t, ctypes.c_int, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+        L.lkcpu_ex_rows.restype = ctypes.c_size_t
+        L.lkcpu_ex_rows.argtypes = [ctypes.c_void_p]
+        L.lkcpu_ex_row.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64),
+                                   ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int32)]
+        L.lkcpu_ex_tags.restype = ctypes.c_char_p
+        L.lkcpu_ex_tags.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        L.lkcpu_ex_free.argtypes = [ctypes.c_void_p]
+        L._ex_bound = True
+    be = pr.baseExpr
+    t0 = time.perf_counter()
+    h = L.lkcpu_exemplar(text.encode(), ptrs, sizes, n, threads, int(be.limit), 1 if be.order.upper() == "DESC" else 0,
+                         1 if pr.reverseSort else 0)
+    if timing is not None:
+        timing.append(time.perf_counter() - t0)
+    if not h:
+        raise RuntimeError(L.lkcpu_error().decode())
+    try:
+        out = []
+        ts, val, g = ctypes.c_int64(), ctypes.c_double(), ctypes.c_int32()
+        for i in range(L.lkcpu_ex_rows(h)):
+            L.lkcpu_ex_row(h, i, ctypes.byref(ts), ctypes.byref(val), ctypes.byref(g))
+            out.append((ts.value, val.value, L.lkcpu_ex_tags(h, i), g.value))
+        return out
+    finally:
+        L.lkcpu_ex_free(h)
+
+
 def _dd(*xs):
     """Correctly rounded sum of double-double parts (IEEE propagation for non-finite values)."""
     return math.fsum(xs) if all(math.isfinite(x) for x in xs) else float(np.sum(np.array(xs)))

@@ -542,6 +542,16 @@ void lkcpu_cells(void* r, int32_t* glob, int64_t* ts, uint64_t* rows, uint64_t* 
                  double* mn, double* mx, uint8_t* nanf, int32_t* keys);
 const char* lkcpu_key_string(void* r, int col, int32_t id);
 void lkcpu_free(void* r);
+// Exemplar rows (no chart): per glob ORDER BY timestamp <desc|asc> LIMIT limit (ties in file order), tags = every
+// column's text, globs folded by Akka mergeSorted (reverse: timestamp descending).  Numbers print as JDBC getString:
+// INT64 in decimal, DOUBLE only when integral and below 1e7 ("N.0", Java Double.toString) -- anything else is refused
+// (the restatement does not carry a Java double formatter; the bench's synthetic values are integers).
+void* lkcpu_exemplar(const char* plan_text, const uint8_t* const* seg_ptrs, const size_t* seg_sizes, size_t n_segs,
+                     int threads, int64_t limit, int desc, int reverse);
+size_t lkcpu_ex_rows(void* r);
+void lkcpu_ex_row(void* r, size_t i, int64_t* ts, double* val, int32_t* glob);
+const char* lkcpu_ex_tags(void* r, size_t i);   // canonical tag key: items sorted by name, "k\x1ev" joined by "\x1f"
+void lkcpu_ex_free(void* r);
 
 }  // extern "C"
 
@@ -850,9 +860,252 @@ Result* evaluate(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes,
   return R;
 }
 
+struct ExResult {
+  std::vector<int64_t> ts;
+  std::vector<double> val;
+  std::vector<int32_t> glob;
+  std::vector<std::string> key;
+};
+
+// Java Double.toString of an integral double below 1e7 in magnitude ("123.0", "-0.0"); refuses the rest.
+std::string java_integral_text(double v) {
+  if (!(std::fabs(v) < 1e7) || v != std::trunc(v)) throw Err("lkcpu exemplar: non-integral double text is not restated");
+  if (v == 0.0) return std::signbit(v) ? "-0.0" : "0.0";
+  return std::to_string((long long)v) + ".0";
+}
+
+ExResult* exemplar(const Plan& P, const uint8_t* const* ptrs, const size_t* sizes, size_t nseg, int threads,
+                   int64_t limit, bool desc, bool reverse) {
+  std::unique_ptr<ExResult> R(new ExResult());
+  std::vector<Segment> segs(nseg);
+  for (size_t s = 0; s < nseg; s++) {
+    segs[s].data = ptrs[s];
+    segs[s].size = sizes[s];
+    segs[s].fm = read_footer(ptrs[s], sizes[s]);
+    for (size_t k = 1; k < segs[s].fm.schema.size(); k++) segs[s].col[segs[s].fm.schema[k].name] = int(k - 1);
+  }
+  const std::vector<std::string> proj = P.metrics ? std::vector<std::string>{}
+                                                  : std::vector<std::string>{"_cardinalhq.timestamp", "_cardinalhq.value",
+                                                                             "_cardinalhq.name", "_cardinalhq.message"};
+  if (P.metrics) throw Err("lkcpu exemplar: logs only");
+  const size_t G = size_t(P.glob_size), nglobs = (nseg + G - 1) / G;
+  const int nstr = int(P.strcols.size());
+  std::vector<uint32_t> leaf_false(nglobs, 0);
+  std::vector<char> skip(nglobs, 0);
+  std::vector<int64_t> wlo(nglobs), whi(nglobs);
+  for (size_t g = 0; g < nglobs; g++) {
+    std::map<std::string, int> uni;
+    wlo[g] = INT64_MAX;
+    whi[g] = INT64_MIN;
+    for (size_t s = g * G; s < std::min(nseg, (g + 1) * G); s++) {
+      for (auto& kv : segs[s].col) uni[kv.first] = 1;
+      wlo[g] = std::min(wlo[g], P.start[s]);
+      whi[g] = std::max(whi[g], P.end[s]);
+    }
+    std::map<std::string, int> nonexist;
+    for (auto& f : P.fieldset)
+      if (!uni.count(f)) nonexist[f] = 1;
+    for (size_t l = 0; l < P.leaves.size(); l++) {
+      const std::string& c = P.strcols[size_t(P.leaves[l].col)];
+      if (nonexist.count(c)) leaf_false[g] |= 1u << l;
+      else if (!uni.count(c)) skip[g] = 1;   // Binder Error: the glob's query fails (empty)
+    }
+    for (auto& c : proj)
+      if (!uni.count(c)) skip[g] = 1;
+  }
+  for (auto& l : P.leaves)
+    if (l.col < 0) throw Err("lkcpu exemplar: numeric leaves are not restated");
+  // candidates per (segment, row group): (ts, segment position in glob, row in file)
+  struct Cand {
+    int64_t ts;
+    uint32_t seg;
+    int64_t row;   // row in the file
+  };
+  std::vector<std::pair<int, int>> tasks;
+  for (size_t s = 0; s < nseg; s++)
+    if (!skip[s / G])
+      for (size_t r = 0; r < segs[s].fm.rgs.size(); r++) tasks.emplace_back(int(s), int(r));
+#ifdef _OPENMP
+  if (threads > 0) omp_set_num_threads(threads);
+#endif
+  std::vector<std::vector<Cand>> part(tasks.size());
+  std::atomic<int> failed{0};
+  std::mutex err_mu;
+  std::string err;
+  auto before = [&](const Cand& a, const Cand& b) {   // ORDER BY ts <dir>, then file order (segment, row)
+    if (a.ts != b.ts) return desc ? a.ts > b.ts : a.ts < b.ts;
+    if (a.seg != b.seg) return a.seg < b.seg;
+    return a.row < b.row;
+  };
+#pragma omp parallel for schedule(dynamic, 1)
+  for (size_t ti = 0; ti < tasks.size(); ti++) {
+    if (failed.load()) continue;
+    try {
+      const Segment& S = segs[size_t(tasks[ti].first)];
+      const int rg = tasks[ti].second;
+      const RowGroupMeta& RG = S.fm.rgs[size_t(rg)];
+      const size_t g = size_t(tasks[ti].first) / G;
+      int64_t row0 = 0;
+      for (int k = 0; k < rg; k++) row0 += S.fm.rgs[size_t(k)].num_rows;
+      auto load = [&](const std::string& name, bool is_string, Chunk& c) -> bool {
+        auto it = S.col.find(name);
+        if (it == S.col.end()) return false;
+        const SchemaElem& se = S.fm.schema[size_t(it->second) + 1];
+        decode_chunk(S.data, S.size, RG.cols[size_t(it->second)], se.rep == 1, RG.num_rows, is_string, c);
+        return true;
+      };
+      Chunk tsc;
+      if (!load("_cardinalhq.timestamp", false, tsc)) continue;
+      std::vector<Chunk> sc(static_cast<size_t>(nstr));
+      std::vector<char> has(static_cast<size_t>(nstr), 0);
+      std::vector<std::vector<uint32_t>> tbits(static_cast<size_t>(nstr));
+      std::vector<uint32_t> colmask(static_cast<size_t>(nstr), 0);
+      for (size_t l = 0; l < P.leaves.size(); l++) colmask[size_t(P.leaves[l].col)] |= 1u << l;
+      for (int c = 0; c < nstr; c++) {
+        if (!colmask[size_t(c)]) continue;
+        has[size_t(c)] = load(P.strcols[size_t(c)], true, sc[size_t(c)]);
+        tbits[size_t(c)].assign(sc[size_t(c)].dict.size(), 0);
+        for (size_t d = 0; d < sc[size_t(c)].dict.size(); d++)
+          for (size_t l = 0; l < P.leaves.size(); l++)
+            if (P.leaves[l].col == c && leaf_hit(P.leaves[l], sc[size_t(c)].dict[d])) tbits[size_t(c)][d] |= 1u << l;
+      }
+      std::vector<Cand>& out = part[ti];
+      for (int64_t r = 0; r < RG.num_rows; r++) {
+        if (!tsc.valid[size_t(r)]) continue;
+        const int64_t t = tsc.i64[size_t(r)];
+        if (t < wlo[g] || t >= whi[g]) continue;
+        uint32_t T = 0, F = 0;
+        for (int c = 0; c < nstr; c++) {
+          const uint32_t m = colmask[size_t(c)];
+          if (!m) continue;
+          const int32_t code = has[size_t(c)] ? sc[size_t(c)].codes[size_t(r)] : -1;
+          if (code < 0) {
+            for (size_t l = 0; l < P.leaves.size(); l++)
+              if (((m >> l) & 1u) && (P.leaves[l].op == "has" || P.leaves[l].op == "exists")) F |= 1u << l;
+            continue;
+          }
+          const uint32_t b = tbits[size_t(c)][size_t(code)];
+          T |= b & m;
+          F |= ~b & m;
+        }
+        T &= ~leaf_false[g];
+        F |= leaf_false[g];
+        if (!kleene(P.prog, T, F)) continue;
+        out.push_back(Cand{t, uint32_t(tasks[ti].first), row0 + r});
+      }
+      if (limit >= 0 && out.size() > size_t(limit)) {   // a task keeps at most its own top `limit`
+        std::nth_element(out.begin(), out.begin() + limit, out.end(), before);
+        out.resize(size_t(limit));
+      }
+    } catch (const std::exception& e) {
+      failed = 1;
+      std::lock_guard<std::mutex> lg(err_mu);
+      err = e.what();
+    }
+  }
+  if (failed) throw Err(err);
+  // per glob: its top `limit` in ORDER BY order
+  std::vector<std::vector<Cand>> per(nglobs);
+  for (size_t ti = 0; ti < tasks.size(); ti++) {
+    auto& v = per[size_t(tasks[ti].first) / G];
+    v.insert(v.end(), part[ti].begin(), part[ti].end());
+  }
+  for (auto& v : per) {
+    std::sort(v.begin(), v.end(), before);
+    if (limit >= 0 && v.size() > size_t(limit)) v.resize(size_t(limit));
+  }
+  // Akka mergeSorted fold over the globs: the left head when strictly less
+  struct Sel {
+    Cand c;
+    int32_t glob;
+  };
+  std::vector<Sel> stream;
+  for (size_t g = 0; g < nglobs; g++) {
+    std::vector<Sel> m;
+    size_t i = 0, j = 0;
+    while (i < stream.size() && j < per[g].size()) {
+      const bool lt = reverse ? stream[i].c.ts > per[g][j].ts : stream[i].c.ts < per[g][j].ts;
+      if (lt) m.push_back(stream[i++]);
+      else m.push_back(Sel{per[g][j++], int32_t(g)});
+    }
+    while (i < stream.size()) m.push_back(stream[i++]);
+    while (j < per[g].size()) m.push_back(Sel{per[g][j++], int32_t(g)});
+    stream.swap(m);
+  }
+  // every column of the selected rows, decoded per (segment, row group) once
+  std::map<std::pair<uint32_t, int>, std::map<std::string, Chunk>> cache;
+  for (const Sel& x : stream) {
+    const Segment& S = segs[x.c.seg];
+    int rg = 0;
+    int64_t r = x.c.row;
+    while (rg < int(S.fm.rgs.size()) && r >= S.fm.rgs[size_t(rg)].num_rows) r -= S.fm.rgs[size_t(rg++)].num_rows;
+    auto& cols = cache[std::make_pair(x.c.seg, rg)];
+    if (cols.empty())
+      for (auto& kv : S.col) {
+        const SchemaElem& se = S.fm.schema[size_t(kv.second) + 1];
+        Chunk& c = cols[kv.first];
+        if (se.type != 6 && se.type != 2 && se.type != 5) throw Err("lkcpu exemplar: column type not restated: " + kv.first);
+        decode_chunk(S.data, S.size, S.fm.rgs[size_t(rg)].cols[size_t(kv.second)], se.rep == 1,
+                     S.fm.rgs[size_t(rg)].num_rows, se.type == 6, c);
+      }
+    std::map<std::string, std::string> tags;
+    double value = 0.0;
+    for (auto& kv : cols) {
+      const SchemaElem& se = S.fm.schema[size_t(S.col.at(kv.first)) + 1];
+      const Chunk& c = kv.second;
+      if (se.type == 6) {
+        const int32_t code = c.codes[size_t(r)];
+        if (code < 0) continue;
+        const std::string& v = c.dict[size_t(code)];
+        if (!v.empty() && v != "null") tags[kv.first] = v;   // Commons.scala:433
+      } else if (c.valid[size_t(r)]) {
+        if (se.type == 2) {
+          tags[kv.first] = std::to_string((long long)c.i64[size_t(r)]);
+        } else {
+          const double d = c.f64[size_t(r)];
+          if (kv.first == "_cardinalhq.value") value = d;
+          tags[kv.first] = java_integral_text(d);
+        }
+      }
+    }
+    std::string key;
+    for (auto& kv : tags) {
+      if (!key.empty()) key += '\x1f';
+      key += kv.first;
+      key += '\x1e';
+      key += kv.second;
+    }
+    R->ts.push_back(x.c.ts);
+    R->val.push_back(value);
+    R->glob.push_back(x.glob);
+    R->key.push_back(std::move(key));
+  }
+  return R.release();
+}
+
 }  // namespace
 
 extern "C" {
+
+void* lkcpu_exemplar(const char* plan_text, const uint8_t* const* seg_ptrs, const size_t* seg_sizes, size_t n_segs,
+                     int threads, int64_t limit, int desc, int reverse) {
+  try {
+    Plan P = parse_plan(plan_text);
+    return exemplar(P, seg_ptrs, seg_sizes, n_segs, threads, limit, desc != 0, reverse != 0);
+  } catch (const std::exception& e) {
+    t_err = e.what();
+    return nullptr;
+  }
+}
+size_t lkcpu_ex_rows(void* r) { return static_cast<ExResult*>(r)->ts.size(); }
+void lkcpu_ex_row(void* r, size_t i, int64_t* ts, double* val, int32_t* glob) {
+  const ExResult& R = *static_cast<ExResult*>(r);
+  *ts = R.ts[i];
+  *val = R.val[i];
+  *glob = R.glob[i];
+}
+const char* lkcpu_ex_tags(void* r, size_t i) { return static_cast<ExResult*>(r)->key[i].c_str(); }
+void lkcpu_ex_free(void* r) { delete static_cast<ExResult*>(r); }
 
 void* lkcpu_eval(const char* plan_text, const uint8_t* const* seg_ptrs, const size_t* seg_sizes, size_t n_segs,
                  int threads) {

@@ -231,8 +231,12 @@ def _worker8(rank, world, port, q):
             req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), segs, "sum", gbs))
             first = eng.eval_pushdown_dist(req, keys, shard, 10)
             res = eng.eval_pushdown_dist(req, keys, shard, 10)   # the agreed dim space is reused
+            # the reused union's agreement (one small all-gather), measured over repeated calls
+            agree = []
+            for _ in range(9 if name == "c5_1h" else 0):
+                agree.append(eng.eval_pushdown_dist(req, keys, shard, 10).stats["dims_ms"])
             if rank == 0:
-                results[name] = (req, res.rows(), res.stats, first.stats)
+                results[name] = (req, res.rows(), dict(res.stats, agree_ms=[res.stats["dims_ms"]] + agree), first.stats)
                 assert first.rows() == res.rows()
             else:
                 assert len(res) == 0
@@ -281,11 +285,14 @@ def test_dist_world8_host_transport_c4_c5_shapes():
             # (dims.cpp), the second reuses it with one small all-gather
             # (c5_1m_hash: the same container dictionaries as c5_1h, so even its first call reuses that union)
             assert first["dims_rebuilt"] == (1 if name == "c5_1h" else 0) and stats["dims_rebuilt"] == 0, (first, stats)
-            # (the reused union costs one small all-gather: host-transport latency of 8 processes sharing one box,
-            # typically 1-5 ms, seen at 13.5 ms under load -- bounded loosely; the rebuild it avoids takes seconds)
-            assert stats["dims_ms"] < 50.0, stats
-            print(f"{name}: dims agreement first {first['dims_ms']:.1f} ms, cached {stats['dims_ms']:.3f} ms; "
-                  f"eval {stats['total_ms']:.1f} ms", flush=True)
+            # the reused union costs one small all-gather: over the host transport that is a gloo all-gather among 8
+            # processes sharing one box (r05: median and maximum printed below); bounded by its median (a single
+            # call can stall on the shared box's scheduler: the r04 run saw one at 13.5 ms)
+            ag = sorted(stats.get("agree_ms", [stats["dims_ms"]]))
+            med = ag[len(ag) // 2]
+            assert med < 10.0, ag
+            print(f"{name}: dims agreement first {first['dims_ms']:.1f} ms, reused median {med:.3f} ms "
+                  f"(max {ag[-1]:.3f} of {len(ag)} calls); eval {stats['total_ms']:.1f} ms", flush=True)
 
 
 def _worker_err(rank, world, port):

@@ -179,3 +179,32 @@ def test_cpu_tag_counts_golden(case):
     rows = [dx.tag_row_tags(tag, v, c) for v, c in got.items()]
     key = lambda t: sorted(t.items())   # noqa: E731
     assert sorted(rows, key=key) == sorted(case["expected_merged"], key=key)
+
+
+@pytest.mark.parametrize("limit,order,reverse,glob_size", [(50, "DESC", False, 2), (7, "ASC", True, 3),
+                                                             (100000, "DESC", False, 4)])
+def test_cpu_exemplar_matches_oracle(limit, order, reverse, glob_size):
+    """The C++ restatement's exemplar mode (the bench's full-size exemplar validator) == oracle/exemplar.py on
+    synthetic segments (integer values: the text the restatement prints), rows in stream order."""
+    import json as _json
+
+    from lakeside_amd import synth
+    from oracle import cpu, dataexpr as dx
+    from oracle import exemplar as ex
+    blobs = []
+    for i in range(5):
+        s = synth.make_segment(synth.segment_spec(i, rows=1 << 15, rg_rows=1 << 13, page_rows=1 << 11))
+        blobs.append(s.bytes())
+        s.free()
+    segs = [synth.segment_request(i) for i in range(5)]
+    filt = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_07"),
+            "q2": {"not": synth.leaf(synth.SERVICE, "regex", "^svc-0[0-4]")}}
+    req = _json.dumps({"baseExpr": {"id": "A", "dataset": "logs", "filter": filt, "limit": limit, "order": order},
+                       "segmentRequests": segs, "reverseSort": reverse})
+    pr = dx.parse_pushdown(req)
+    want = ex.evaluate_exemplar(pr, [f"s{i}" for i in range(5)], glob_size, sources=blobs)
+    got = cpu.evaluate_exemplar_rows(pr, glob_size, blobs, threads=4)
+    assert len(got) == len(want) and len(got) > 0
+    for i, (g, w) in enumerate(zip(got, want)):
+        assert (g[0], g[1], g[3]) == (w[0], w[1], w[3]), i
+        assert cpu.tags_of_key(g[2]) == w[2], i
