@@ -727,6 +727,7 @@ CallCtx::CallCtx(int dev) : device(dev) {
   HIP_CHECK(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
   HIP_CHECK(hipEventCreate(&ev_scan0));
   HIP_CHECK(hipEventCreate(&ev_scan1));
+  HIP_CHECK(hipEventCreateWithFlags(&ev_rows, hipEventDisableTiming));
   HIP_CHECK(hipHostMalloc(&pinned, pinned_cap = 1 << 20));
 }
 
@@ -739,6 +740,7 @@ CallCtx::~CallCtx() {
   if (comm_pin) (void)hipHostFree(comm_pin);
   if (ev_scan0) (void)hipEventDestroy(ev_scan0);
   if (ev_scan1) (void)hipEventDestroy(ev_scan1);
+  if (ev_rows) (void)hipEventDestroy(ev_rows);
   if (stream) (void)hipStreamDestroy(stream);
 }
 

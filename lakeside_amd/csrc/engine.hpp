@@ -49,6 +49,7 @@ struct CallCtx {
   int device = 0;
   hipStream_t stream = nullptr;
   hipEvent_t ev_scan0 = nullptr, ev_scan1 = nullptr;
+  hipEvent_t ev_rows = nullptr;   // large results: bucket_pos written (host expands timestamps meanwhile)
   std::map<std::string, Workspace> ws;
   void* pinned = nullptr;
   size_t pinned_cap = 0;

@@ -234,6 +234,31 @@ struct MetricsUnaligned {};
 // Merged MIN with an all-NaN partial cell: the scan is re-run with per-glob cells (see below).
 struct MinNanApart {};
 enum Redo : unsigned { REDO_METRICS_RAW = 1u, REDO_MIN_APART = 2u };
+
+// Large dense results cross the host link without their timestamp column: finalize_write records the first row of
+// every bucket (FParams::bucket_pos) and the timestamps are expanded here, rows being in bucket-major order.
+constexpr unsigned long long kTsRunsMinKeys = 1ull << 18;   // output key spaces this large (C5: 10M keys)
+constexpr uint64_t kTsRunsMaxBuckets = 1u << 16;            // bucket_pos entries (mapped pinned memory)
+
+void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F) {
+  if (!nrows) return;
+  const uint32_t* bp = F.bucket_pos;
+  const uint64_t nb = F.nbuckets;
+  const size_t piece = size_t(1) << 19;
+  const size_t npieces = (nrows + piece - 1) / piece;
+  parallel_for(npieces, int(std::min<size_t>(npieces, 8)), [&](size_t p) {
+    const size_t lo = p * piece, hi = std::min(nrows, lo + piece);
+    // the bucket of row lo: the last bucket starting at or before it
+    uint64_t b = uint64_t(std::upper_bound(bp, bp + nb, uint32_t(lo)) - bp);
+    b = b ? b - 1 : 0;
+    for (size_t r = lo; r < hi;) {
+      const size_t end = std::min<size_t>(hi, b + 1 < nb ? bp[b + 1] : nrows);
+      const int64_t t = F.bucket_base + int64_t(b) * F.step;
+      for (; r < end; r++) ts[r] = t;
+      b++;
+    }
+  });
+}
 }  // namespace
 
 static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
@@ -1300,12 +1325,15 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   const size_t o_maps = reserve(flat.size() * 4);
   const size_t stage_bytes = off;
   const size_t o_tail = reserve(64);   // host side only: the small-table epilogue's flags and row count (mapped)
+  // host side only (mapped): the first row of every bucket, when a large result's timestamps are expanded on the host
+  const bool ts_runs_ok = nbuckets <= kTsRunsMaxBuckets && !getenv("LK_NO_TS_RUNS");
+  const size_t o_bpos = reserve(ts_runs_ok ? (size_t(nbuckets) + 1) * 4 : 0);
   // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)
   uint8_t* hbuf = nullptr;
   uint8_t* dbuf = nullptr;
   try {
     HIP_TRY(hipSetDevice(E.device));
-    hbuf = static_cast<uint8_t*>(X->pinned_buf(o_tail + 64));
+    hbuf = static_cast<uint8_t*>(X->pinned_buf(off + 64));
     dbuf = static_cast<uint8_t*>(X->workspace("query", stage_bytes));
   } catch (const PlanError& e) {
     if (!dist) throw;
@@ -1592,10 +1620,24 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         setup_final(Fs, nslots);
         const uint32_t nb = finalize_blocks(Fs.nkeys);
         uint32_t* cnts = static_cast<uint32_t*>(X->workspace("counts", (size_t(nb) + 2) * 4));
+        if (ts_runs_ok && out_keys >= kTsRunsMinKeys) Fs.bucket_pos = reinterpret_cast<uint32_t*>(hbuf + o_bpos);
         HIP_TRY(launch_finalize_count(Fs, cnts, st));
-        HIP_TRY(launch_finalize_write(Fs, cnts, res->ts, res->val, res->gid, per_glob_rows ? res->glob : nullptr, st));
+        if (Fs.bucket_pos) {
+          HIP_TRY(launch_finalize_bucket_pos(Fs, cnts, st));
+          HIP_TRY(hipEventRecord(X->ev_rows, st));
+        }
+        HIP_TRY(launch_finalize_write(Fs, cnts, Fs.bucket_pos ? nullptr : res->ts, res->val, res->gid,
+                                      per_glob_rows ? res->glob : nullptr, st));
         HIP_TRY(hipMemcpyAsync(&fast_rows, cnts + nb, 4, hipMemcpyDeviceToHost, st));
         fast_done = true;
+        if (Fs.bucket_pos) {   // timestamps expanded here while finalize_write's rows cross the host link
+          HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
+          HIP_TRY(hipEventSynchronize(X->ev_rows));
+          expand_ts_runs(res->ts, Fs.bucket_pos[nbuckets], Fs);
+          HIP_TRY(hipStreamSynchronize(st));
+          memcpy(&plan_bytes, fl + 2, 8);
+          return fl[0];
+        }
       }
     }
     HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
@@ -2108,13 +2150,23 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     double* o_val = direct ? res->val : reinterpret_cast<double*>(ob + nk * 8);
     uint32_t* o_gid = direct ? res->gid : reinterpret_cast<uint32_t*>(ob + nk * 16);
     uint32_t* o_glob = per_glob_rows ? (direct ? res->glob : reinterpret_cast<uint32_t*>(ob + nk * 24)) : nullptr;
+    const bool ts_runs = direct && !hash_mode && ts_runs_ok && F.nkeys >= kTsRunsMinKeys;
+    if (ts_runs) {
+      F.bucket_pos = reinterpret_cast<uint32_t*>(hbuf + o_bpos);
+      HIP_TRY(launch_finalize_bucket_pos(F, d_counts, st));
+      HIP_TRY(hipEventRecord(X->ev_rows, st));
+    }
     if (hash_mode) HIP_TRY(launch_sparse_write(S, nocc, sws, o_ts, o_val, o_gid, o_glob, st));
-    else HIP_TRY(launch_finalize_write(F, d_counts, o_ts, o_val, o_gid, o_glob, st));
+    else HIP_TRY(launch_finalize_write(F, d_counts, ts_runs ? nullptr : o_ts, o_val, o_gid, o_glob, st));
     if (!direct) {
       HIP_TRY(hipMemcpyAsync(res->ts, o_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->val, o_val, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
       HIP_TRY(hipMemcpyAsync(res->gid, o_gid, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
       if (per_glob_rows) HIP_TRY(hipMemcpyAsync(res->glob, o_glob, size_t(nrows_out) * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (ts_runs) {   // timestamps expanded here while finalize_write's rows cross the host link
+      HIP_TRY(hipEventSynchronize(X->ev_rows));
+      expand_ts_runs(res->ts, nrows_out, F);
     }
     HIP_TRY(hipStreamSynchronize(st));
   }

@@ -188,15 +188,38 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
       tot += ws[w];
     }
     if (r.exists) {
-      uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
-      unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
-      out_ts[pos] = F.bucket_base + (int64_t)b * F.step;
+      const uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
+      const unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
+      if (out_ts) out_ts[pos] = F.bucket_base + (int64_t)b * F.step;   // null: expanded on the host (bucket_pos)
       out_val[pos] = r.value;
       out_gid[pos] = uint32_t(r.gid);
       if (out_glob) out_glob[pos] = r.glob;   // null: merged rows (glob 0, a shared zero block on the host)
     }
     off += tot;
     __syncthreads();
+  }
+}
+
+// Large results (FParams::bucket_pos, whole key space): the row position of every bucket's first row -- rows are
+// bucket-major, so it is the scanned count of the block holding the bucket's first key plus the existing keys ahead of
+// it in that block -- and bucket_pos[nbuckets] = the row count.  One workgroup per bucket; enqueued before
+// finalize_write, so the host expands the timestamps while the other columns cross the host link.
+__global__ __launch_bounds__(FB) void finalize_bucket_pos(FParams F, const uint32_t* block_offsets, uint32_t nb) {
+  __shared__ uint32_t ws[FB / 64];
+  const unsigned long long per = F.per_glob ? F.ngroups * F.nglob_slots : (F.collapse ? 1ull : F.ngroups);
+  const unsigned long long b = blockIdx.x;
+  const unsigned long long K = b * per;
+  const unsigned long long blk = K / (FB * FITEMS);
+  uint32_t n = 0;
+  for (unsigned long long k = blk * FB * FITEMS + threadIdx.x; k < K; k += FB) n += make_row(F, k).exists ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
+  if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = n;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t t = 0;
+    for (int w = 0; w < FB / 64; w++) t += ws[w];
+    F.bucket_pos[b] = block_offsets[blk] + t;
+    if (b == 0) F.bucket_pos[F.nbuckets] = block_offsets[nb];
   }
 }
 
@@ -758,6 +781,13 @@ hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int
   uint32_t nb = finalize_blocks(F.nkeys);
   if (nb == 0) return hipSuccess;
   hipLaunchKernelGGL(finalize_write, dim3(nb), dim3(FB), 0, stream, F, d_counts, ts, val, gid, glob);
+  return hipGetLastError();
+}
+
+hipError_t launch_finalize_bucket_pos(const FParams& F, const uint32_t* d_counts, hipStream_t stream) {
+  const uint32_t nb = finalize_blocks(F.nkeys);
+  if (nb == 0 || F.nbuckets == 0 || !F.bucket_pos || F.key_base) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(finalize_bucket_pos, dim3(uint32_t(F.nbuckets)), dim3(FB), 0, stream, F, d_counts, nb);
   return hipGetLastError();
 }
 

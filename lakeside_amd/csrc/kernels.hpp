@@ -29,6 +29,10 @@ struct FParams {
   // cells [cell_base, ...) of the full table (0, 0: the whole table)
   unsigned long long key_base;
   unsigned long long cell_base;
+  // large results (whole key space): finalize_bucket_pos writes the row position of every bucket's first row here
+  // (rows are in bucket-major order) and finalize_write is given no timestamp column -- the host expands it (8 of the
+  // 20-24 bytes per row that cross the host link)
+  uint32_t* bucket_pos;
 };
 
 constexpr int AGG_AVG = 4;
@@ -222,6 +226,7 @@ uint32_t finalize_blocks(unsigned long long nkeys);
 // Split form: count + scan (row total at d_counts[nblocks]), then write -- the write may target mapped pinned host
 // memory (hipHostMalloc) directly, so no device->host copy follows.
 hipError_t launch_finalize_count(const FParams& F, uint32_t* d_counts, hipStream_t stream);
+hipError_t launch_finalize_bucket_pos(const FParams& F, const uint32_t* d_counts, hipStream_t stream);
 hipError_t launch_finalize_write(const FParams& F, const uint32_t* d_counts, int64_t* ts, double* val,
                                  uint32_t* gid, uint32_t* glob, hipStream_t stream);
 hipError_t launch_finalize(const FParams& F, uint32_t* d_counts, int64_t* ts, double* val, uint32_t* gid,

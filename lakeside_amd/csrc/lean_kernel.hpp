@@ -26,7 +26,7 @@
 namespace lk {
 
 constexpr int LEAN_H = HCAP / 2;                                 // LDS hash cells (hash mode)
-constexpr uint32_t LEAN_CHUNKS = TILE_ROWS / 16 + RUN_CAP + 1;   // chunks of a tile, upper bound
+constexpr uint32_t LEAN_CHUNKS = (TILE_ROWS / 16 + RUN_CAP + 1 + 7) & ~7u;   // chunks of a tile, upper bound (x4 B writes)
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
 constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
 
@@ -73,7 +73,7 @@ struct LeanLds {
   static constexpr uint32_t RW = lean_dir_words(NL);
   LeanRun runs[RUN_CAP];
   uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
-  uint8_t ctab[LEAN_CHUNKS];              // flattened chunk -> run
+  alignas(4) uint8_t ctab[LEAN_CHUNKS];   // flattened chunk -> run (written 4 entries at a time)
   uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
   // The tile's aggregation table: the hash table, or the direct table (the tile's buckets x ngroups cells, P.dir_planes
   // u64 planes: value (SUM: hi), SUM: lo, rows when the table keeps them)
@@ -84,7 +84,7 @@ struct LeanLds {
   uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
   // late columns (NL > 0): value runs (+ sentinel), run-block tables, lookup values, the late conjuncts' table
   LRun lruns[NLA][NL > 0 ? RUN_CAP + 1 : 1];
-  uint8_t lrblk[NLA][NL > 0 ? TILE_ROWS / 64 + 8 : 1];
+  alignas(4) uint8_t lrblk[NLA][NL > 0 ? TILE_ROWS / 64 + 8 : 1];
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
@@ -317,15 +317,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
 #pragma unroll
   for (int k = 0; k < NL; k++)   // run-block tables of the late columns (runs staged above)
     if ((lpres >> k) & 1u)
-      for (uint32_t b = tid; b <= nblk; b += BLOCK) {
+      for (uint32_t b0 = 4u * uint32_t(tid); b0 <= nblk; b0 += 4u * BLOCK) {   // 4 blocks per thread: one search
         uint32_t lo = 0;
-        const uint32_t v = lvb[k] + 64u * b;
+        const uint32_t v = lvb[k] + 64u * b0;
 #pragma unroll
         for (uint32_t st = RUN_CAP / 2; st >= 1; st >>= 1) {
           const uint32_t m = lo + st;
           lo = (m < lnr[k] && L.lruns[k][m].start <= v) ? m : lo;
         }
-        L.lrblk[k][b] = uint8_t(lo);
+        uint32_t word = lo;
+#pragma unroll
+        for (uint32_t i = 1; i < 4; i++) {
+          while (lo + 1u < lnr[k] && L.lruns[k][lo + 1u].start <= v + 64u * i) lo++;
+          word |= lo << (8u * i);
+        }
+        *reinterpret_cast<uint32_t*>(&L.lrblk[k][b0]) = word;
       }
   if (tid < 64) {   // exclusive prefix of the chunk counts (<= 128 runs: two per lane)
     const uint32_t i0 = 2u * uint32_t(lane), i1 = i0 + 1u;
@@ -350,14 +356,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   }
   __syncthreads();
   const uint32_t total = L.cb[nr];   // chunks of the tile
-  for (uint32_t q = tid; q < total; q += BLOCK) {   // chunk -> run: last run whose first chunk <= q
+  // chunk -> run: the last run whose first chunk <= q; 4 chunks per thread (one search, then runs advanced in order)
+  for (uint32_t q = 4u * uint32_t(tid); q < total; q += 4u * BLOCK) {
     uint32_t lo = 0;
 #pragma unroll
     for (uint32_t st = RUN_CAP / 2; st >= 1; st >>= 1) {
       const uint32_t m = lo + st;
       lo = (m < nr && L.cb[m] <= q) ? m : lo;
     }
-    L.ctab[q] = uint8_t(lo);
+    uint32_t word = lo;
+#pragma unroll
+    for (uint32_t i = 1; i < 4; i++) {
+      while (lo + 1u < nr && L.cb[lo + 1u] <= q + i) lo++;
+      word |= lo << (8u * i);
+    }
+    *reinterpret_cast<uint32_t*>(&L.ctab[q]) = word;
   }
   __syncthreads();
 
@@ -762,10 +775,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
             z0 |= zf(w0 ^ rp);
             if (BW == 4) z1 |= zf(w1 ^ rp);
           }
-          // valid rows in field-high-bit form
-          unsigned long long vm = 0;
-#pragma unroll
-          for (int e = 0; e < 16; e++) vm |= (unsigned long long)((valid >> e) & 1u) << (e * BW + BW - 1);
+          // valid rows [a, bnd) in field-high-bit form: fields a*BW .. bnd*BW - 1 of the high-bit pattern
+          constexpr unsigned long long HI64 = ((unsigned long long)HI << 32) | HI;
+          const uint32_t hb = bnd * BW;   // <= 64
+          const unsigned long long vm = valid ? (hb >= 64u ? ~0ull : (1ull << hb) - 1ull) & ~((1ull << (a * BW)) - 1ull) & HI64 : 0ull;
           m = (((unsigned long long)z1 << 32) | z0) & vm;
           shs = BW == 1 ? 0u : BW == 2 ? 1u : 2u;
         }
@@ -891,11 +904,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         // Late columns: the wave's passing rows are appended to its LDS list (lane-major) and processed LEAN_TRIP at
         // a time (list_trip) -- a per-lane loop would run as many trips as the lane with the most passing rows, each
         // a chain of dependent late-column and value loads.
-        uint32_t f16 = uint32_t(m);
-        if (swar) {
-          f16 = 0;
+        // passing rows: row e at bit (e << fs) + (1 << fs) - 1 of fm (SWAR: the field's high bit; else one bit per row)
+        unsigned long long fm = m;
+        uint32_t fs = shs;
+        uint32_t f16 = 0;
+        if constexpr (ECH) {   // early_late: one bit per row
+          f16 = uint32_t(m);
+          if (swar) {
+            f16 = 0;
 #pragma unroll
-          for (int e = 0; e < 16; e++) f16 |= uint32_t((m >> (e * BW + BW - 1)) & 1ull) << e;
+            for (int e = 0; e < 16; e++) f16 |= uint32_t((m >> (e * BW + BW - 1)) & 1ull) << e;
+          }
         }
         // early_late: row e's late code k from the chunk's window (chunk-relative index e - a), its lookup value
         auto late_code = [&](int k, uint32_t e) __attribute__((always_inline)) -> uint32_t {
@@ -942,6 +961,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
             }
             f16 = keep;
           }
+          fm = f16;
+          fs = 0;
         }
         if constexpr (ECH) {
           // COUNT(*) into a one-bucket direct table (tag queries): the chunk's late codes are in
@@ -967,7 +988,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
             continue;   // (uniform) the next round of chunks
           }
         }
-        const uint32_t cnt = uint32_t(__popc(f16));
+        const uint32_t cnt = uint32_t(__popcll(fm));
         uint32_t inc = cnt;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -978,10 +999,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         const uint32_t pos0 = inc - cnt;
         for (uint32_t done = 0; done < wtotal;) {   // uniform
           const uint32_t take = min(LEAN_LIST - (ltail - lhead), wtotal - done);
-          uint32_t f = f16, pos = pos0;
+          unsigned long long f = fm;
+          uint32_t pos = pos0;
           while (f) {
-            const uint32_t e = uint32_t(__builtin_ctz(f));
-            f &= f - 1u;
+            const uint32_t e = uint32_t(__builtin_ctzll(f)) >> fs;
+            f &= f - 1ull;
             if (pos >= done && pos < done + take) {
               const uint32_t code = lit ? lean_code<BW>(w0, w1, w2, e) : rval;
               uint32_t hi16 = code;
@@ -1034,10 +1056,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     if (tid == 0) {
       pbytes += sizeof(TileDesc) + 3 * sizeof(TileCol) + uint64_t(nr) * sizeof(RunDesc) + uint64_t(dict_n) * 8u;
     }
-    for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_t[i]) + __popc(L.lines_v[i]));
+    // diagnostics only (LK_ABLATE bits 8..11): leave a category out of the count -- bit 8 timestamp lines, 9 value
+    // lines, 10 late-stream lines, 11 the name stream and metadata
+    const uint32_t pm = P.ablate >> 8;
+    if (pm & 8u) pbytes = 0;
+    for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK)
+      pbytes += 128u * uint64_t((pm & 1u ? 0 : __popc(L.lines_t[i])) + (pm & 2u ? 0 : __popc(L.lines_v[i])));
 #pragma unroll
     for (int k = 0; k < NL; k++)
-      for (uint32_t i = tid; i < LEAN_LLINES; i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_l[k][i]));
+      for (uint32_t i = tid; i < LEAN_LLINES && !(pm & 4u); i += BLOCK) pbytes += 128u * uint64_t(__popc(L.lines_l[k][i]));
     if (pbytes) atomicAdd(P.plan_bytes, (unsigned long long)pbytes);
   }
   // ---- the table's cells -> the global table (device atomics) ----

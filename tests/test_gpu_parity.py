@@ -231,6 +231,9 @@ def test_c5_shape_high_cardinality_group_by(engine):
     assert len(res) > 50000
     _synth_case(engine, 2, 1 << 19, 1, 0.05, filt, "max", [synth.CONTAINER], step=600000, highcard_n=100000,
                 hour=0)
+    # 60 buckets x 20k groups (1.2M output keys): the timestamps of a result this large are expanded on the host from
+    # each bucket's first row (FParams::bucket_pos); most buckets' first keys are empty cells
+    _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
 
 
 def test_full_size_properties(engine):
