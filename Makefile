@@ -54,7 +54,7 @@ clean:
 	rm -rf build $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
 
 
-.PHONY: all clean asm exp-depth3
+.PHONY: all clean asm
 
 # CPU restatement of the evaluator (oracle: test / bench-baseline infrastructure only, never the product path)
 CPULIB = oracle/liblkcpu.so
@@ -63,11 +63,15 @@ $(CPULIB): oracle/cpu/lkcpu.cpp
 
 all: $(CPULIB)
 
-# Kernel A/B builds (experiments): the library with another software-pipeline depth, lakeside_amd/exp/ (LK_LIB_PATH).
-exp-depth3:
-	@mkdir -p build/exp/obj lakeside_amd/exp
-	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) '-DLK_DEPTH(n)=2' -c $(SRC)/scan_$$a.hip -o build/exp/obj/scan_$$a.o & done; wait
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_d2.so $(HOST_OBJS) $(OBJDIR)/kernels.o build/exp/obj/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+# Kernel A/B builds (experiments): the library with the scan kernels built under EXP_FLAGS (e.g.
+# EXP_FLAGS=-DLK_LEAN_ROWS=4 EXP_NAME=rows4) -> lakeside_amd/exp/liblakeside_gpu_<EXP_NAME>.so, selected with LK_LIB_PATH.
+EXP_FLAGS ?=
+EXP_NAME ?= x
+exp: $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o
+	@mkdir -p build/exp/$(EXP_NAME) lakeside_amd/exp
+	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) $(EXP_FLAGS) -c $(SRC)/scan_$$a.hip -o build/exp/$(EXP_NAME)/scan_$$a.o & done; wait
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_$(EXP_NAME).so $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o build/exp/$(EXP_NAME)/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+.PHONY: exp
 
 # Host-only loader harness (no HIP): the Parquet walk, dictionary interning and staging copy of lakeside_amd/csrc/
 # loader.cpp, plain and under ASan + UBSan / TSan (`make sanitize`, tools/sanitize.sh).

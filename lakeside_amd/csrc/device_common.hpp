@@ -179,6 +179,10 @@ __device__ __forceinline__ void global_merge(const QParams& P, unsigned long lon
   if (!(P.lean & (LEAN_NO_CNT | LEAN_NO_ROWS | LEAN_SUM_EXISTS))) atomicAdd(&P.cnt[cell], (unsigned long long)cnt);
   if (AGG == AGG_SUM) {
     if (P.lean & LEAN_SUM_EXISTS) hi = hi + 0.0;   // never -0.0: the empty cell's marker (layout.hpp)
+    if (P.exact_sum) {   // exact adds (QParams::exact_sum): no compensation, no returned value to wait for
+      __hip_atomic_fetch_add(&P.hi[cell], hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      return;
+    }
     double old = atomicAdd(&P.hi[cell], hi);   // returning atomic: old is exact -> TwoSum recovers the error
     double s, e;
     two_sum(old, hi, s, e);

@@ -1129,6 +1129,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   std::vector<uint32_t> seg_begin;
   uint32_t total_tiles = 0;
   uint64_t rows_scanned = 0, alg_bytes = 0;
+  // QParams::exact_sum: every bound value column integral (HostCol::int_abs_max), its largest magnitude, their rows
+  bool vals_integral = true;
+  double vals_abs_max = 0.0, vals_rows = 0.0;
   bool all_lean = true;       // every fused-kernel tile is scan_lean's (the general kernel need not run)
   int local_err = 0;          // distributed: a rank-local failure, agreed on with the other ranks after the scan
   std::string local_msg;
@@ -1168,6 +1171,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
           // an integer value column in a glob whose value type is FLOAT is cast to FLOAT first (DuckDB's implicit
           // BIGINT -> FLOAT of the union column), then aggregated as a float
           if (vunion == pq::FLOAT && hc.ptype != pq::FLOAT) pad |= VCONV_VIA_FLOAT;
+          if (hc.int_abs_max < 0.0) vals_integral = false;
+          vals_abs_max = std::max(vals_abs_max, hc.int_abs_max);
+          vals_rows += double(S.num_rows);
         }
         q.cols[qc] = QCol{hc.d_pages, hc.d_runs, hc.d_tcols, hc.d_remap, 1u, pad};
         alg_bytes += hc.compressed_bytes;
@@ -1415,6 +1421,13 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
                     ? (all_lean ? 2u : 1u) : 0u;
   if (numeric && !(vleaf && gsegs.empty())) P.lean = 0;   // the general row scan accumulates every table field
   if (P.lean && getenv("LK_NO_DENSE_DIRECT")) P.lean |= LEAN_NO_DENSE_DIRECT;   // env: A/B only
+  // exact integer sums: every partial sum of <= vals_rows integers of magnitude <= vals_abs_max is <= 2^52 (a margin for
+  // the FLOAT cast of union_by_name integer columns), so it is
+  // exact in any order and the compensated sum equals the plain one bit for bit (LK_NO_EXACT_SUM=1: A/B)
+  P.exact_sum = (kagg == AGG_SUM && !sketch && !ces && vals_integral && vals_abs_max * vals_rows <= 4503599627370496.0 &&
+                 !getenv("LK_NO_EXACT_SUM")) ? 1u : 0u;
+  // a group space far beyond scan_lean's LDS hash table (1M+ cells): register cells go straight to the global table
+  P.global_cells = (uint64_t(ngroups) * nbuckets >= (1ull << 20) && !getenv("LK_LDS_CELLS")) ? 1u : 0u;
   if (vleaf && !qsegs.empty()) {   // scan_lean tests the value leaves of every row its string conjuncts pass
     P.nvl = uint32_t(nleaves.size());
     P.vtab = vtab;
@@ -2262,19 +2275,19 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       res->owned.push_back(kv.second);
       res->qt_of_glob[gi].emplace_back(c, res->owned.back().c_str());
     }
-  char buf[896];
+  char buf[1280];
   snprintf(buf, sizeof(buf),
            "{\"scan_ms\":%.6f,\"total_ms\":%.6f,\"plan_ms\":%.6f,\"device_ms\":%.6f,\"launch_ms\":%.6f,"
            "\"sync_ms\":%.6f,\"alloc_ms\":%.6f,\"copy_ms\":%.6f,\"rows_scanned\":%llu,"
            "\"algorithmic_bytes\":%llu,\"tiles\":%u,\"cells\":%llu,\"segments\":%zu,\"general_segments\":%zu,"
            "\"failed_globs\":%zu,\"table\":\"%s\","
            "\"slots\":%llu,\"occupied\":%llu,\"attempts\":%d,\"plan_bytes\":%llu,\"reduce\":\"%s\","
-           "\"dims_ms\":%.6f,\"dims_rebuilt\":%d,\"emit\":\"%s\"",
+           "\"dims_ms\":%.6f,\"dims_rebuilt\":%d,\"emit\":\"%s\",\"exact_sum\":%u,\"global_cells\":%u",
            double(scan_ms), ms_since(t_start), plan_ms, device_ms, launch_ms, sync_ms, alloc_ms, copy_ms, (unsigned long long)rows_scanned,
            (unsigned long long)alg_bytes, total_tiles, (unsigned long long)ncells, qsegs.size() + gsegs.size(), gsegs.size(),
            nfailed, hash_mode ? "hash" : "dense", (unsigned long long)(hash_mode ? cap : ncells), nocc, attempts, plan_bytes,
            !dist ? "none" : (keyrange ? "keyrange" : (hash_mode ? "records_to_root" : "gather_to_root")), dims_ms,
-           dims_rebuilt, emit_mode);
+           dims_rebuilt, emit_mode, P.exact_sum, P.global_cells);
   res->stats = buf;
   if (dist) {   // the distributed call's stages and collectives (this rank)
     const CommCounters cc = comm_counters(E);

@@ -171,7 +171,9 @@ struct QParams {
   uint32_t lean;                    // LEAN_* bits: table fields the scan leaves to the fix-up pass (fewer atomics)
   uint32_t* flags;                  // error / diagnostic flags
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode,
-                                    // 4 no global-table atomics
+                                    // 4 no global-table atomics; scan_lean: 0x100..0x800 plan-byte categories left
+                                    // out, 0x10000 no row listed, 0x20000 listed rows dropped unprocessed, 0x40000
+                                    // listed rows loaded but not accumulated
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
   // Plan bytes (the roofline numerator): bytes the late-materialized plan must read from HBM, counted
   // by the kernel: tile metadata + staged runs + dictionary lookups, every fully decoded stream of a tile, and the
@@ -187,6 +189,12 @@ struct QParams {
                                      // list then carries each row's group term; lean_kernel.hpp)
   uint32_t spec_gather;              // scan_lean NL > 0 with a late filter: a listed row's timestamp / value loads go
                                      // out with its late-column loads, before the late filter decides (lean_kernel.hpp)
+  // SUM over integral values (every segment's value column: integers of magnitude <= M, load-time summary) whose
+  // rows x M < 2^53: every partial sum is exact in any order, so the TwoSum compensation (and the old value a
+  // returning atomic fetches for it) is dropped -- adds are fire-and-forget; results are identical
+  uint32_t exact_sum;
+  // group spaces far beyond the tile's LDS hash table (C5's 10M container ids): cells go straight to the global table
+  uint32_t global_cells;
   // Numeric comparison leaves on the value column (`value > 1.5`, BaseExpr.scala:488-498) in the fused kernel: a row
   // whose string conjuncts pass is kept iff vtab bit (its leaves' outcomes, bit k = leaf k) is set -- the numeric
   // conjuncts' value.  scan_lean tiles hold no NULL value, so no leaf is UNKNOWN there.

@@ -40,7 +40,22 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #ifndef LK_LEAN_WAVES2
 #define LK_LEAN_WAVES2 4
 #endif
-#define LEAN_WAVES(NL) ((NL) <= 1 ? 5 : LK_LEAN_WAVES2)   // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES2)
+#ifndef LK_LEAN_WAVES1
+#define LK_LEAN_WAVES1 5
+#endif
+// chunk loads in flight ahead of the round, by late-column count (A/B: -DLK_LEAN_PF0 / 1 / 2); the 5-wave shapes
+// (NL <= 1, 96 VGPRs) keep their register budget, the 4-wave NL = 2 shape has room for a deeper ring
+#ifndef LK_LEAN_PF0
+#define LK_LEAN_PF0 0
+#endif
+#ifndef LK_LEAN_PF1
+#define LK_LEAN_PF1 1
+#endif
+#ifndef LK_LEAN_PF2
+#define LK_LEAN_PF2 3
+#endif
+// waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES1 / -DLK_LEAN_WAVES2)
+#define LEAN_WAVES(NL) ((NL) <= 1 ? LK_LEAN_WAVES1 : LK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 // the per-wave list is a ring indexed with & (LEAN_LIST - 1) and drained LEAN_TRIP rows at a time
@@ -428,7 +443,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   // span), or the LDS hash table
   auto flush = [&]() __attribute__((always_inline)) {
     if (acc.rows == 0) return;
-    if (!tspan) {
+    if (!tspan && P.global_cells) {   // (uniform) a group space far beyond the LDS table: straight to HBM
+      global_merge<AGG, HASH>(P, acc.key, acc.rows, acc.cnt, acc.hi, acc.lo, acc.ext);
+    } else if (!tspan) {
       lds_merge<AGG, HASH, false>(L.agg.hs, P, acc);
     } else if (acc.key & GBIT) {
       global_merge<AGG, HASH>(P, acc.key & ~GBIT, acc.rows, acc.cnt, acc.hi, acc.lo, acc.ext);
@@ -436,11 +453,15 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
       const uint32_t x = uint32_t(acc.key);
       if (AGG == AGG_SUM) {
         const double h = acc.hi + 0.0;   // never -0.0 (the empty marker)
-        const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
-        double s, e;
-        two_sum(old, h, s, e);
-        const double c = acc.lo + e;
-        if (c != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), c);
+        if (P.exact_sum) {   // exact adds: nothing to compensate
+          __hip_atomic_fetch_add(reinterpret_cast<double*>(rv + x), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        } else {
+          const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
+          double s, e;
+          two_sum(old, h, s, e);
+          const double c = acc.lo + e;
+          if (c != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), c);
+        }
       } else if (AGG == AGG_MIN) {
         atomicMin(rv + x, acc.ext);
       } else if (AGG == AGG_MAX) {
@@ -628,6 +649,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         if (AGG != AGG_COUNT || P.nvl) mark(L.lines_v, (vb1 + rr[u]) * 8u, line_v0);
       }
     }
+    if (P.ablate & 0x40000u) {   // diagnostics only: nothing accumulated (the loads' cost without the table updates)
+#pragma unroll
+      for (int u = 0; u < N; u++) p[u] = p[u] && (tt[u].x ^ xx[u].x ^ dd[u]) == 0x9e3779b9u;
+    }
 #pragma unroll
     for (int u = 0; u < N; u++)
       if (p[u])
@@ -640,6 +665,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   uint32_t* const wl = L.wlist[tid >> 6];
   auto list_trip = [&](auto ec, uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
     constexpr bool ELIST = decltype(ec)::value;   // entries carry complete group terms (early_late)
+    if (P.ablate & 0x20000u) {   // diagnostics only: listed rows dropped unprocessed (the trips' cost)
+      lhead += n;
+      return;
+    }
     uint32_t rr[LEAN_ROWS], dd[LEAN_ROWS];
     bool aa[LEAN_ROWS];
 #pragma unroll
@@ -676,16 +705,19 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         em &= em ? em - 1 : 0ull;
       }
     }
-    // NL > 0: the next round's packed codes are loaded one round ahead, so they arrive while this round waits on its
-    // late-column and value loads (loads return in issue order: one memory round trip less per round)
+    // The packed codes of the next PF rounds are in flight while a round runs (a register ring; loads return in issue
+    // order, so a round waits only for its own chunk): a round's own work is far shorter than a memory round trip, and
+    // one load per lane in flight would leave the tile's stream latency-bound (PF = 0: loaded in the round itself).
+    constexpr int PF = NL == 0 ? LK_LEAN_PF0 : (NL == 1 ? LK_LEAN_PF1 : LK_LEAN_PF2);
     auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
       const bool lv = qq < total;
       const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];
       const uint32_t bn = (Rn.off_lit & 0x7fffffffu) + 2u * BW * (qq - Rn.cbk);
       return __builtin_amdgcn_raw_buffer_load_b128(rs2, (lv && (Rn.off_lit & 0x80000000u)) ? (bn & ~3u) : OOB, 0, 0);
     };
-    v4u xpre = v4u{0u, 0u, 0u, 0u};
-    if constexpr (NL > 0) xpre = chunk_load(uint32_t(tid));
+    v4u xr[PF > 0 ? PF : 1];
+#pragma unroll
+    for (int i = 0; i < PF; i++) xr[i] = chunk_load(uint32_t(tid) + uint32_t(i) * BLOCK);
     // early_late: chunk qq's late codes -- one 20-B window per late column over the late values of its valid rows
     // (meta: bit 31 a bit-packed window, bits 0..7 its bit offset; bit 30 the rows straddle a run boundary: decoded
     // row by row; else the RLE run's code)
@@ -740,16 +772,18 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
       const uint32_t byte = (R.off_lit & 0x7fffffffu) + 2u * BW * k;
       v4u x;
       LWin lcur[LT::NLA];
-      if constexpr (NL > 0) {
-        x = xpre;
-        xpre = chunk_load(q + BLOCK);
-        if constexpr (ECH) {
+      if constexpr (PF > 0) {
+        x = xr[0];
 #pragma unroll
-          for (int k = 0; k < NL; k++) lcur[k] = lpre[k];
-          late_load(q + BLOCK);
-        }
+        for (int i = 0; i + 1 < PF; i++) xr[i] = xr[i + 1];
+        xr[PF - 1] = chunk_load(q + uint32_t(PF) * BLOCK);
       } else {
         x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
+      }
+      if constexpr (ECH) {
+#pragma unroll
+        for (int k = 0; k < NL; k++) lcur[k] = lpre[k];
+        late_load(q + BLOCK);
       }
       const uint32_t sh = (byte & 3u) * 8u;
       uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
@@ -862,10 +896,14 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
                 min_nan_check<AGG>(P, true, v);
                 if (AGG == AGG_SUM) {
                   const double h = v + 0.0;   // never -0.0 (the empty marker)
-                  const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
-                  double s, e;
-                  two_sum(old, h, s, e);
-                  if (e != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), e);
+                  if (P.exact_sum) {
+                    __hip_atomic_fetch_add(reinterpret_cast<double*>(rv + x), h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                  } else {
+                    const double old = atomicAdd(reinterpret_cast<double*>(rv + x), h);
+                    double s, e;
+                    two_sum(old, h, s, e);
+                    if (e != 0.0) atomicAdd(reinterpret_cast<double*>(rlo + x), e);
+                  }
                 } else if (AGG == AGG_MIN) {
                   atomicMin(rv + x, dbl_order(v));
                 } else if (AGG == AGG_MAX) {
@@ -988,6 +1026,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
             continue;   // (uniform) the next round of chunks
           }
         }
+        if (P.ablate & 0x10000u) fm = 0;   // diagnostics only: no row listed (the chunk filter's cost alone)
         const uint32_t cnt = uint32_t(__popcll(fm));
         uint32_t inc = cnt;
 #pragma unroll

@@ -2,6 +2,8 @@
 // (tools/load_check.cpp under ASan / UBSan / TSan, `make sanitize`).
 #include "loader.hpp"
 
+#include <cmath>
+
 #include <algorithm>
 #include <atomic>
 #include <chrono>
@@ -447,12 +449,14 @@ inline uint32_t run_containing(const std::vector<RunDesc>& runs, uint32_t lo, ui
 // Tiles of one row group: row ranges inside one page of every column, clipped so each stream's runs over a tile fit
 // RUN_CAP; the timestamp zone map per tile.  `page0[c]`: index of column c's first page of this row group.
 void build_tiles_rg(const SegmentData& S, const std::vector<std::vector<HostPage>>& pages, uint32_t rg,
-                    const std::vector<size_t>& page0, std::vector<TileDesc>& tiles, std::vector<std::vector<TileCol>>& tcols) {
+                    const std::vector<size_t>& page0, std::vector<TileDesc>& tiles, std::vector<std::vector<TileCol>>& tcols,
+                    std::vector<double>& imax) {
   const int nc = int(S.cols.size());
   const int ts_col = S.col_index(kTimestamp);
   std::vector<size_t> cursor(page0);
   const uint32_t nrows = uint32_t(S.rg_rows[rg]);
   tcols.assign(size_t(nc), {});
+  imax.assign(size_t(nc), 0.0);   // HostCol::int_abs_max over this row group
   uint32_t a = 0;
   std::vector<size_t> pidx(static_cast<size_t>(nc));
   while (a < nrows) {
@@ -522,6 +526,28 @@ void build_tiles_rg(const SegmentData& S, const std::vector<std::vector<HostPage
         tc.ndruns = r1 - r0 + 1;
       }
       tcols[size_t(c)].push_back(tc);
+      const int pt = S.cols[size_t(c)].ptype;
+      if (c != ts_col && imax[size_t(c)] >= 0.0) {   // integral-value summary (a tile's values: indices [va, ve))
+        if (p.d.kind != PAGE_PLAIN64 || (pt != pq::DOUBLE && pt != pq::INT64)) {
+          imax[size_t(c)] = -1.0;
+        } else {
+          bool integral = true;
+          double m = imax[size_t(c)];
+          for (uint32_t i = va; i < ve; i++) {
+            double x;
+            if (pt == pq::DOUBLE) {
+              memcpy(&x, p.host_vals + size_t(i) * 8, 8);
+              integral &= x == std::trunc(x);   // NaN fails; +-inf fails the bound below
+            } else {
+              int64_t y;
+              memcpy(&y, p.host_vals + size_t(i) * 8, 8);
+              x = double(y);
+            }
+            m = std::max(m, std::fabs(x));
+          }
+          imax[size_t(c)] = integral ? m : -1.0;
+        }
+      }
       if (c == ts_col && p.d.kind == PAGE_PLAIN64 && !S.cols[size_t(c)].is_string) {
         const int64_t* v = reinterpret_cast<const int64_t*>(p.host_vals);   // (host_vals: 8-B PLAIN values)
         int64_t lo = INT64_MAX, hi = INT64_MIN;
@@ -759,16 +785,22 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
   // ---- 3. tiles, per row group in parallel ----
   std::vector<std::vector<TileDesc>> rg_tiles(nrg);
   std::vector<std::vector<std::vector<TileCol>>> rg_tcols(nrg);
+  std::vector<std::vector<double>> rg_imax(nrg);
   if (S->num_rows > 0 && nc) {
     parallel_for(nrg, threads, [&](size_t rg) {
       std::vector<size_t> p0(nc);
       for (size_t c = 0; c < nc; c++) p0[c] = page0[c][rg];
-      build_tiles_rg(*S, pages, uint32_t(rg), p0, rg_tiles[rg], rg_tcols[rg]);
+      build_tiles_rg(*S, pages, uint32_t(rg), p0, rg_tiles[rg], rg_tcols[rg], rg_imax[rg]);
     });
     for (size_t rg = 0; rg < nrg; rg++) {
       S->tiles.insert(S->tiles.end(), rg_tiles[rg].begin(), rg_tiles[rg].end());
       for (size_t c = 0; c < nc; c++)
         S->cols[c].tcols.insert(S->cols[c].tcols.end(), rg_tcols[rg][c].begin(), rg_tcols[rg][c].end());
+    }
+    for (size_t c = 0; c < nc; c++) {   // integral-value summary over the row groups (HostCol::int_abs_max)
+      double m = 0.0;
+      for (size_t rg = 0; rg < nrg && m >= 0.0; rg++) m = rg_imax[rg][c] < 0.0 ? -1.0 : std::max(m, rg_imax[rg][c]);
+      S->cols[c].int_abs_max = S->cols[c].is_string ? -1.0 : m;
     }
   }
   for (size_t ci = 0; ci < nc; ci++) {

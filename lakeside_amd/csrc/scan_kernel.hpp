@@ -105,6 +105,10 @@ __device__ __forceinline__ void lds_merge(LT& L, const QParams& P, const Acc& a)
         if (a.cnt) {
           atomicAdd(&L.hcnt[h], a.cnt);
           if (AGG == AGG_SUM) {
+            if (P.exact_sum) {   // exact adds: nothing to compensate
+              __hip_atomic_fetch_add(&L.hhi[h], a.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+              return;
+            }
             double old = atomicAdd(&L.hhi[h], a.hi);
             double s, e;
             two_sum(old, a.hi, s, e);

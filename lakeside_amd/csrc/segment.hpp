@@ -193,6 +193,9 @@ struct HostCol {
   bool pages_lean_name = false;           // every page: dictionary indices, chunk dictionary <= 64 values, 1..6 bits
   bool pages_lean_late = false;           // every page: dictionary indices of <= 32 bits
   uint64_t compressed_bytes = 0;          // Σ ColumnMetaData.total_compressed_size (algorithmic bytes)
+  // DOUBLE / INT64 columns with PLAIN pages: the largest magnitude when every value is an integer, else -1 (a
+  // non-integral or non-finite value, another encoding, another type) -- QParams::exact_sum
+  double int_abs_max = -1.0;
   std::vector<PageDesc> pages;            // host copy (planner reads dict sizes / null flags)
   std::vector<RunDesc> runs;              // load-time only
   std::vector<TileCol> tcols;             // load-time only

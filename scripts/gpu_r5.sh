@@ -11,7 +11,7 @@ if [ -z "$NOTESTS" ]; then
 fi
 for e in ${ENVS:--}; do
   ee=""; [ "$e" != "-" ] && ee=$(echo "$e" | tr "+" " ")
-  tag=$(echo "${e}" | tr '=,+' '___')
+  tag=$(echo "${e}" | tr '=,+/' '____')
   for q in ${QUERIES:-}; do
     cs=0; [ -n "$VALIDATE" ] && cs=-1
     env $ee timeout -k 10 ${PER:-400} python3 bench.py --query $q --steps ${STEPS:-10} --warmup 3 --cpu-sample $cs $BENCH_ARGS > gpurun_out/r5/${q}_${tag}.json 2> gpurun_out/r5/${q}_${tag}.log || exit $?

@@ -236,6 +236,27 @@ def test_c5_shape_high_cardinality_group_by(engine):
     _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
 
 
+@pytest.mark.parametrize("exact", [True, False], ids=["exact_sum", "compensated"])
+def test_integral_sums_exact_and_compensated(engine, exact, monkeypatch):
+    """Integer values (load-time summary: every value integral, |v| <= 999): SUM adds are fire-and-forget
+    (QParams::exact_sum) -- on the direct LDS table, the LDS hash table and the global table (C5 shape, global
+    cells) -- and equal the compensated path (LK_NO_EXACT_SUM=1) and the oracle bit for bit.  Real values never
+    take it."""
+    from lakeside_amd import synth
+    if not exact:
+        monkeypatch.setenv("LK_NO_EXACT_SUM", "1")
+    filt = synth.leaf(synth.NAME, "in", "metric_03", "metric_09")
+    res = _synth_case(engine, 2, 1 << 20, 0, 0.0, filt, "sum", [synth.SERVICE])
+    assert res.stats["exact_sum"] == (1 if exact else 0)
+    res = _synth_case(engine, 2, 1 << 19, 0, 0.0, filt, "avg", [synth.NAMESPACE], step=10000)
+    assert res.stats["exact_sum"] == (1 if exact else 0)
+    res = _synth_case(engine, 2, 1 << 20, 0, 0.0, synth.leaf(synth.NAME, "eq", "metric_07"), "sum", [synth.CONTAINER],
+                      step=3600000, highcard_n=2_000_000, hour=0)
+    assert res.stats["exact_sum"] == (1 if exact else 0) and res.stats["global_cells"] == 1
+    res = _synth_case(engine, 2, 1 << 19, 1, 0.0, filt, "sum", [synth.SERVICE])
+    assert res.stats["exact_sum"] == 0   # real values
+
+
 def test_full_size_properties(engine):
     """At a BASELINE-sized segment (2^24 rows): counts are exact, every row lands in one bucket, and the
     per-name counts over all buckets add up to the rows of the segment (no row lost or double counted)."""
