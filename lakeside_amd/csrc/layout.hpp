@@ -206,8 +206,11 @@ struct QParams {
 // their occupancy), at most LEAN_DIR_MAXSPAN buckets
 constexpr uint32_t LEAN_DIR_WORDS0 = 1536;
 constexpr uint32_t LEAN_DIR_WORDS1 = 1024;
+// two late columns (C3's shape: a 4-wave kernel, 4 workgroups per CU): 18 KB, one bucket of a 2,000-group space at
+// one plane (MIN / MAX) -- its cells otherwise overflow the 256-slot LDS hash table into device atomics
+constexpr uint32_t LEAN_DIR_WORDS2 = 2304;
 constexpr uint32_t LEAN_DIR_MAXSPAN = 8;
-constexpr uint32_t lean_dir_words(uint32_t nl) { return nl == 0 ? LEAN_DIR_WORDS0 : LEAN_DIR_WORDS1; }
+constexpr uint32_t lean_dir_words(uint32_t nl) { return nl == 0 ? LEAN_DIR_WORDS0 : (nl == 1 ? LEAN_DIR_WORDS1 : LEAN_DIR_WORDS2); }
 
 enum Flag : uint32_t {
   FLAG_METRICS_UNALIGNED = 1u, FLAG_CELL_RANGE = 2u, FLAG_HASH_FULL = 4u, FLAG_SKETCH_RANGE = 8u,

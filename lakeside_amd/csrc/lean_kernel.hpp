@@ -86,6 +86,9 @@ template <int NL>
 struct LeanLds {
   static constexpr int NLA = NL > 0 ? NL : 1;
   static constexpr uint32_t RW = lean_dir_words(NL);
+  // per-wave list ring (a power of two >= LEAN_TRIP): half size with two late columns, whose direct table is larger
+  static constexpr uint32_t LIST = NL >= 2 ? LEAN_LIST / 2 : LEAN_LIST;
+  static_assert((LIST & (LIST - 1u)) == 0u && LEAN_TRIP <= LIST, "LeanLds::LIST");
   LeanRun runs[RUN_CAP];
   uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
   alignas(4) uint8_t ctab[LEAN_CHUNKS];   // flattened chunk -> run (written 4 entries at a time)
@@ -103,7 +106,7 @@ struct LeanLds {
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
-  uint32_t wlist[NL > 0 ? BLOCK / 64 : 1][NL > 0 ? LEAN_LIST : 1];   // late columns: each wave's passing rows
+  uint32_t wlist[NL > 0 ? BLOCK / 64 : 1][NL > 0 ? LIST : 1];   // late columns: each wave's passing rows
 };
 
 // The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
@@ -675,7 +678,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     for (int u = 0; u < LEAN_ROWS; u++) {
       const uint32_t i = uint32_t(lane) + 64u * uint32_t(u);
       aa[u] = i < n;
-      const uint32_t x = aa[u] ? wl[(lhead + i) & (LEAN_LIST - 1u)] : 0u;
+      const uint32_t x = aa[u] ? wl[(lhead + i) & (LT::LIST - 1u)] : 0u;
       rr[u] = x & 0xffffu;
       dd[u] = ELIST ? (x >> 16) : (npass > 1 ? (L.lut[x >> 16] & DIM_MASK) * stride : dim_u);
     }
@@ -1037,7 +1040,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         const uint32_t wtotal = uni(uint32_t(__shfl(int(inc), 63)));
         const uint32_t pos0 = inc - cnt;
         for (uint32_t done = 0; done < wtotal;) {   // uniform
-          const uint32_t take = min(LEAN_LIST - (ltail - lhead), wtotal - done);
+          const uint32_t take = min(LT::LIST - (ltail - lhead), wtotal - done);
           unsigned long long f = fm;
           uint32_t pos = pos0;
           while (f) {
@@ -1055,7 +1058,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
                                               : sp.dim_null * sp.dim_stride;
                 }
               }
-              wl[(ltail + pos - done) & (LEAN_LIST - 1u)] = (rbase + e) | (hi16 << 16);
+              wl[(ltail + pos - done) & (LT::LIST - 1u)] = (rbase + e) | (hi16 << 16);
             }
             pos++;
           }

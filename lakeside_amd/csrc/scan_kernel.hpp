@@ -101,9 +101,19 @@ __device__ __forceinline__ void lds_merge(LT& L, const QParams& P, const Acc& a)
         else atomicAdd(&L.hval[h], (unsigned long long)a.rows);
         return;
       } else {
-        atomicAdd(&L.hrows[h], a.rows);
+        // lean tables whose rows / cnt the global table never accumulates (LEAN_NO_ROWS, LEAN_SUM_EXISTS; fixup_table
+        // restores them): the LDS cell's rows / cnt only mark it occupied -- set once by the inserting lane, no atomics
+        const bool marks = (P.lean & (LEAN_NO_ROWS | LEAN_SUM_EXISTS)) != 0u;
+        if (marks) {
+          if (prev == EMPTY) {
+            L.hrows[h] = 1u;
+            L.hcnt[h] = 1u;
+          }
+        } else {
+          atomicAdd(&L.hrows[h], a.rows);
+        }
         if (a.cnt) {
-          atomicAdd(&L.hcnt[h], a.cnt);
+          if (!marks) atomicAdd(&L.hcnt[h], a.cnt);
           if (AGG == AGG_SUM) {
             if (P.exact_sum) {   // exact adds: nothing to compensate
               __hip_atomic_fetch_add(&L.hhi[h], a.hi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
