@@ -43,6 +43,14 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #ifndef LK_LEAN_WAVES1
 #define LK_LEAN_WAVES1 5
 #endif
+// one late column with a value gather (C4 / C5: SUM / MIN / MAX): 4 waves per SIMD and 3 chunk loads in flight measured
+// faster than 5 waves with one (C4 1.59 -> 1.47 ms); COUNT(*) (tag queries, no gather) keeps 5 waves (A/B: -DLK_LEAN_WAVES1V)
+#ifndef LK_LEAN_WAVES1V
+#define LK_LEAN_WAVES1V 4
+#endif
+#ifndef LK_LEAN_PF1V
+#define LK_LEAN_PF1V 3
+#endif
 // chunk loads in flight ahead of the round, by late-column count (A/B: -DLK_LEAN_PF0 / 1 / 2); the 5-wave shapes
 // (NL <= 1, 96 VGPRs) keep their register budget, the 4-wave NL = 2 shape has room for a deeper ring
 #ifndef LK_LEAN_PF0
@@ -55,7 +63,7 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #define LK_LEAN_PF2 3
 #endif
 // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES1 / -DLK_LEAN_WAVES2)
-#define LEAN_WAVES(NL) ((NL) <= 1 ? LK_LEAN_WAVES1 : LK_LEAN_WAVES2)
+#define LEAN_WAVES(NL, AGG) ((NL) == 0 ? LK_LEAN_WAVES1 : (NL) == 1 ? ((AGG) == AGG_COUNT ? LK_LEAN_WAVES1 : LK_LEAN_WAVES1V) : LK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 // the per-wave list is a ring indexed with & (LEAN_LIST - 1) and drained LEAN_TRIP rows at a time
@@ -170,7 +178,7 @@ __device__ __forceinline__ void lean_rep(uint32_t v, uint32_t& w0, uint32_t& w1,
 // EARLY (NL > 0, a late filter leaf: P.late_chunk): tiles that allow it decode the late columns per chunk (early_late
 // below); its own kernel, built for 4 waves per SIMD, so the other shapes keep their occupancy.
 template <int AGG, bool HASH, int NL, bool EARLY = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4 : LEAN_WAVES(NL)))) void scan_lean(QParams P) {
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4 : LEAN_WAVES(NL, AGG)))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
   __shared__ LT L;
   const int tid = threadIdx.x;
@@ -711,7 +719,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     // The packed codes of the next PF rounds are in flight while a round runs (a register ring; loads return in issue
     // order, so a round waits only for its own chunk): a round's own work is far shorter than a memory round trip, and
     // one load per lane in flight would leave the tile's stream latency-bound (PF = 0: loaded in the round itself).
-    constexpr int PF = NL == 0 ? LK_LEAN_PF0 : (NL == 1 ? LK_LEAN_PF1 : LK_LEAN_PF2);
+    constexpr int PF = NL == 0 ? LK_LEAN_PF0 : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : LK_LEAN_PF1V) : LK_LEAN_PF2);
     auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
       const bool lv = qq < total;
       const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];

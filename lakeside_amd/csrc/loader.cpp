@@ -732,11 +732,16 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
   auto intern_column = [&](size_t ci, int t) {
     HostCol& col = S->cols[ci];
     std::vector<std::string_view> sv;
+    size_t nsv = 0;
+    for (size_t rg = 0; rg < nrg; rg++) nsv += chunks[ci * nrg + rg].dict.size();
+    sv.reserve(nsv);
     for (size_t rg = 0; rg < nrg; rg++) sv.insert(sv.end(), chunks[ci * nrg + rg].dict.begin(), chunks[ci * nrg + rg].dict.end());
-    col.remap.assign(sv.size(), 0);
+    col.remap.resize(sv.size());
+    if (t > 1) mark("  views");
     GlobalDict& gd = dict(col.name);
     std::lock_guard<std::mutex> g(gd.mu);
     gd.intern_all(sv, col.remap.data(), t);
+    if (t > 1) mark("  interned");
   };
   mark("layout");
   std::vector<char> big(nc, 0);
