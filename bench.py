@@ -70,6 +70,11 @@ QUERIES = {
     "gt": dict(filter={"op": "and", "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
                        "q2": {"k": "_cardinalhq.value", "v": ["1.5"], "op": "gt", "dataType": "number"}},
                agg="sum", group_bys=[], desc=":and(:eq _cardinalhq.name=metric_07, :gt _cardinalhq.value 1.5) :sum, step 1m"),
+    # C2's filter with COUNT: name codes only (no value column read for a NULL-free value column; zone-map buckets),
+    # the single-column scan_lean's filter + accumulate cost on its own (beside the tag query's one late column)
+    "count": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                          "computed": False, "dataType": "string"}, agg="count", group_bys=[],
+                  desc=":eq _cardinalhq.name=metric_07 :count, step 1m"),
     # every row passes: reads every timestamp/value (calibrates the PMC byte counters against a known count)
     "dense": dict(filter={"k": "_cardinalhq.name", "v": [f"metric_{i:02d}" for i in range(16)], "op": "in",
                           "extracted": False, "computed": False, "dataType": "string"}, agg="sum", group_bys=[],

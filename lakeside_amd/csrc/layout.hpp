@@ -173,7 +173,7 @@ struct QParams {
   uint32_t ablate;                  // diagnostics only (env LK_ABLATE): 1 skip phase 2, 2 skip tag decode,
                                     // 4 no global-table atomics; scan_lean: 0x100..0x800 plan-byte categories left
                                     // out, 0x10000 no row listed, 0x20000 listed rows dropped unprocessed, 0x40000
-                                    // listed rows loaded but not accumulated
+                                    // listed rows loaded but not accumulated, 0x80000 the tile prologue alone
   unsigned long long* stamps;       // diagnostics only (env LK_STAMPS): per block s_memtime phase totals
   // Plan bytes (the roofline numerator): bytes the late-materialized plan must read from HBM, counted
   // by the kernel: tile metadata + staged runs + dictionary lookups, every fully decoded stream of a tile, and the

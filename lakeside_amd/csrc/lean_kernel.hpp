@@ -400,6 +400,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   }
   __syncthreads();
 
+  if (P.ablate & 0x80000u) return;   // diagnostics only: the tile prologue alone (uniform)
+
   // ---- per-row state ----
   const uint32_t vb0 = tc0->vbase, vb1 = tc1->vbase;
   const __amdgpu_buffer_rsrc_t rs0 = make_rsrc(Sp->base + tc0->vals, tc0->vals_len);
