@@ -371,7 +371,7 @@ def main():
         sgm.free()
 
     # HBM traffic of the scan kernel(s) per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same bench
-    # command (scripts/gpu_bench_prof.sh -> scripts/pmc_summary.py; separate runs, as counters must be collected
+    # command (scripts/gpu_bench_prof.sh -> scripts/pmc_traffic.py; separate runs, as counters must be collected
     # alone), committed under profiles/ -- read here only when it profiled this query at this size.
     traffic, traffic_src = None, None
     pmc_file = None
