@@ -1428,6 +1428,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
                  !getenv("LK_NO_EXACT_SUM")) ? 1u : 0u;
   // a group space far beyond scan_lean's LDS hash table (1M+ cells): register cells go straight to the global table
   P.global_cells = (uint64_t(ngroups) * nbuckets >= (1ull << 20) && !getenv("LK_LDS_CELLS")) ? 1u : 0u;
+  P.split_ok = getenv("LK_NO_SPLIT") ? 0u : 1u;   // env: A/B only
   if (vleaf && !qsegs.empty()) {   // scan_lean tests the value leaves of every row its string conjuncts pass
     P.nvl = uint32_t(nleaves.size());
     P.vtab = vtab;

@@ -55,10 +55,13 @@ struct TileDesc {           // 32 B
   uint32_t rg;              // row group
   uint32_t row0;            // first row (within the row group)
   uint32_t nrows;
-  uint32_t pad;
+  uint32_t pad;             // TILE_TS_SORTED
   int64_t ts_min;           // zone map of the timestamp column over the tile (INT64_MAX/MIN if no value)
   int64_t ts_max;
 };
+
+// TileDesc::pad bit: the tile's timestamps (PLAIN INT64, no NULL) never decrease from row to row
+constexpr uint32_t TILE_TS_SORTED = 1u;
 
 struct TileCol {            // 64 B: everything the kernel needs about one column over one tile
   uint64_t vals;            // byte offset (segment base) of the page's value stream
@@ -195,6 +198,8 @@ struct QParams {
   uint32_t exact_sum;
   // group spaces far beyond the tile's LDS hash table (C5's 10M container ids): cells go straight to the global table
   uint32_t global_cells;
+  // scan_lean split tiles (TILE_TS_SORTED tiles spanning a few buckets: rows bucketed by index, no timestamp gather)
+  uint32_t split_ok;
   // Numeric comparison leaves on the value column (`value > 1.5`, BaseExpr.scala:488-498) in the fused kernel: a row
   // whose string conjuncts pass is kept iff vtab bit (its leaves' outcomes, bit k = leaf k) is set -- the numeric
   // conjuncts' value.  scan_lean tiles hold no NULL value, so no leaf is UNKNOWN there.

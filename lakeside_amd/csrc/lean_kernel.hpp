@@ -29,6 +29,7 @@ constexpr int LEAN_H = HCAP / 2;                                 // LDS hash cel
 constexpr uint32_t LEAN_CHUNKS = (TILE_ROWS / 16 + RUN_CAP + 1 + 7) & ~7u;   // chunks of a tile, upper bound (x4 B writes)
 constexpr uint32_t LEAN_LINES = (TILE_ROWS * 8 / 128 + 2 + 31) / 32;   // plan bytes: line bitmap words
 constexpr uint32_t LEAN_LLINES = (TILE_ROWS * 4 / 128 + 2 + 31) / 32;  // plan bytes: late stream lines (bw <= 32)
+constexpr uint32_t LEAN_SPLIT_MAX = 4;   // split tiles: class boundaries (the tile's bucket span + 1) at most
 
 #ifndef LK_LEAN_LIST
 #define LK_LEAN_LIST 512
@@ -55,6 +56,9 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 // (NL <= 1, 96 VGPRs) keep their register budget, the 4-wave NL = 2 shape has room for a deeper ring
 #ifndef LK_LEAN_PF0
 #define LK_LEAN_PF0 0
+#endif
+#ifndef LK_LEAN_PF0C
+#define LK_LEAN_PF0C 2   // NL = 0 COUNT (no value gather): 0.857 -> 0.754 ms on `count` with 2 rounds in flight
 #endif
 #ifndef LK_LEAN_PF1
 #define LK_LEAN_PF1 1
@@ -108,6 +112,7 @@ struct LeanLds {
     unsigned long long dir[RW];
   } agg;
   uint32_t lines_t[LEAN_LINES], lines_v[LEAN_LINES];   // plan bytes only: 128-B lines gathered
+  uint32_t scnt[LEAN_SPLIT_MAX], sbnd[LEAN_SPLIT_MAX];  // split tiles: samples below each class, boundary rows
   // late columns (NL > 0): value runs (+ sentinel), run-block tables, lookup values, the late conjuncts' table
   LRun lruns[NLA][NL > 0 ? RUN_CAP + 1 : 1];
   alignas(4) uint8_t lrblk[NLA][NL > 0 ? TILE_ROWS / 64 + 8 : 1];
@@ -260,6 +265,10 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
       const uint32_t g = remap[tid];
       L.lut[tid] = tab ? tab[g] : g;
     }
+  }
+  if (tid < int(LEAN_SPLIT_MAX)) {
+    L.scnt[tid] = 0u;
+    L.sbnd[tid] = ~0u;
   }
   if (count_plan) {
     for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) L.lines_t[i] = L.lines_v[i] = 0u;
@@ -428,6 +437,86 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
   }
   const bool one_bucket = tile_b >= 0;
   const uint32_t step32 = uint32_t(P.step);
+  // Split tiles (TILE_TS_SORTED: the tile's timestamps never decrease; not metrics, whose rows must be checked on the
+  // step grid): a tile the zone map cannot pin to one bucket has its rows' classes -- 0 before the window, 1 .. span
+  // its buckets split_bl .. split_bl + span - 1, span + 1 after the window, non-decreasing with the row -- split by
+  // boundary rows found with two rounds of timestamp loads (256 samples, then the sample gap holding each boundary),
+  // so a passing row's bucket follows from its row index and no timestamp is gathered per row.
+  uint32_t nsb = 0;        // boundaries (span + 1; 0: not a split tile) -- uniform
+  int64_t split_bl = 0;
+  uint32_t sb[LEAN_SPLIT_MAX];
+#pragma unroll
+  for (uint32_t k = 0; k < LEAN_SPLIT_MAX; k++) sb[k] = 0u;
+  // (not built into the COUNT(*) late-column shape: tag queries have one bucket, and its 5-wave budget has no room)
+  constexpr bool SPLIT = !(AGG == AGG_COUNT && NL >= 1);
+  if (SPLIT && !one_bucket && !P.metrics && (tdp->pad & TILE_TS_SORTED) && P.split_ok) {
+    auto bucket_of = [&](int64_t ts) __attribute__((always_inline)) -> int64_t {
+      return ((ts - ts % P.step) - P.bucket_base) / P.step;
+    };
+    const int64_t lo_ts = tdp->ts_min > win_lo ? tdp->ts_min : win_lo;
+    const int64_t hi_ts = tdp->ts_max < win_hi - 1 ? tdp->ts_max : win_hi - 1;
+    const int64_t bl = bucket_of(lo_ts), bh = bucket_of(hi_ts);
+    if (lo_ts <= hi_ts && bl >= 0 && bh < int64_t(P.nbuckets) && bh - bl + 2 <= int64_t(LEAN_SPLIT_MAX)) {
+      nsb = uint32_t(bh - bl + 2);
+      split_bl = bl;
+    }
+  }
+  if (nsb) {   // uniform
+    const __amdgpu_buffer_rsrc_t rst = make_rsrc(Sp->base + tc0->vals, tc0->vals_len);
+    const uint32_t vbt = tc0->vbase;
+    auto cls_of = [&](int64_t ts) __attribute__((always_inline)) -> uint32_t {
+      if (ts < win_lo) return 0u;
+      if (ts >= win_hi) return nsb;
+      return uint32_t(((ts - ts % P.step) - P.bucket_base) / P.step - split_bl) + 1u;
+    };
+    auto sample = [&](uint32_t t) __attribute__((always_inline)) -> uint32_t {   // row of sample t (t = 256: nrows)
+      return uint32_t((uint64_t(t) * nrows) >> 8);
+    };
+    {   // round 1: samples; per class c, the samples below it
+      const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rst, (vbt + sample(uint32_t(tid))) * 8u, 0, 0);
+      const uint32_t c = cls_of(int64_t(((uint64_t)x.y << 32) | x.x));
+#pragma unroll
+      for (uint32_t k = 0; k < LEAN_SPLIT_MAX; k++) {
+        if (k >= nsb) break;
+        const unsigned long long bl = __ballot(c < k + 1u);
+        if (lane == 0 && bl) atomicAdd(&L.scnt[k], uint32_t(__popcll(bl)));
+      }
+    }
+    __syncthreads();
+    // round 2: boundary k + 1 lies in the sample gap (sample(n - 1), sample(n)] (n samples below it; none: row 0)
+#pragma unroll
+    for (uint32_t k = 0; k < LEAN_SPLIT_MAX; k++) {
+      if (k >= nsb) break;
+      const uint32_t n = L.scnt[k];
+      if (n == 0u) continue;   // uniform
+      const uint32_t lo = sample(n - 1u) + 1u, hi = sample(n);
+      const uint32_t r = lo + uint32_t(tid);
+      bool f = false;
+      if (r < hi) {
+        const v2u x = __builtin_amdgcn_raw_buffer_load_b64(rst, (vbt + r) * 8u, 0, 0);
+        f = cls_of(int64_t(((uint64_t)x.y << 32) | x.x)) >= k + 1u;
+      }
+      const unsigned long long bl = __ballot(f);
+      if (lane == 0 && bl) atomicMin(&L.sbnd[k], r - uint32_t(lane) + uint32_t(__builtin_ctzll(bl)));
+    }
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < LEAN_SPLIT_MAX; k++) {
+      const uint32_t n = L.scnt[k];
+      const uint32_t hi = sample(n);   // the first sample at or above the class (n = 256: nrows, no such row)
+      const uint32_t b = n == 0u ? 0u : (L.sbnd[k] < hi ? L.sbnd[k] : hi);
+      sb[k] = k < nsb ? uint32_t(__builtin_amdgcn_readfirstlane(int(b))) : 0xffffffffu;
+    }
+    if (count_plan && tid == 0) pbytes += 128u * (256u / 16u + nsb * 2u);   // sample and gap lines (approx.)
+  }
+  const bool split = nsb != 0u;
+  const bool ts_gather = !one_bucket && !split;   // rows gather their timestamp (uniform)
+  auto split_class = [&](uint32_t r) __attribute__((always_inline)) -> uint32_t {
+    uint32_t c = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < LEAN_SPLIT_MAX; k++) c += r >= sb[k] ? 1u : 0u;
+    return c;
+  };
   // dense-block test only where a quarter or more of the chunk dictionary's codes pass (uniform; C2's 1 of 16 skips it)
   const bool dense_codes = NL == 0 && 4u * npass >= dict_n;
   // dense blocks over several passing codes: rows straight into the direct table (`row`'s `direct`)
@@ -486,7 +575,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     }
   };
   // one passing row: bucket (BaseExpr.scala:159-165 window, 163-165 / 376-394 bucket), cell, register cell
-  auto row = [&](int64_t ts, double v, uint32_t dim) __attribute__((always_inline)) {
+  auto row = [&](int64_t ts, double v, uint32_t dim, uint32_t r) __attribute__((always_inline)) {
     if (P.nvl) {   // numeric leaves on the value column (uniform)
       uint32_t bits = 0;
       // read through the kernarg segment pointer (P is the kernel's only argument): a runtime index into the by-value
@@ -503,7 +592,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     }
     bool ok = true;
     int64_t b = tile_b;
-    if (!one_bucket) {
+    if (split) {   // uniform: the row's class from its index
+      const uint32_t c = split_class(r);
+      if (c == 0u || c >= nsb) return;   // outside the window
+      b = split_bl + int64_t(c) - 1;
+    } else if (!one_bucket) {
       ok = ts >= win_lo && ts < win_hi;
       if (P.fast_div) {
         const uint32_t d = uint32_t(ts - P.bucket_base);
@@ -566,7 +659,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     auto gather = [&]() __attribute__((always_inline)) {   // timestamps / values of the passing rows
 #pragma unroll
       for (int u = 0; u < N; u++) {
-        if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, p[u] ? (vb0 + rr[u]) * 8u : OOB, 0, 0);
+        if (ts_gather) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, p[u] ? (vb0 + rr[u]) * 8u : OOB, 0, 0);
         if (AGG != AGG_COUNT || P.nvl) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, p[u] ? (vb1 + rr[u]) * 8u : OOB, 0, 0);
       }
     };
@@ -658,7 +751,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
 #pragma unroll
       for (int u = 0; u < N; u++) {
         if (!ld[u]) continue;
-        if (!one_bucket) mark(L.lines_t, (vb0 + rr[u]) * 8u, line_t0);
+        if (ts_gather) mark(L.lines_t, (vb0 + rr[u]) * 8u, line_t0);
         if (AGG != AGG_COUNT || P.nvl) mark(L.lines_v, (vb1 + rr[u]) * 8u, line_v0);
       }
     }
@@ -669,7 +762,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
 #pragma unroll
     for (int u = 0; u < N; u++)
       if (p[u])
-        row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x)), dd[u]);
+        row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), __longlong_as_double((long long)(((uint64_t)xx[u].y << 32) | xx[u].x)), dd[u], rr[u]);
   };
   // Late columns: each wave's passing rows wait in its LDS list (a ring of LEAN_LIST entries, tile row | code << 16)
   // until a full trip of LEAN_TRIP rows -- LEAN_ROWS per lane, every lane busy, all their late-column loads and then
@@ -721,7 +814,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     // The packed codes of the next PF rounds are in flight while a round runs (a register ring; loads return in issue
     // order, so a round waits only for its own chunk): a round's own work is far shorter than a memory round trip, and
     // one load per lane in flight would leave the tile's stream latency-bound (PF = 0: loaded in the round itself).
-    constexpr int PF = NL == 0 ? LK_LEAN_PF0 : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : LK_LEAN_PF1V) : LK_LEAN_PF2);
+    constexpr int PF = NL == 0 ? (AGG == AGG_COUNT ? LK_LEAN_PF0C : LK_LEAN_PF0)
+                               : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : LK_LEAN_PF1V) : LK_LEAN_PF2);
     auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
       const bool lv = qq < total;
       const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];
@@ -880,7 +974,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
               const uint32_t r = rb0 + 64u * uint32_t(j0 + u) + uint32_t(lane);
               tt[u] = v2u{0u, 0u};
               xx[u] = v2u{0u, 0u};
-              if (!one_bucket) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, pp[u] ? (vb0 + r) * 8u : OOB, 0, 0);
+              if (ts_gather) tt[u] = __builtin_amdgcn_raw_buffer_load_b64(rs0, pp[u] ? (vb0 + r) * 8u : OOB, 0, 0);
               if (AGG != AGG_COUNT || P.nvl) xx[u] = __builtin_amdgcn_raw_buffer_load_b64(rs1, pp[u] ? (vb1 + r) * 8u : OOB, 0, 0);
               dd[u] = dim_u;
               if (npass > 1) {   // uniform
@@ -890,7 +984,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
                 dd[u] = (L.lut[lean_code<BW>(a0, a1, a2c, e)] & DIM_MASK) * stride;
               }
               if (count_plan && pp[u]) {
-                if (!one_bucket) {
+                if (ts_gather) {
                   const uint32_t l = (((vb0 + r) * 8u) >> 7) - line_t0;
                   atomicOr(&L.lines_t[l >> 5], 1u << (l & 31u));
                 }
@@ -926,7 +1020,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
                 }
                 if (rrows_on) atomicAdd(rrows + x, 1ull);
               } else {
-                row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), v, dd[u]);
+                row((int64_t)(((uint64_t)tt[u].y << 32) | tt[u].x), v, dd[u], rb0 + 64u * uint32_t(j0 + u) + uint32_t(lane));
               }
             }
           }

@@ -550,15 +550,21 @@ void build_tiles_rg(const SegmentData& S, const std::vector<std::vector<HostPage
       }
       if (c == ts_col && p.d.kind == PAGE_PLAIN64 && !S.cols[size_t(c)].is_string) {
         const int64_t* v = reinterpret_cast<const int64_t*>(p.host_vals);   // (host_vals: 8-B PLAIN values)
-        int64_t lo = INT64_MAX, hi = INT64_MIN;
+        int64_t lo = INT64_MAX, hi = INT64_MIN, prev = INT64_MIN;
+        bool sorted = true;
         for (uint32_t i = va; i < ve; i++) {
           int64_t x;
           memcpy(&x, v + i, 8);
           lo = std::min(lo, x);
           hi = std::max(hi, x);
+          sorted &= x >= prev;
+          prev = x;
         }
         t.ts_min = lo;
         t.ts_max = hi;
+        // every row has a timestamp and they never decrease: a query's bucket boundaries inside the tile can be found
+        // by searching the timestamps (scan_lean's split tiles)
+        if (sorted && ve - va == e - a && !p.d.has_nulls) t.pad |= TILE_TS_SORTED;
       } else if (c == ts_col && p.d.kind == PAGE_PLAIN32 && S.cols[size_t(c)].ptype == pq::INT32) {
         for (uint32_t v = va; v < ve; v++) {   // INT32 timestamps (BIGINT in a union_by_name glob)
           int32_t x;

@@ -212,6 +212,22 @@ def test_zone_map_bucket_paths(engine):
     _synth_case(engine, 1, 1 << 21, 1, 0.0, filt, "max", [], step=7000)
 
 
+@pytest.mark.parametrize("split", [True, False], ids=["split", "no_split"])
+def test_split_tiles_sorted_timestamps(engine, split, monkeypatch):
+    """Tiles whose timestamps never decrease (TILE_TS_SORTED) and span 2-3 buckets take the split path: bucket and
+    window boundaries found by searching the timestamps, rows bucketed by index with no timestamp gather.  Steps
+    putting 1-4 boundaries inside a 32K-row tile (~56 s of data), a window cutting tiles at both ends, and a 7 s step
+    whose tiles span too many buckets (per-row timestamps again) -- each against the oracle, with and without it."""
+    from lakeside_amd import synth
+    if not split:
+        monkeypatch.setenv("LK_NO_SPLIT", "1")
+    filt = synth.leaf(synth.NAME, "in", "metric_03", "metric_11")
+    _synth_case(engine, 2, 1 << 21, 1, 0.0, filt, "sum", [synth.NAME], step=20000)
+    _synth_case(engine, 1, 1 << 21, 0, 0.0, filt, "count", [], step=30000, window=(7 * 60000 + 123, 11 * 60000 - 17))
+    _synth_case(engine, 1, 1 << 21, 1, 0.0, filt, "max", [synth.SERVICE], step=60000, window=(45_000, 1_001))
+    _synth_case(engine, 1, 1 << 21, 1, 0.0, filt, "min", [], step=7000)
+
+
 def test_window_cuts_tiles(engine):
     """A glob window narrower than the data: tiles crossing either edge filter rows by timestamp, tiles outside
     are skipped by their zone map."""

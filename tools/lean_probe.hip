@@ -8,3 +8,6 @@ template __global__ void scan_lean<AGG_SUM, false, 1, false>(QParams);
 template __global__ void scan_lean<AGG_MAX, false, 2, false>(QParams);
 template __global__ void scan_lean<AGG_COUNT, false, 1, false>(QParams);
 }  // namespace lk
+namespace lk {
+template __global__ void scan_lean<AGG_COUNT, false, 0, false>(QParams);
+}  // namespace lk
