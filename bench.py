@@ -418,8 +418,12 @@ def main():
                                        "shard at N > 1. `value` "
                                        "counts every row of the workload as scanned, including rows of tiles whose "
                                        "load-time zone map (timestamp min/max per tile) pins them to a single "
-                                       "bucket: their timestamps are never read, and value lines with no passing "
-                                       "row are skipped, so plan bytes < SURVEY's algorithmic bytes",
+                                       "bucket and of split tiles (timestamps never decreasing: the bucket "
+                                       "boundary rows are found by searching them, r05): their timestamps are "
+                                       "never gathered per row, and value lines with no passing row are skipped, "
+                                       "so plan bytes < SURVEY's algorithmic bytes; a plan change that reads fewer "
+                                       "bytes lowers `frac` at equal time -- compare `value` and scan time across "
+                                       "rounds",
                          "plan_bytes_per_launch": pbytes,
                          "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_gbs": alg_gbs,
                          "traffic_source": traffic_src,

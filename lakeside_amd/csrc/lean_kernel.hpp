@@ -44,6 +44,11 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #ifndef LK_LEAN_WAVES1
 #define LK_LEAN_WAVES1 5
 #endif
+// NL = 0 (C2): passing rows through the wave's LDS list too (A/B: -DLK_LEAN_LIST0=1), instead of each lane looping
+// over its own chunk's passing rows two at a time
+#ifndef LK_LEAN_LIST0
+#define LK_LEAN_LIST0 0
+#endif
 // one late column with a value gather (C4 / C5: SUM / MIN / MAX): 4 waves per SIMD and 3 chunk loads in flight measured
 // faster than 5 waves with one (C4 1.59 -> 1.47 ms); COUNT(*) (tag queries, no gather) keeps 5 waves (A/B: -DLK_LEAN_WAVES1V)
 #ifndef LK_LEAN_WAVES1V
@@ -119,7 +124,7 @@ struct LeanLds {
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
-  uint32_t wlist[NL > 0 ? BLOCK / 64 : 1][NL > 0 ? LIST : 1];   // late columns: each wave's passing rows
+  uint32_t wlist[NL > 0 || LK_LEAN_LIST0 ? BLOCK / 64 : 1][NL > 0 || LK_LEAN_LIST0 ? LIST : 1];   // each wave's passing rows
 };
 
 // The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
@@ -1027,7 +1032,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
           m = 0;
         }
       }
-      if constexpr (NL == 0) {
+      if constexpr (NL == 0 && !LK_LEAN_LIST0) {
         // passing rows: two per trip (their loads in flight together)
         while (m) {
           const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
@@ -1174,7 +1179,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         }
       }
     }
-    if constexpr (NL > 0) {
+    if constexpr (NL > 0 || LK_LEAN_LIST0) {
       while (ltail != lhead) list_trip(ec, min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
       wave_sync();
     }

@@ -60,9 +60,13 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
   };
   constexpr size_t K = IdMap::kShards;
   const size_t B = std::min<size_t>(size_t(threads) * 8, (n + 4095) / 4096), bs = (n + B - 1) / B;
-  std::vector<uint64_t> h(n);
+  if (sc_hash.size() < n) sc_hash.resize(n);
+  if (sc_first.size() < n) sc_first.resize(n);
+  uint64_t* const h = sc_hash.data();
+  uint32_t* const first = sc_first.data();   // unknown positions: the first position of the same value
   parallel_for(B, threads, [&](size_t b) {
     const size_t lo = b * bs, hi = std::min(n, (b + 1) * bs);
+    std::fill(first + lo, first + hi, UINT32_MAX);
     constexpr size_t D = 16;   // lookups in flight: slot lines prefetched D values ahead (each lookup is a cache miss)
     for (size_t i = lo; i < std::min(hi, lo + D); i++) {
       h[i] = IdMap::hash(v[i]);
@@ -83,7 +87,6 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
       if (out[i] == UINT32_MAX) lists[b * K + IdMap::shard_of(h[i])].push_back(uint32_t(i));
   });
   mark("lists");
-  std::vector<uint32_t> first(n, UINT32_MAX);   // unknown positions: the first position of the same value
   parallel_for(K, threads, [&](size_t k) {
     // open addressing over this shard's positions (slot: hash tag | position), walked in position order
     size_t m = 0;
@@ -737,16 +740,15 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
   // parallel_for, so a load never runs more than `threads` threads.
   auto intern_column = [&](size_t ci, int t) {
     HostCol& col = S->cols[ci];
-    std::vector<std::string_view> sv;
-    size_t nsv = 0;
-    for (size_t rg = 0; rg < nrg; rg++) nsv += chunks[ci * nrg + rg].dict.size();
-    sv.reserve(nsv);
+    GlobalDict& gd = dict(col.name);
+    std::lock_guard<std::mutex> g(gd.mu);
+    std::vector<std::string_view>& sv = gd.sc_views;   // (reused across loads)
+    sv.clear();
     for (size_t rg = 0; rg < nrg; rg++) sv.insert(sv.end(), chunks[ci * nrg + rg].dict.begin(), chunks[ci * nrg + rg].dict.end());
     col.remap.resize(sv.size());
     if (t > 1) mark("  views");
-    GlobalDict& gd = dict(col.name);
-    std::lock_guard<std::mutex> g(gd.mu);
     gd.intern_all(sv, col.remap.data(), t);
+    if (t <= 1 || sv.size() < (size_t(1) << 16)) std::vector<std::string_view>().swap(sv);   // small: not kept
     if (t > 1) mark("  interned");
   };
   mark("layout");
