@@ -44,10 +44,16 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #ifndef LK_LEAN_WAVES1
 #define LK_LEAN_WAVES1 5
 #endif
-// NL = 0 (C2): passing rows through the wave's LDS list too (A/B: -DLK_LEAN_LIST0=1), instead of each lane looping
-// over its own chunk's passing rows two at a time
+// NL = 0 with a value gather (C2): passing rows through the wave's LDS list too -- a trip of 128 rows with every lane
+// busy per round trip -- instead of each lane looping over its own chunk's passing rows two at a time (a round then
+// lasts as many round trips as its busiest lane); built for 4 waves per SIMD with 2 chunk rounds in flight: C2 1.27 ->
+// 1.08 ms, C2 at a 10 s step 1.40 -> 1.18 ms (A/B: -DLK_LEAN_LIST0=0).  Dense-code tiles (a quarter or more of the
+// codes pass: the dense query) keep the per-lane loop and its row-major dense blocks.
 #ifndef LK_LEAN_LIST0
-#define LK_LEAN_LIST0 0
+#define LK_LEAN_LIST0 1
+#endif
+#ifndef LK_LEAN_WAVES0V
+#define LK_LEAN_WAVES0V 4
 #endif
 // one late column with a value gather (C4 / C5: SUM / MIN / MAX): 4 waves per SIMD and 3 chunk loads in flight measured
 // faster than 5 waves with one (C4 1.59 -> 1.47 ms); COUNT(*) (tag queries, no gather) keeps 5 waves (A/B: -DLK_LEAN_WAVES1V)
@@ -60,7 +66,7 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 // chunk loads in flight ahead of the round, by late-column count (A/B: -DLK_LEAN_PF0 / 1 / 2); the 5-wave shapes
 // (NL <= 1, 96 VGPRs) keep their register budget, the 4-wave NL = 2 shape has room for a deeper ring
 #ifndef LK_LEAN_PF0
-#define LK_LEAN_PF0 0
+#define LK_LEAN_PF0 (LK_LEAN_LIST0 ? 2 : 0)
 #endif
 #ifndef LK_LEAN_PF0C
 #define LK_LEAN_PF0C 2   // NL = 0 COUNT (no value gather): 0.857 -> 0.754 ms on `count` with 2 rounds in flight
@@ -72,7 +78,8 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #define LK_LEAN_PF2 3
 #endif
 // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES1 / -DLK_LEAN_WAVES2)
-#define LEAN_WAVES(NL, AGG) ((NL) == 0 ? LK_LEAN_WAVES1 : (NL) == 1 ? ((AGG) == AGG_COUNT ? LK_LEAN_WAVES1 : LK_LEAN_WAVES1V) : LK_LEAN_WAVES2)
+#define LEAN_WAVES(NL, AGG) ((NL) == 0 ? ((AGG) == AGG_COUNT || !LK_LEAN_LIST0 ? LK_LEAN_WAVES1 : LK_LEAN_WAVES0V) \
+                                      : (NL) == 1 ? ((AGG) == AGG_COUNT ? LK_LEAN_WAVES1 : LK_LEAN_WAVES1V) : LK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 // the per-wave list is a ring indexed with & (LEAN_LIST - 1) and drained LEAN_TRIP rows at a time
@@ -124,7 +131,8 @@ struct LeanLds {
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
-  uint32_t wlist[NL > 0 || LK_LEAN_LIST0 ? BLOCK / 64 : 1][NL > 0 || LK_LEAN_LIST0 ? LIST : 1];   // each wave's passing rows
+  static constexpr bool LISTED = NL > 0 || LK_LEAN_LIST0;   // (NL = 0: the value-gathering shapes use it)
+  uint32_t wlist[LISTED ? BLOCK / 64 : 1][LISTED ? LIST : 1];   // each wave's passing rows
 };
 
 // The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
@@ -1032,7 +1040,8 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
           m = 0;
         }
       }
-      if constexpr (NL == 0 && !LK_LEAN_LIST0) {
+      constexpr bool LIST0 = NL == 0 && LK_LEAN_LIST0 && AGG != AGG_COUNT;
+      if (NL == 0 && (!LIST0 || dense_codes)) {   // uniform
         // passing rows: two per trip (their loads in flight together)
         while (m) {
           const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
@@ -1179,7 +1188,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
         }
       }
     }
-    if constexpr (NL > 0 || LK_LEAN_LIST0) {
+    if constexpr (NL > 0 || (LK_LEAN_LIST0 && AGG != AGG_COUNT)) {
       while (ltail != lhead) list_trip(ec, min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
       wave_sync();
     }

@@ -77,6 +77,7 @@ void GlobalDict::intern_all(const std::vector<std::string_view>& v, uint32_t* ou
         h[i + D] = IdMap::hash(v[i + D]);
         ids.prefetch(h[i + D]);
       }
+      if (i + D / 2 < hi) ids.prefetch_str(h[i + D / 2]);   // its slot arrived: the string it points at next
       out[i] = ids.find_h(v[i], h[i]);   // kNone (UINT32_MAX) when unknown
     }
   });

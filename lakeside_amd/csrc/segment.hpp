@@ -114,6 +114,14 @@ class IdMap {
     const Shard& sh = m_[shard_of(h)];
     if (!sh.slots.empty()) __builtin_prefetch(&sh.slots[size_t(h >> 6) & (sh.slots.size() - 1)]);
   }
+  // second stage (the home slot prefetched earlier): the stored string of a tag-matching home slot, which the
+  // lookup's compare reads next (short values live inside the string object)
+  void prefetch_str(uint64_t h) const {
+    const Shard& sh = m_[shard_of(h)];
+    if (sh.slots.empty()) return;
+    const uint64_t v = sh.slots[size_t(h >> 6) & (sh.slots.size() - 1)];
+    if (v && (v >> 32) == tag_of(h)) __builtin_prefetch(&(*strs_)[uint32_t(v)]);
+  }
   // id -> its value (*strs)[id] must not be in the map yet
   void emplace(uint32_t id) { emplace_h(id, hash((*strs_)[id])); }
   void emplace_h(uint32_t id, uint64_t h) {
