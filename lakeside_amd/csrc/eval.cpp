@@ -259,6 +259,48 @@ void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F) {
     }
   });
 }
+
+// Rows of a large result from its output keys' existence bits (FParams::key_bits): rows are the existing keys in key
+// order, so row r's key -- and from it the timestamp, group id and glob -- follow from the bits alone.  Pieces of 2^20
+// keys: counts, a prefix, then every piece expanded on its own thread.
+void expand_rows_from_keys(int64_t* ts, uint32_t* gid, uint32_t* glob, const unsigned long long* bits,
+                           const FParams& F, bool per_glob) {
+  const uint64_t words = (F.nkeys + 63) / 64;
+  constexpr uint64_t kPiece = uint64_t(1) << 14;   // words per piece
+  const size_t np = size_t((words + kPiece - 1) / kPiece);
+  std::vector<size_t> base(np + 1, 0);
+  const int threads = int(std::min<size_t>(np, 8));
+  parallel_for(np, threads, [&](size_t p) {
+    size_t c = 0;
+    for (uint64_t w = p * kPiece; w < std::min(words, (p + 1) * kPiece); w++) c += size_t(__builtin_popcountll(bits[w]));
+    base[p + 1] = c;
+  });
+  for (size_t p = 0; p < np; p++) base[p + 1] += base[p];
+  const uint64_t ng = F.ngroups, ns = F.nglob_slots ? F.nglob_slots : 1;
+  parallel_for(np, threads, [&](size_t p) {
+    size_t r = base[p];
+    for (uint64_t w = p * kPiece; w < std::min(words, (p + 1) * kPiece); w++) {
+      unsigned long long x = bits[w];
+      if (!x) continue;
+      const uint64_t k0 = w * 64;
+      uint64_t t0 = k0 / ng, g0 = k0 - t0 * ng;   // key = t * ngroups + g
+      while (x) {
+        const uint64_t b = uint64_t(__builtin_ctzll(x));
+        x &= x - 1;
+        uint64_t g = g0 + b, t = t0;
+        if (g >= ng) {
+          t += g / ng;
+          g %= ng;
+        }
+        const uint64_t bucket = per_glob ? t / ns : t;
+        ts[r] = F.bucket_base + int64_t(bucket) * F.step;
+        gid[r] = uint32_t(g);
+        if (glob) glob[r] = uint32_t(t % ns);
+        r++;
+      }
+    }
+  });
+}
 }  // namespace
 
 static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
@@ -1334,6 +1376,12 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // host side only (mapped): the first row of every bucket, when a large result's timestamps are expanded on the host
   const bool ts_runs_ok = nbuckets <= kTsRunsMaxBuckets && !getenv("LK_NO_TS_RUNS");
   const size_t o_bpos = reserve(ts_runs_ok ? (size_t(nbuckets) + 1) * 4 : 0);
+  // host side only (mapped): the existence bit of every output key of a large grouped result (FParams::key_bits)
+  const uint64_t okeys = per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups);
+  // opt-in (LK_KEY_ROWS=1): measured slower on C5 (eval 2.28 vs 2.13 ms) -- the host's 68 MB of row writes take
+  // longer than the 23 MB of group ids they keep off the host link
+  const bool key_rows_ok = !collapse && okeys >= kTsRunsMinKeys && getenv("LK_KEY_ROWS") && *getenv("LK_KEY_ROWS") == '1';
+  const size_t o_kbits = reserve(key_rows_ok ? size_t((okeys + 2047) / 2048) * 2048 / 8 : 0);
   // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)
   uint8_t* hbuf = nullptr;
   uint8_t* dbuf = nullptr;
@@ -2084,6 +2132,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     if (fast_done) {
       nrows_out = fast_rows;   // rows already in the result block (speculative finalize behind the scan)
     } else if (emit && F.nkeys) {
+      if (key_rows_ok && F.nkeys == okeys && !F.key_base) F.key_bits = reinterpret_cast<unsigned long long*>(hbuf + o_kbits);
       HIP_TRY(launch_finalize_count(F, d_counts, st));
       HIP_TRY(hipMemcpyAsync(&nrows_out, d_counts + nfb, 4, hipMemcpyDeviceToHost, st));
     }
@@ -2164,13 +2213,17 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     double* o_val = direct ? res->val : reinterpret_cast<double*>(ob + nk * 8);
     uint32_t* o_gid = direct ? res->gid : reinterpret_cast<uint32_t*>(ob + nk * 16);
     uint32_t* o_glob = per_glob_rows ? (direct ? res->glob : reinterpret_cast<uint32_t*>(ob + nk * 24)) : nullptr;
-    const bool ts_runs = direct && !hash_mode && ts_runs_ok && F.nkeys >= kTsRunsMinKeys;
+    // large grouped results: values only; timestamps, group ids and globs from the key bits (finalize_count's, already
+    // on the host) while the values cross the host link
+    const bool key_rows = direct && !hash_mode && F.key_bits;
+    const bool ts_runs = direct && !hash_mode && !key_rows && ts_runs_ok && F.nkeys >= kTsRunsMinKeys;
     if (ts_runs) {
       F.bucket_pos = reinterpret_cast<uint32_t*>(hbuf + o_bpos);
       HIP_TRY(launch_finalize_bucket_pos(F, d_counts, st));
       HIP_TRY(hipEventRecord(X->ev_rows, st));
     }
     if (hash_mode) HIP_TRY(launch_sparse_write(S, nocc, sws, o_ts, o_val, o_gid, o_glob, st));
+    else if (key_rows) HIP_TRY(launch_finalize_write(F, d_counts, nullptr, o_val, nullptr, nullptr, st));
     else HIP_TRY(launch_finalize_write(F, d_counts, ts_runs ? nullptr : o_ts, o_val, o_gid, o_glob, st));
     if (!direct) {
       HIP_TRY(hipMemcpyAsync(res->ts, o_ts, size_t(nrows_out) * 8, hipMemcpyDeviceToHost, st));
@@ -2182,6 +2235,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       HIP_TRY(hipEventSynchronize(X->ev_rows));
       expand_ts_runs(res->ts, nrows_out, F);
     }
+    if (key_rows) expand_rows_from_keys(res->ts, res->gid, per_glob_rows ? res->glob : nullptr, F.key_bits, F, per_glob_rows);
     HIP_TRY(hipStreamSynchronize(st));
   }
   const double copy_ms = ms_since(t_start);

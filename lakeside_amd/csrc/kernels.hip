@@ -128,7 +128,12 @@ __global__ __launch_bounds__(FB) void finalize_count(FParams F, uint32_t* block_
   const unsigned long long base = (unsigned long long)blockIdx.x * FB * FITEMS;
   for (int i = 0; i < FITEMS; i++) {
     unsigned long long key = base + (unsigned long long)i * FB + threadIdx.x;
-    if (key < F.nkeys && make_row(F, F.key_base + key).exists) n++;
+    const bool ex = key < F.nkeys && make_row(F, F.key_base + key).exists;
+    n += ex ? 1u : 0u;
+    if (F.key_bits) {   // one 64-key word per wave (keys 64-aligned: base is a multiple of FB * FITEMS)
+      const unsigned long long w = __ballot(ex);
+      if ((threadIdx.x & 63) == 0) F.key_bits[(key - (threadIdx.x & 63)) >> 6] = w;
+    }
   }
   for (int o = 32; o > 0; o >>= 1) n += __shfl_down(n, o, 64);
   if ((threadIdx.x & 63) == 0) ws[threadIdx.x >> 6] = n;
@@ -190,9 +195,9 @@ __global__ __launch_bounds__(FB) void finalize_write(FParams F, const uint32_t* 
     if (r.exists) {
       const uint32_t pos = off + wb + __popcll(m & ((1ull << lane) - 1ull));
       const unsigned long long b = F.per_glob ? key / F.ngroups / F.nglob_slots : (F.collapse ? key : key / F.ngroups);
-      if (out_ts) out_ts[pos] = F.bucket_base + (int64_t)b * F.step;   // null: expanded on the host (bucket_pos)
+      if (out_ts) out_ts[pos] = F.bucket_base + (int64_t)b * F.step;   // null: expanded on the host
       out_val[pos] = r.value;
-      out_gid[pos] = uint32_t(r.gid);
+      if (out_gid) out_gid[pos] = uint32_t(r.gid);   // null: derived on the host (key_bits)
       if (out_glob) out_glob[pos] = r.glob;   // null: merged rows (glob 0, a shared zero block on the host)
     }
     off += tot;

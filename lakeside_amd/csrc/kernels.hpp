@@ -33,6 +33,10 @@ struct FParams {
   // (rows are in bucket-major order) and finalize_write is given no timestamp column -- the host expands it (8 of the
   // 20-24 bytes per row that cross the host link)
   uint32_t* bucket_pos;
+  // large results with a group key (not collapsed): finalize_count also writes one existence bit per output key here
+  // (mapped pinned memory), from which the host derives every row's timestamp, group id and glob -- finalize_write then
+  // sends the values alone (8 of 20-24 bytes per row)
+  unsigned long long* key_bits;
 };
 
 constexpr int AGG_AVG = 4;
