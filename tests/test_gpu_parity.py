@@ -252,6 +252,16 @@ def test_c5_shape_high_cardinality_group_by(engine):
     _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
 
 
+def test_large_result_rows_from_key_bits(engine, monkeypatch):
+    """LK_KEY_ROWS=1 (opt-in): a large grouped result's rows carry only their values over the host link; timestamps,
+    group ids and globs come from finalize_count's per-key existence bits -- per glob and merged, one and 60 buckets."""
+    from lakeside_amd import synth
+    monkeypatch.setenv("LK_KEY_ROWS", "1")
+    filt = synth.leaf(synth.NAME, "eq", "metric_07")
+    _synth_case(engine, 2, 1 << 20, 0, 0.0, filt, "sum", [synth.CONTAINER], step=3600000, highcard_n=300000, hour=0)
+    _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
+
+
 @pytest.mark.parametrize("exact", [True, False], ids=["exact_sum", "compensated"])
 def test_integral_sums_exact_and_compensated(engine, exact, monkeypatch):
     """Integer values (load-time summary: every value integral, |v| <= 999): SUM adds are fire-and-forget
