@@ -117,6 +117,7 @@ struct LeanLds {
   uint32_t cb[RUN_CAP + 1];               // first flattened chunk of each run (cb[nr] = chunks of the tile)
   alignas(4) uint8_t ctab[LEAN_CHUNKS];   // flattened chunk -> run (written 4 entries at a time)
   uint32_t lut[64];                       // code -> (leaf bits << 24) | dim id
+  uint32_t etruth[(1u << (2 * TT_MAX_LEAVES)) / 32];   // the early conjuncts' truth table (staged with the lookups)
   // The tile's aggregation table: the hash table, or the direct table (the tile's buckets x ngroups cells, P.dir_planes
   // u64 planes: value (SUM: hi), SUM: lo, rows when the table keeps them)
   union {
@@ -283,6 +284,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     L.scnt[tid] = 0u;
     L.sbnd[tid] = ~0u;
   }
+  {   // staged beside the code lookups, so the pass ballot after the barrier waits on no global load
+    const uint32_t* tt = NL > 0 ? P.truth_early : P.truth;
+    const uint32_t words = ((1u << (2 * P.nleaves)) + 31) / 32;
+    for (uint32_t i = tid; i < words; i += BLOCK) L.etruth[i] = tt[i];
+  }
   if (count_plan) {
     for (uint32_t i = tid; i < LEAN_LINES; i += BLOCK) L.lines_t[i] = L.lines_v[i] = 0u;
 #pragma unroll
@@ -301,7 +307,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
       const uint32_t lmask = P.strp[0].lmask;
       const uint32_t T = bits & lmask & ~lf, F = (~bits & lmask) | lf;
       const uint32_t ix = T | (F << P.nleaves);
-      pass = ((NL > 0 ? P.truth_early : P.truth)[ix >> 5] >> (ix & 31)) & 1u;
+      pass = (L.etruth[ix >> 5] >> (ix & 31)) & 1u;
     }
     emask = __ballot(pass);
   }
