@@ -11,11 +11,11 @@
 // run of a failing code contributes no chunk at all).  Per chunk:
 //   one 16-B buffer load of the packed codes -> a pass mask:  SWAR (BW = 1, 2, 4, at most 4 passing codes: per
 //   32-bit word, xor with the code repeated, zero-field detect) or per code (a bit test of the pass mask);
-//   the passing rows (a divergent loop, two rows per trip) gather their value (and timestamp when the tile's zone
-//   map does not pin a single bucket) and accumulate into a per-thread register cell, spilling to an LDS table;
-//   dense blocks (most rows pass) are read row-major with coalesced loads instead;
-//   with late string columns (NL > 0) the wave's passing rows are first compacted into its LDS list and processed
-//   128 per trip with every lane busy (late-column lookups, late filter, value gather).
+//   the wave's passing rows are compacted into its LDS list and processed 128 per trip with every lane busy
+//   (late-column lookups, late filter, value gather; NL = 0 COUNT and dense-code tiles keep a per-lane loop, two rows
+//   per round trip) and accumulate into a per-thread register cell, spilling to an LDS table; the timestamp is
+//   gathered only when neither the tile's zone map (one bucket) nor a split (sorted timestamps, bucket boundaries
+//   found by search) gives the row's bucket; dense blocks (most rows pass) are read row-major with coalesced loads.
 // No workgroup barrier in the main loop.  VALU per row is a fraction of scan_tiles' (which decodes every column
 // generally and compacts rows through LDS).
 #pragma once
