@@ -1464,6 +1464,18 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     // (half of C3's listed rows) cost more than the round trip they save (profiles/r05_bench_c3*.json)
     const char* sg = getenv("LK_SPEC_GATHER");
     P.spec_gather = (late_leaves && sg && *sg == '1') ? 1u : 0u;
+    // one string column whose eq / in filter passes a quarter or more of its values (the dense query): the 5-wave
+    // per-lane scan_lean<..., 0, EARLY> -- its dense-code tiles lose ~0.3 ms in C2's 4-wave listed shape
+    // (LK_NO_DENSE_SHAPE=1: A/B)
+    if (P.nstr == 1 && !strs[0].cand.empty() && !getenv("LK_NO_DENSE_SHAPE")) {
+      GlobalDict& gd = E.dict(strs[0].name);
+      size_t nv = 0;
+      {
+        std::lock_guard<std::mutex> g(gd.mu);
+        nv = gd.size();
+      }
+      if (strs[0].cand.size() * 4 >= nv) P.late_chunk = 1u;
+    }
   }
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
                     ? (all_lean ? 2u : 1u) : 0u;

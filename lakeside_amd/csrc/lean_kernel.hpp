@@ -197,7 +197,9 @@ __device__ __forceinline__ void lean_rep(uint32_t v, uint32_t& w0, uint32_t& w1,
 // EARLY (NL > 0, a late filter leaf: P.late_chunk): tiles that allow it decode the late columns per chunk (early_late
 // below); its own kernel, built for 4 waves per SIMD, so the other shapes keep their occupancy.
 template <int AGG, bool HASH, int NL, bool EARLY = false>
-__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4 : LEAN_WAVES(NL, AGG)))) void scan_lean(QParams P) {
+// NL = 0 with EARLY (P.late_chunk set by the host when the filter passes a quarter or more of the name values: the
+// dense query): the per-lane loop and row-major dense blocks at 5 waves per SIMD, the shape those tiles measured best in
+__global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (NL == 0 ? LK_LEAN_WAVES1 : 4) : LEAN_WAVES(NL, AGG)))) void scan_lean(QParams P) {
   using LT = LeanLds<NL>;
   __shared__ LT L;
   const int tid = threadIdx.x;
@@ -833,7 +835,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
     // The packed codes of the next PF rounds are in flight while a round runs (a register ring; loads return in issue
     // order, so a round waits only for its own chunk): a round's own work is far shorter than a memory round trip, and
     // one load per lane in flight would leave the tile's stream latency-bound (PF = 0: loaded in the round itself).
-    constexpr int PF = NL == 0 ? (AGG == AGG_COUNT ? LK_LEAN_PF0C : LK_LEAN_PF0)
+    constexpr int PF = NL == 0 ? (EARLY ? 0 : AGG == AGG_COUNT ? LK_LEAN_PF0C : LK_LEAN_PF0)
                                : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : LK_LEAN_PF1V) : LK_LEAN_PF2);
     auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
       const bool lv = qq < total;
@@ -1046,7 +1048,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? 4
           m = 0;
         }
       }
-      constexpr bool LIST0 = NL == 0 && LK_LEAN_LIST0 && AGG != AGG_COUNT;
+      constexpr bool LIST0 = NL == 0 && LK_LEAN_LIST0 && AGG != AGG_COUNT && !EARLY;
       if (NL == 0 && (!LIST0 || dense_codes)) {   // uniform
         // passing rows: two per trip (their loads in flight together)
         while (m) {

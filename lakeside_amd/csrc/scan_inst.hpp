@@ -13,8 +13,8 @@ static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
   const dim3 block(BLOCK);
   if (P.lean_split) {   // lean tiles first (lean_kernel.hpp), by late string columns
     switch (P.nstr * 2 + (P.late_chunk ? 1 : 0)) {
-      case 2:
-      case 3: hipLaunchKernelGGL((scan_lean<AGG, HASH, 0>), grid, block, 0, st, P); break;
+      case 2: hipLaunchKernelGGL((scan_lean<AGG, HASH, 0>), grid, block, 0, st, P); break;
+      case 3: hipLaunchKernelGGL((scan_lean<AGG, HASH, 0, true>), grid, block, 0, st, P); break;   // dense codes
       case 4: hipLaunchKernelGGL((scan_lean<AGG, HASH, 1>), grid, block, 0, st, P); break;
       case 5: hipLaunchKernelGGL((scan_lean<AGG, HASH, 1, true>), grid, block, 0, st, P); break;
       case 6: hipLaunchKernelGGL((scan_lean<AGG, HASH, 2>), grid, block, 0, st, P); break;
