@@ -38,6 +38,16 @@ QUERIES = {
     "c2s10": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
                           "computed": False, "dataType": "string"}, agg="sum", group_bys=[], step=10000,
                   desc=":eq _cardinalhq.name=metric_07 :sum, step 10s"),
+    # C2 over real values (SURVEY §8(d) "real" mode, lognormal(0, 2)): no load-time "integral" summary applies, so every
+    # SUM add takes the compensated double-double path (the <= 1 ulp bar of north_star)
+    "c2real": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                           "computed": False, "dataType": "string"}, agg="sum", group_bys=[], value_mode=1,
+                   desc=":eq _cardinalhq.name=metric_07 :sum, step 1m, lognormal(0,2) values (compensated sums)"),
+    # C2 with the timestamps permuted within each 1M-row row group: no tile is sorted (no split tile) and no tile is
+    # pinned to one bucket by its zone map, so every passing row gathers its timestamp (the sortedness-free C2)
+    "c2shuf": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                           "computed": False, "dataType": "string"}, agg="sum", group_bys=[], ts_shuffle=1,
+                   desc=":eq _cardinalhq.name=metric_07 :sum, step 1m, timestamps shuffled within each row group"),
     # C3 (configs[2]): :and/:re multi-tag predicate + :by 2-key group-by :max
     "c3": dict(filter={"op": "and",
                        "q1": {"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq"},
@@ -49,6 +59,11 @@ QUERIES = {
     "c4": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
                        "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.service.name"],
                desc=":eq _cardinalhq.name=metric_07 :sum :by resource.service.name, step 1m"),
+    # C4 over real values (compensated sums into 24,000 cells)
+    "c4real": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
+                           "computed": False, "dataType": "string"}, agg="sum", group_bys=["resource.service.name"],
+                   value_mode=1,
+                   desc=":eq _cardinalhq.name=metric_07 :sum :by resource.service.name, step 1m, lognormal(0,2) values"),
     # C5 (configs[4]): 10M-value group key, all segments in hour 0, one 1h bucket (<= 10M datapoints); 8 segments
     # per GPU (64 over the node)
     "c5": dict(filter={"k": "_cardinalhq.name", "v": ["metric_07"], "op": "eq", "extracted": False,
@@ -164,7 +179,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--segments", type=int, default=None, help="segments per GPU (default: the query's config)")
     ap.add_argument("--rows", type=int, default=1 << 24, help="rows per segment")
-    ap.add_argument("--query", default="c2", choices=sorted(QUERIES))
+    ap.add_argument("--query", default=None, choices=sorted(QUERIES),
+                    help="default: c2 (BASELINE configs[1]) at N=1, c4 (configs[3]: :sum :by service, 64 segments "
+                         "per GPU) at N > 1")
     ap.add_argument("--cpu-sample", type=int, default=-1,
                     help="segments per rank timed on the CPU restatement (-1: all = full-size validation; 0: skip)")
     ap.add_argument("--gen-workers", type=int, default=4)
@@ -177,6 +194,8 @@ def main():
                          "ncclSend/ncclRecv of the table reduce or the key-range all-to-all) runs on this GPU")
     args = ap.parse_args()
 
+    if args.query is None:
+        args.query = "c4" if args.gpus > 1 else "c2"
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -229,7 +248,8 @@ def main():
 
     def gen(i):
         return i, synth.make_segment(synth.segment_spec(i, rows=args.rows, threads=4, hour=hour,
-                                                        highcard_n=highcard))
+                                                        highcard_n=highcard, value_mode=q.get("value_mode", 0),
+                                                        ts_shuffle=q.get("ts_shuffle", 0)))
 
     # The CPU baseline / validator reads the same Parquet bytes: every rank keeps its shard in host memory.
     keep_cpu = args.cpu_sample != 0
@@ -373,20 +393,29 @@ def main():
     # HBM traffic of the scan kernel(s) per launch: rocprofv3 FETCH_SIZE / WRITE_SIZE passes over this same bench
     # command (scripts/gpu_bench_prof.sh -> scripts/pmc_traffic.py; separate runs, as counters must be collected
     # alone), committed under profiles/ -- read here only when it profiled this query at this size.
+    # Accepted only when that summary was taken with this very library build (sha256 of the loaded .so) and counted
+    # the same plan bytes: a PMC pass of an older kernel says nothing about this one, so otherwise traffic is null.
     traffic, traffic_src = None, None
+    lib_sha = _lib_sha16()
     pmc_file = None
-    for rnd in ("r05", "r04", "r03", "r02"):   # the newest committed PMC summary of this query
+    for rnd in ("r06", "r05", "r04", "r03", "r02"):   # the newest committed PMC summary of this query
         cand = os.path.join(ROOT, "profiles", f"{rnd}_pmc_{args.query}.json")
         if os.path.exists(cand):
             pmc_file = cand
             break
     if pmc_file:
         pmc = json.load(open(pmc_file))
-        if pmc.get("query") == args.query and pmc.get("algorithmic_bytes_per_launch") == alg_bytes:
+        if (pmc.get("query") == args.query and pmc.get("lib_sha16") == lib_sha
+                and pmc.get("plan_bytes_per_launch") == pbytes and world == 1):
             traffic = pmc["hbm_bytes_per_launch"]
             traffic_src = (f"profiles/{os.path.basename(pmc_file)}: rocprofv3 --pmc FETCH_SIZE (x{pmc['fetch_correction']} "
                            f"gfx950 correction, calibrated in profiles/r02_gather_fetchsize.json) + WRITE_SIZE passes "
-                           f"over this bench command; scan kernel {pmc.get('scan_kernel_ms')} ms in that run")
+                           f"over this bench command with this library build (sha256 {lib_sha}); scan kernel "
+                           f"{pmc.get('scan_kernel_ms')} ms in that run")
+        else:
+            traffic_src = (f"null: the newest PMC summary (profiles/{os.path.basename(pmc_file)}) was taken with "
+                           f"library {pmc.get('lib_sha16')} / plan bytes {pmc.get('plan_bytes_per_launch')}, this run "
+                           f"is library {lib_sha} / plan bytes {pbytes:.0f}")
 
     if rank == 0:
         line = {
@@ -426,10 +455,16 @@ def main():
                                        "rounds",
                          "plan_bytes_per_launch": pbytes,
                          "algorithmic_bytes_per_launch": alg_bytes, "algorithmic_gbs": alg_gbs,
+                         "frac_algorithmic": alg_gbs / HBM_PEAK_GBS,
+                         "frac_algorithmic_note": "SURVEY §8(d)'s algorithmic bytes (every referenced column chunk in "
+                                                  "full) / scan-kernel time / 8 TB/s, beside `frac` (plan bytes): above "
+                                                  "1 when the plan skips bytes §8(d) counts (zone-mapped / split-tile "
+                                                  "timestamps, value lines with no passing row)",
                          "traffic_source": traffic_src,
                          "traffic_gbs": traffic / (scan_avg / 1e3) / 1e9 if traffic else None,
                          "stream_copy_gbs": copy_gbs},
             "validated": validated,
+            "lib_sha16": lib_sha,
             "cpu_baseline": cpu,
         }
         if use_dist:   # the distributed call's own stages (rank 0): group-dim agreement, table reduce, row emission
@@ -451,6 +486,17 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     eng.close()
+
+
+def _lib_sha16():
+    """First 16 hex digits of the sha256 of the evaluator library this process loaded."""
+    import hashlib
+    from lakeside_amd import _lib
+    h = hashlib.sha256()
+    with open(_lib.LIB_PATH, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 20), b""):
+            h.update(blk)
+    return h.hexdigest()[:16]
 
 
 def _cpu_model():

@@ -149,7 +149,7 @@ const char* lk_engine_stats(lk_engine* e) {
     }
   }
   o += "}";
-  o += ",\"comm\":" + lk::comm_describe(E);   // set once by lk_comm_init*; not under comm_mu (a call may hold it)
+  o += ",\"comm\":" + lk::comm_describe(E);   // the description cached at lk_comm_init* (not under comm_mu)
   o += "}";
   t_err.clear();
   static thread_local std::string t_stats;

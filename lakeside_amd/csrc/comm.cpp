@@ -356,7 +356,12 @@ struct HostComm final : Comm {
 }  // namespace
 
 int comm_world(const Engine& E) { return E.comm ? E.comm->world : 1; }
-std::string comm_describe(const Engine& E) { return E.comm ? E.comm->describe() : std::string("null"); }
+// The communicator's description, cached when lk_comm_init* installed it: a stats call never touches the
+// communicator itself, so it cannot race with its creation.
+std::string comm_describe(const Engine& E) {
+  std::lock_guard<std::mutex> g(const_cast<Engine&>(E).comm_init_mu);
+  return E.comm_desc;
+}
 CommCounters comm_counters(const Engine& E) { return E.comm ? E.comm->cnt : CommCounters{}; }
 bool comm_loopback(const Engine& E) { return E.comm && E.comm->loopback; }
 int comm_rank(const Engine& E) { return E.comm ? E.comm->rank : 0; }
@@ -711,6 +716,7 @@ int lk_comm_unique_id(uint8_t* id) {
 int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
   if (!e || !id || world < 1 || rank < 0 || rank >= world) return LK_ERR_ARG;
   lk::Engine& E = *e->e;
+  std::lock_guard<std::mutex> g(E.comm_init_mu);   // set once: concurrent inits cannot both pass the check
   if (E.comm) {
     lk::set_error("communicator already initialised");
     return LK_ERR_ARG;
@@ -729,6 +735,7 @@ int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
     delete C;
     return LK_ERR_DEVICE;
   }
+  E.comm_desc = C->describe();
   E.comm = C;
   return LK_OK;
 }
@@ -736,6 +743,7 @@ int lk_comm_init(lk_engine* e, const uint8_t* id, int world, int rank) {
 int lk_comm_init_host(lk_engine* e, int world, int rank, lk_allgather_fn fn, void* user) {
   if (!e || !fn || world < 1 || rank < 0 || rank >= world) return LK_ERR_ARG;
   lk::Engine& E = *e->e;
+  std::lock_guard<std::mutex> g(E.comm_init_mu);
   if (E.comm) {
     lk::set_error("communicator already initialised");
     return LK_ERR_ARG;
@@ -745,6 +753,7 @@ int lk_comm_init_host(lk_engine* e, int world, int rank, lk_allgather_fn fn, voi
   C->rank = rank;
   C->fn = fn;
   C->user = user;
+  E.comm_desc = C->describe();
   E.comm = C;
   return LK_OK;
 }

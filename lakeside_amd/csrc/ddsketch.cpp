@@ -35,6 +35,20 @@ void Sketch::add_bin(uint32_t bin, double count) {
   }
 }
 
+bool Sketch::accept(double v) {
+  const Mapping& m = mapping();
+  const double a = std::fabs(v);
+  if (!(a <= m.max_indexable)) return false;
+  if (a <= m.min_indexable) {
+    zero += 1.0;
+    return true;
+  }
+  const double x = std::log(a) * m.multiplier;
+  const int32_t i = x >= 0.0 ? int32_t(x) : int32_t(x) - 1;
+  (v < 0.0 ? neg : pos)[i] += 1.0;
+  return true;
+}
+
 void Sketch::merge(const Sketch& o) {
   for (auto& kv : o.pos) pos[kv.first] += kv.second;
   for (auto& kv : o.neg) neg[kv.first] += kv.second;

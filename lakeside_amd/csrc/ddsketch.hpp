@@ -31,6 +31,9 @@ struct Sketch {
   std::map<int32_t, double> pos, neg;   // index -> count (DenseStore bins, sparse here)
   double zero = 0.0;
   void add_bin(uint32_t bin, double count);   // a kernel bin id (layout.hpp DD_*)
+  // DDSketch.accept(v) on the host (the kernel's dd_bin restated: |v| <= min indexable -> zero count, else
+  // LogarithmicMapping.index); false for NaN / a magnitude beyond the mapping's range (checkValueTrackable throws)
+  bool accept(double v);
   void merge(const Sketch& o);                // DDSketch.mergeWith: bin counts add
   double count() const;
   // DDSketch.getValueAtQuantile(q): rank = q * (count - 1); walk negative bins (descending index), the zero count,

@@ -167,7 +167,9 @@ struct Engine {
   std::mutex leaf_mu;
   std::map<std::string, std::shared_ptr<LeafBits>> leaf_cache;   // key: column \x1f op \x1f values
   std::shared_ptr<LeafBits> leaf_bits(const std::string& key);
-  Comm* comm = nullptr;
+  Comm* comm = nullptr;                          // set once by lk_comm_init* (under comm_init_mu), never replaced
+  std::mutex comm_init_mu;                       //   guards the set-once check and comm_desc
+  std::string comm_desc = "null";                //   comm->describe() taken at init: lk_engine_stats reads this copy
   std::mutex order_mu;
   std::unordered_map<std::string, std::shared_ptr<const DictOrder>> orders;   // per column, latest size
   std::shared_ptr<const DictOrder> dict_order(const std::string& col, size_t n);

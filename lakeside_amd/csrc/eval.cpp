@@ -305,6 +305,11 @@ void expand_rows_from_keys(int64_t* ts, uint32_t* gid, uint32_t* glob, const uns
 
 static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
                          int glob_size, unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo);
+// internal evaluation flag: per-glob rows of a distributed call (rank 0 receives them), for evaluate_metrics_pct
+constexpr unsigned kEvalDistPerGlob = 1u << 30;
+static int evaluate_metrics_pct(Engine& E, const std::string& json, const Request& R, const char* const* paths,
+                                size_t n_paths, int glob_size, unsigned flags, const int32_t* shard, bool dist,
+                                lk_result* res);
 static int evaluate_mixed_steps(Engine& E, const std::string& json, const Request& R, const char* const* paths,
                                 size_t n_paths, int glob_size, unsigned flags, const int32_t* shard, bool dist,
                                 lk_result* res);
@@ -348,6 +353,9 @@ static int evaluate_req(Engine& E, const std::shared_ptr<const Request>& Rp, con
 int evaluate(Engine& E, const std::string& json, const char* const* paths, size_t n_paths, int glob_size,
              unsigned flags, const int32_t* shard, bool dist, lk_result* res) {
   const std::shared_ptr<const Request> Rp = E.parse_cached(json);
+  if (Rp->dataset == "metrics" && Rp->has_chart && !Rp->is_tag_query && Rp->aggregation.size() > 1 &&
+      Rp->aggregation[0] == 'p' && !Rp->field_chart && !Rp->has_extract && !Rp->has_compute)
+    return evaluate_metrics_pct(E, json, *Rp, paths, n_paths, glob_size, flags, shard, dist, res);
   if (n_paths == Rp->segments.size() && mixed_steps(*Rp, glob_size <= 0 ? 10 : glob_size))
     return evaluate_mixed_steps(E, json, *Rp, paths, n_paths, glob_size <= 0 ? 10 : glob_size, flags, shard, dist, res);
   return evaluate_req(E, Rp, paths, n_paths, glob_size, flags, shard, dist, res);
@@ -366,7 +374,7 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
   // sketch aggregations (VERDICT r4 missing #4): percentiles (logs / traces `p<NN>`) merge their DDSketches and
   // cardinality (`ces`) its HLLs per (timestamp, tags), as query-api merges sketches of any origin
   // (TimeGroupedSketchAggregator.scala:34-43), then read the quantile / estimate of the merged sketch
-  const bool ces = (agg == "ces" || R.rollup.find("ces") != std::string::npos) && R.dataset != "metrics";
+  const bool ces = agg == "ces" || (R.rollup.find("ces") != std::string::npos && R.dataset != "metrics");
   const bool pct = !ces && agg.size() > 1 && agg[0] == 'p' && R.dataset != "metrics";
   double quantile = 0.0;
   if (pct) quantile = strtod(agg.c_str() + 1, nullptr) / 100.0;
@@ -497,6 +505,107 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
   return LK_OK;
 }
 
+// Metrics percentiles (VERDICT r5 missing #1).  Each glob's SQL is
+//   SELECT ts, MAX(rollup_<rollup|sum>) AS value, name, <groupBys> ... GROUP BY ts, <groupBys>, name
+// (BaseExpr.scala:379-383), and the worker's PushDownAggregatorStage feeds every row's value (NULL -> 0.0, JDBC
+// getDouble) into the DDSketch of its (raw timestamp, key tags) -- the groupBys' tags, or {"name": v} without
+// groupBys (PushDownAggregatorStage.scala:56-60, 69-81, 188-197); query-api merges the sketches per (timestamp, tags)
+// (TimeGroupedSketchAggregator.scala:34-37).  Here the per-glob MAX rows come from the GPU scan (the metrics MAX
+// path with per-glob cells, every rank's partial table folded on rank 0 when distributed) and the host builds the
+// sketches from those rows -- O(output rows), as the logs path assembles its sketches from the kernel's bins.
+static int evaluate_metrics_pct(Engine& E, const std::string& json, const Request& R, const char* const* paths,
+                                size_t n_paths, int glob_size, unsigned flags, const int32_t* shard, bool dist,
+                                lk_result* res) {
+  const auto t0 = std::chrono::steady_clock::now();
+  const bool per_glob_rows = (flags & LK_PER_GLOB_ROWS) != 0;
+  if (!per_glob_rows && !(flags & LK_MERGED)) throw PlanError(LK_ERR_ARG, "flags must be LK_PER_GLOB_ROWS or LK_MERGED");
+  if (dist && per_glob_rows) throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
+  char* end = nullptr;
+  const std::string qs = R.aggregation.substr(1);
+  const double quantile = strtod(qs.c_str(), &end) / 100.0;
+  if (end == qs.c_str() || *end || !(quantile >= 0.0 && quantile <= 1.0))
+    throw PlanError(LK_ERR_ARG, "percentile aggregation " + R.aggregation);
+  if (n_paths == R.segments.size() && mixed_steps(R, glob_size <= 0 ? 10 : glob_size))
+    throw PlanError(LK_ERR_UNSUPPORTED, "metrics percentiles over globs with different steps");
+  auto sub = std::make_shared<Request>(parse_request(json));
+  sub->aggregation = "max";
+  lk_result r;
+  evaluate_req(E, sub, paths, n_paths, glob_size, LK_PER_GLOB_ROWS | kEvalDistPerGlob, shard, dist, &r);
+  using Tags = std::vector<std::pair<std::string, std::string>>;
+  struct Row {
+    int64_t ts;
+    uint32_t glob;
+    Tags tags;          // key tags, sorted by name
+    dd::Sketch sk;
+  };
+  std::vector<Row> rows;
+  std::map<std::tuple<int64_t, uint32_t, Tags>, size_t> at;   // (ts, glob, key tags) -> row
+  const bool by_name = R.group_bys.empty();
+  const size_t nt = r.tag_names.size();
+  for (size_t i = 0; i < r.nrows; i++) {
+    Tags all;   // the DataPoint's tags (NULL / "null" / "" dropped, queryTags when none, Commons.scala:433, 450-452)
+    for (size_t c = 0; c < nt; c++)
+      if (const char* v = r.tag(i, c)) all.emplace_back(r.tag_names[c], v);
+    auto get = [&](const std::string& k) -> const std::string* {
+      for (auto& kv : all)
+        if (kv.first == k) return &kv.second;
+      return nullptr;
+    };
+    Tags kt;   // getGroupByKeyTags
+    if (by_name) {
+      const std::string* nm = get("name");
+      kt.emplace_back("name", nm ? *nm : std::string());
+    } else {
+      for (auto& g : R.group_bys)
+        if (const std::string* v = get(g))
+          if (std::none_of(kt.begin(), kt.end(), [&](const auto& kv) { return kv.first == g; })) kt.emplace_back(g, *v);
+      std::sort(kt.begin(), kt.end());
+    }
+    const uint32_t glob = per_glob_rows ? r.glob[i] : 0u;
+    // merged without groupBys: one sketch per timestamp whose tags are one input's (here: the smallest name)
+    Tags key = (!per_glob_rows && by_name) ? Tags{} : kt;
+    auto ins = at.emplace(std::make_tuple(r.ts[i], glob, key), rows.size());
+    if (ins.second) rows.push_back(Row{r.ts[i], glob, kt, dd::Sketch{}});
+    Row& o = rows[ins.first->second];
+    if (!per_glob_rows && by_name && kt[0].second < o.tags[0].second) o.tags = kt;
+    // DDSketch.accept throws on NaN / an untrackable magnitude: the worker's stream fails (Commons.scala:331-335)
+    if (!o.sk.accept(r.val[i])) throw PlanError(LK_ERR_ARG, "DDSketch: value outside the trackable range");
+  }
+  std::sort(rows.begin(), rows.end(), [](const Row& a, const Row& b) {
+    return a.ts != b.ts ? a.ts < b.ts : (a.glob != b.glob ? a.glob < b.glob : a.tags < b.tags);
+  });
+  std::vector<std::string> names;   // tag names, first-seen order
+  for (auto& o : rows)
+    for (auto& kv : o.tags)
+      if (std::find(names.begin(), names.end(), kv.first) == names.end()) names.push_back(kv.first);
+  res->exemplar = true;   // tags materialized per row (ex_tags)
+  res->per_glob = per_glob_rows;
+  res->alloc_rows(rows.size());
+  res->tag_names = names;
+  res->ex_tags.assign(rows.size() * names.size(), nullptr);
+  for (size_t i = 0; i < rows.size(); i++) {
+    res->ts[i] = rows[i].ts;
+    res->val[i] = rows[i].sk.quantile(quantile);
+    res->glob[i] = rows[i].glob;
+    res->gid[i] = uint32_t(i);
+    res->sketches.push_back(rows[i].sk.serialize());
+    if (res->keep_sketches) res->dd_objs.push_back(rows[i].sk);
+    for (auto& kv : rows[i].tags) {
+      const size_t c = size_t(std::find(names.begin(), names.end(), kv.first) - names.begin());
+      res->owned.push_back(kv.second);
+      res->ex_tags[i * names.size() + c] = res->owned.back().c_str();
+    }
+  }
+  // the MAX scan's own stats, then this stage's
+  std::string st = r.stats;
+  if (!st.empty() && st.back() == '}') st.pop_back();
+  char buf[160];
+  snprintf(buf, sizeof buf, ",\"metrics_pct_rows_in\":%zu,\"pct_total_ms\":%.6f}", r.nrows,
+           std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+  res->stats = st + buf;
+  return LK_OK;
+}
+
 static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, const char* const* paths, size_t n_paths,
                          int glob_size, unsigned flags, const int32_t* shard, bool dist, lk_result* res, unsigned redo) {
   const bool metrics_raw = (redo & REDO_METRICS_RAW) != 0;
@@ -540,7 +649,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   if (tagq) agg = AGG_ROWS;
   // Cardinality (`ces` in the chart's rollup, PushDownAggregatorStage.scala:44,82-94; computeCardinality sets it,
   // QueryEngineV2.scala:616-617): per step one HLL over the rows' group-key strings, whatever the SQL aggregate.
-  else if ((R.aggregation == "ces" || R.rollup.find("ces") != std::string::npos) && R.dataset != "metrics") agg = AGG_CES;
+  // Metrics: `ces` as the chart's aggregation compiles to `SELECT ts, 1.0 as value, name, <groupBys> ... WHERE
+  // <filter>` -- every passing row, no rollup column (BaseExpr.scala:385-388); a metrics rollup of "ces" under another
+  // aggregation stays that aggregation over rollup_ces (the SQL reads that column).
+  else if (R.aggregation == "ces" || (R.rollup.find("ces") != std::string::npos && R.dataset != "metrics")) agg = AGG_CES;
   else if (R.aggregation == "sum") agg = AGG_SUM;
   else if (R.aggregation == "min") agg = AGG_MIN;
   else if (R.aggregation == "max") agg = AGG_MAX;
@@ -555,6 +667,8 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // assembles the sketches.
   const bool sketch = agg == AGG_SKETCH;
   const bool ces = agg == AGG_CES;
+  // queries whose SQL references no value column: tag queries (COUNT(*)) and metrics `ces` (1.0 per row)
+  const bool no_value_col = tagq || (ces && R.dataset == "metrics");
   double quantile = 0.0;
   if (sketch) {
     char* end = nullptr;
@@ -566,7 +680,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // Merged avg: query-api runs AVG as separate SUM and COUNT pushdowns, merges them per (timestamp, tags) into
   // a {sum, count} map and divides (QueryEngineV2.scala:280-283, TimeGroupedSketchAggregator.scala:74-78,
   // BaseExpr.scala:88-91).  The table holds both, so one scan gives Σsum / Σcount (NaN when no value).
-  if (dist && per_glob_rows) throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
+  // (metrics percentiles evaluate their per-glob MAX rows distributed: kEvalDistPerGlob, internal)
+  if (dist && per_glob_rows && !(flags & kEvalDistPerGlob))
+    throw PlanError(LK_ERR_ARG, "distributed evaluation returns merged rows");
   const bool metrics = R.dataset == "metrics" && !tagq;   // a tag query groups no timestamps
   const std::string vcol = value_column(R);
 
@@ -731,7 +847,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // ---- globs ----
   const std::set<std::string> fset = field_set(R);
   std::vector<std::string> probe_cols(fset.begin(), fset.end());   // columns whose existence matters
-  for (auto& k : tagq ? std::vector<std::string>{kTimestamp, R.tag_name} : std::vector<std::string>{kTimestamp, kName, vcol})
+  for (auto& k : tagq ? std::vector<std::string>{kTimestamp, R.tag_name}
+                      : (no_value_col ? std::vector<std::string>{kTimestamp, kName}
+                                      : std::vector<std::string>{kTimestamp, kName, vcol}))
     if (std::find(probe_cols.begin(), probe_cols.end(), k) == probe_cols.end()) probe_cols.push_back(k);
   for (auto* l : all_leaves)
     if (std::find(probe_cols.begin(), probe_cols.end(), l->k) == probe_cols.end()) probe_cols.push_back(l->k);
@@ -791,7 +909,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         return value_rank(hc.ptype) == 0;   // value column / numeric comparison column
       };
       if (bad(kTimestamp, 0)) gfail[gi] = 1;
-      if (!tagq) {
+      if (!no_value_col) {
         if (bad(vcol, 1)) {
           // sum / avg over a VARCHAR value column is DuckDB's Binder Error (empty glob); count / min / max over it
           // run in DuckDB and this engine does not implement them: the call fails (LK_ERR_UNSUPPORTED)
@@ -848,7 +966,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     // Binder Error: referenced column absent from the whole glob
     if (tagq) {
       if (!glob_has(gi, kTimestamp) || !glob_has(gi, R.tag_name)) g.skip = true;   // SELECT "<tag>": Binder Error
-    } else if (!glob_has(gi, kTimestamp) || !glob_has(gi, kName) || !glob_has(gi, vcol)) {
+    } else if (!glob_has(gi, kTimestamp) || !glob_has(gi, kName) || (!no_value_col && !glob_has(gi, vcol))) {
       g.skip = true;
     }
     for (auto& l : leaves)
@@ -1222,16 +1340,17 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       };
       bind(0, kTimestamp, false);
       if (!q.cols[0].present) continue;            // no timestamps: every row fails the window
-      if (!tagq) bind(1, vcol, false);             // COUNT(*) reads no value column
+      if (!no_value_col) bind(1, vcol, false);     // COUNT(*) / metrics `ces` read no value column
       for (size_t s = 0; s < strs.size(); s++) bind(2 + dev_of[s], strs[s].name, true);
       for (size_t n = 0; n < nums.size(); n++) bind(int(2 + strs.size() + n), nums[n], false);
       // scan_lean takes every tile of this segment when no page of its three columns holds a NULL and every
       // name page has a small dictionary (lean_tile's test at page granularity)
       bool seg_lean = !general;
       if (seg_lean) {
-        const int ct = S.col_index(kTimestamp), cv = tagq ? -1 : S.col_index(vcol);
+        const int ct = S.col_index(kTimestamp), cv = no_value_col ? -1 : S.col_index(vcol);
         const int cn = strs.size() <= 3 ? S.col_index(strs[size_t(lead)].name) : -1;
-        seg_lean = ct >= 0 && (cv >= 0 || tagq) && cn >= 0 && !S.cols[ct].any_nulls && (tagq || !S.cols[cv].any_nulls) &&
+        seg_lean = ct >= 0 && (cv >= 0 || no_value_col) && cn >= 0 && !S.cols[ct].any_nulls &&
+                   (no_value_col || !S.cols[cv].any_nulls) &&
                    !S.cols[cn].any_nulls;
         for (size_t s2 = 0; s2 < strs.size() && seg_lean; s2++) {   // late columns: absent, or NULL-free dictionaries
           if (int(s2) == lead) continue;
@@ -1436,7 +1555,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   const uint32_t* d_maps = reinterpret_cast<const uint32_t*>(dbuf + o_maps);
   const int kagg = agg == AGG_AVG ? AGG_SUM : ((agg == AGG_ROWS || agg == AGG_SKETCH || agg == AGG_CES) ? AGG_COUNT : agg);
   // lean tables: no NULL value anywhere in the value column -> cnt == rows; min/max also imply rows
-  if (!value_nulls && agg != AGG_ROWS && !getenv("LK_NO_LEAN"))
+  if (!value_nulls && !no_value_col && !getenv("LK_NO_LEAN"))
     P.lean = (kagg == AGG_MIN || kagg == AGG_MAX) ? LEAN_NO_ROWS : LEAN_NO_CNT;
   // dense SUM (not AVG, which needs the row counts): existence from the -0.0 marker, no rows atomics at all
   if (P.lean == LEAN_NO_CNT && agg == AGG_SUM && !hash_mode && !sketch && !ces && !getenv("LK_NO_SUM_EXISTS"))
@@ -1447,7 +1566,8 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   // (<= 2 of them): NULL-free tiles with a small name dictionary go to scan_lean (lean_kernel.hpp), the rest to
   // scan_tiles
   const bool lean_shape = P.nstr == 1 || (P.nstr <= 3 && P.late_mask == ((1u << P.nstr) - 2u));
-  P.rows_only = tagq ? 1u : 0u;   // COUNT(*): no value column is bound (lean tiles need none)
+  P.rows_only = no_value_col ? 1u : 0u;   // COUNT(*) / metrics ces: no value column is bound (lean tiles need none)
+  bool dense_shape = false;               // the single-column dense-code scan_lean shape was picked (stats)
   // late columns decoded per chunk (scan_lean<..., EARLY>) where a late filter leaf exists: the late filter then runs
   // before the rows are listed, and a listed row waits only on its value.  Opt-in (LK_LATE_CHUNK=1): measured slower
   // than the per-row late stage on C3 (3.47 vs 1.97 ms) and the tag query (2.28 vs 1.06 ms) -- every chunk pays a
@@ -1466,15 +1586,19 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     P.spec_gather = (late_leaves && sg && *sg == '1') ? 1u : 0u;
     // one string column whose eq / in filter passes a quarter or more of its values (the dense query): the 5-wave
     // per-lane scan_lean<..., 0, EARLY> -- its dense-code tiles lose ~0.3 ms in C2's 4-wave listed shape
-    // (LK_NO_DENSE_SHAPE=1: A/B)
+    // (LK_NO_DENSE_SHAPE=1: A/B).  Against the dictionary's live ids (values some cached segment references), not
+    // its size, which also counts ids evicted segments left behind; the pick is in stats.lean_dense_shape.
     if (P.nstr == 1 && !strs[0].cand.empty() && !getenv("LK_NO_DENSE_SHAPE")) {
       GlobalDict& gd = E.dict(strs[0].name);
       size_t nv = 0;
       {
         std::lock_guard<std::mutex> g(gd.mu);
-        nv = gd.size();
+        nv = gd.live;
       }
-      if (strs[0].cand.size() * 4 >= nv) P.late_chunk = 1u;
+      if (strs[0].cand.size() * 4 >= nv) {
+        P.late_chunk = 1u;
+        dense_shape = true;
+      }
     }
   }
   P.lean_split = (lean_shape && P.truth && (agg != AGG_ROWS || tagq) && !sketch && (!numeric || vleaf) && !getenv("LK_NO_LEAN_SPLIT"))
@@ -2369,6 +2493,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   }
   if (!bad_msg.empty()) res->stats += ",\"first_glob_error\":\"" + json_escape(bad_msg) + "\"";
   if (redo) res->stats += ",\"redo\":" + std::to_string(redo);   // 1: metrics at 1 ms, 2: MIN cells kept per glob
+  if (dense_shape) res->stats += ",\"lean_dense_shape\":1";
   res->stats += "}";
   return LK_OK;
 }

@@ -299,7 +299,12 @@ static int exemplar_dist(Engine& E, CallCtx& X, const Request& R, const char* co
       }
       if (R.limit >= 0 && out.size() > uint64_t(R.limit)) out.resize(size_t(R.limit));
     } else {
-      // counts summed per tag text (the "count" tag rewritten), NULL / dropped tag apart, first-seen order
+      // counts summed per tag text (the "count" tag rewritten), NULL / dropped tag apart, first-seen order.
+      // A deliberate deviation: query-api's streamTags (QueryEngineV2.scala:452-487) flatMapMerges the
+      // pods' (tag, count) rows unsummed, in arrival order (TagQueryUtils.aggregate is commented out there), so a
+      // value present on two pods reaches the client twice.  The distributed call returns one merged table instead
+      // -- the same table the string-tag distributed path returns (one row per value, counts added) -- because
+      // arrival order across ranks is not reproducible; DESIGN.md §5 records this.
       std::map<std::string, size_t> at;
       for (auto& v : streams)
         for (auto& row : v) {

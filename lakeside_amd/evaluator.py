@@ -230,12 +230,15 @@ class Engine:
 
     # ---- evaluation ----
     def _path_array(self, paths: Sequence[str]):
-        """The C array of encoded paths, reused while the caller passes the same path list (a dashboard's refresh)."""
+        """The C array of encoded paths, reused while the caller passes the same path list (a dashboard's refresh).
+        Key and array live in one tuple swapped in by a single assignment, and the call returns the array it built
+        or checked itself, so concurrent callers with different path lists never see each other's array."""
         key = tuple(paths)
-        if getattr(self, "_paths_key", None) != key:
-            self._paths_key = key
-            self._paths_arr = (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths])
-        return self._paths_arr
+        c = getattr(self, "_paths_cache", None)
+        if c is None or c[0] != key:
+            c = (key, (ctypes.c_char_p * len(paths))(*[p.encode() for p in paths]))
+            self._paths_cache = c
+        return c[1]
 
     def eval_pushdown(self, request_json: str, paths: Sequence[str], glob_size: int = 10,
                       flags: int = LK_PER_GLOB_ROWS) -> Result:

@@ -12,7 +12,7 @@ class Spec(ctypes.Structure):
     _fields_ = [("rows", ctypes.c_uint64), ("seed", ctypes.c_uint64), ("t0_ms", ctypes.c_int64),
                 ("span_ms", ctypes.c_int64), ("rg_rows", ctypes.c_uint32), ("page_rows", ctypes.c_uint32),
                 ("value_mode", ctypes.c_int32), ("null_frac", ctypes.c_double), ("highcard_n", ctypes.c_uint32),
-                ("threads", ctypes.c_int32)]
+                ("threads", ctypes.c_int32), ("ts_shuffle", ctypes.c_int32)]
 
 
 _L = None
@@ -51,12 +51,15 @@ class Segment:
 
 
 def segment_spec(index: int, rows: int = 1 << 24, hour: int = None, value_mode: int = 0, null_frac: float = 0.0,
-                 rg_rows: int = 1 << 20, page_rows: int = 131072, highcard_n: int = 0, threads: int = 0) -> Spec:
-    """Segment `index` of the bench configs: seed 20240101 + index, covering hour (index mod 4) of T0."""
+                 rg_rows: int = 1 << 20, page_rows: int = 131072, highcard_n: int = 0, threads: int = 0,
+                 ts_shuffle: int = 0) -> Spec:
+    """Segment `index` of the bench configs: seed 20240101 + index, covering hour (index mod 4) of T0.
+    value_mode 0: integer values in [0, 1000); 1: lognormal(0, 2) reals (SURVEY §8(d) "real").  ts_shuffle 1: the
+    timestamps permuted within each row group (no sorted tile, no tile pinned to one bucket by its zone map)."""
     h = index % 4 if hour is None else hour
     return Spec(rows=rows, seed=20240101 + index, t0_ms=T0 + h * HOUR, span_ms=HOUR, rg_rows=rg_rows,
                 page_rows=page_rows, value_mode=value_mode, null_frac=null_frac, highcard_n=highcard_n,
-                threads=threads)
+                threads=threads, ts_shuffle=ts_shuffle)
 
 
 def make_segment(spec: Spec) -> Segment:

@@ -233,7 +233,7 @@ def check_hot_path(pr: PushDownRequest) -> None:
     if pr.isTagQuery or be.chart is None:
         raise NotImplementedError("tag/exemplar queries are outside the hot path")
     agg = be.chart.aggregation
-    if (is_percentile(agg) or is_ces(be)) and be.dataset != METRICS:
+    if is_percentile(agg) or is_ces(be):   # logs / traces and metrics (BaseExpr.scala:379-388, 397-399)
         pass
     elif agg not in (SUM, MIN, MAX, COUNT, AVG):
         raise NotImplementedError(f"aggregation {agg} (sketch path) is outside the hot path")
@@ -683,6 +683,9 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
     chart = be.chart
     segs = [pr.segmentRequests[i] for i in seg_idx]
     vcol = value_column(be)
+    # metrics `ces`: `SELECT ts, 1.0 as value, name, <groupBys> ... WHERE <filter>` reads no rollup column
+    # (BaseExpr.scala:385-388)
+    no_value = be.dataset == METRICS and is_ces(be)
     fs = field_set(be)
     numcols = sorted({l.k for l in _leaves(be.filter) if l.op in NUMERIC_OPS})
     strings = sorted((set(_leaf_columns(be.filter)) - set(numcols)) | set(chart.groupBys) | {NAME})
@@ -690,7 +693,7 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
         paths = [paths[j] for j in only]
         sources = None if sources is None else [sources[j] for j in only]
     try:
-        read_union, nums, strs = _read_glob(paths, [TIMESTAMP, vcol], strings, sources)
+        read_union, nums, strs = _read_glob(paths, [TIMESTAMP] + ([] if no_value else [vcol]), strings, sources)
         strs.update(_read_numeric(paths, [c for c in numcols if c in read_union], sources))
     except Exception:   # missing / unreadable file, a column DuckDB cannot bind: that glob alone is empty
         return []       # (Commons.scala:249-253: any exception -> (null, null, null) -> Source.empty)
@@ -701,7 +704,7 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
     # Columns the generated SQL references but that no file of the glob has: DuckDB raises a Binder
     # Error, which Commons.toGlobResultSet turns into an empty result (Commons.scala:249-253).  This
     # happens for a field used only under `not` (not in fieldSet), and for ts/name/value columns.
-    referenced = (set(_leaf_columns(be.filter)) - nonexistent) | {TIMESTAMP, NAME, vcol}
+    referenced = (set(_leaf_columns(be.filter)) - nonexistent) | {TIMESTAMP, NAME} | (set() if no_value else {vcol})
     if not referenced <= set(union):
         return []
     start = min(s.startTs for s in segs)                            # Commons.scala:225-226
@@ -722,7 +725,7 @@ def evaluate_glob(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[s
         bucket = ts - np.fmod(ts, step)                              # BaseExpr.scala:163-165 (fmod)
     gcols = [g for g in chart.groupBys if g not in nonexistent]      # BaseExpr.scala:338-346 (S12)
     keycols = [("name", strs[NAME])] + [(g, strs[g]) for g in gcols]
-    vals, vvalid = nums[vcol]
+    vals, vvalid = (np.zeros(n), np.zeros(n, dtype=bool)) if no_value else nums[vcol]
     idx = np.nonzero(keep)[0]
     if len(idx) == 0:
         return []
@@ -1084,7 +1087,10 @@ def _key_tags(pr: PushDownRequest, tags: Dict[str, str]) -> Dict[str, str]:
 def evaluate_percentile_per_glob(pr: PushDownRequest, glob_size: int, paths: Sequence[str], sources=None):
     """Per glob: [(ts, key tags, Sketch)] ascending in ts (ties: sorted tags).  The worker's SQL returns the passing
     rows (BaseExpr.scala:397-399); each row's value (NULL -> 0.0, JDBC getDouble) goes into the sketch of its
-    (ts - ts % step, key tags) (PushDownAggregatorStage.scala:56-60, 69-81)."""
+    (ts - ts % step, key tags) (PushDownAggregatorStage.scala:56-60, 69-81).  Metrics: the SQL returns one row per
+    (raw ts, groupBys, name) with MAX(rollup_<r>) (BaseExpr.scala:379-383), whose value (NULL -> 0.0) goes into the
+    sketch of its (raw ts, key tags) -- moduloTs is the raw timestamp for metrics (PushDownAggregatorStage.scala:
+    56-60)."""
     from oracle import ddsketch
     check_hot_path(pr)
     out = []
@@ -1093,7 +1099,10 @@ def evaluate_percentile_per_glob(pr: PushDownRequest, glob_size: int, paths: Seq
         acc: Dict[Tuple, Tuple[Dict[str, str], Any]] = {}
         for c in cells:
             kt = _key_tags(pr, c.tags)
-            vals = np.concatenate([c.values, np.zeros(c.rows - c.count)])
+            if pr.baseExpr.dataset == METRICS:
+                vals = np.array([c.agg_value(MAX)])
+            else:
+                vals = np.concatenate([c.values, np.zeros(c.rows - c.count)])
             sk = ddsketch.Sketch().accept_all(vals)
             key = (c.ts, tuple(sorted(kt.items())))
             if key in acc:
@@ -1126,8 +1135,10 @@ def merge_percentile(pr: PushDownRequest, per_glob) -> List[Tuple[int, Dict[str,
 # Cardinality estimates (`ces`): one HLL per step over the group-key strings
 # ----------------------------------------------------------------------------------------------
 def is_ces(be: BaseExpr) -> bool:
+    """`ces` as the aggregation, or (logs / traces) in the rollup; a metrics rollup of "ces" under another
+    aggregation stays that aggregation over the rollup_ces column (BaseExpr.scala:376-395)."""
     c = be.chart
-    return c is not None and (c.aggregation == "ces" or "ces" in (c.rollup or ""))
+    return c is not None and (c.aggregation == "ces" or ("ces" in (c.rollup or "") and be.dataset != METRICS))
 
 
 def evaluate_ces_per_glob(pr: PushDownRequest, glob_size: int, paths: Sequence[str], sources=None):

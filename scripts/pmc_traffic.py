@@ -51,7 +51,10 @@ out = {
     "traffic_over_algorithmic": (read + write) / q_alg,
     "plan_bytes_per_launch": bench_line("bench_fetch.json")["roofline"].get("plan_bytes_per_launch"),
     "scan_kernel_ms": bench_line("bench_fetch.json").get("scan_kernel_ms"),
+    # the library build the counters were taken with: bench.py uses this summary only for the same build
+    "lib_sha16": bench_line("bench_fetch.json").get("lib_sha16"),
 }
+assert bench_line("bench_write.json").get("lib_sha16") == out["lib_sha16"], "FETCH and WRITE passes ran different builds"
 d_fetch = counter("dense_fetch", "FETCH_SIZE")
 if d_fetch:
     d_alg = bench_line("dense_fetch.json")["roofline"]["algorithmic_bytes_per_launch"]

@@ -9,6 +9,7 @@ import json
 import os
 import socket
 
+import numpy as np
 import pytest
 
 from tests.parity import assert_rows_equal, from_jsonable
@@ -218,15 +219,18 @@ def _worker8(rank, world, port, q):
         shapes = [("c4", 2, 1 << 20, 0, 60_000, None, [synth.SERVICE], {}),
                   ("c5_1h", 1, 1 << 20, 10_000_000, 3_600_000, 0, [synth.CONTAINER], {}),
                   ("c5_1m_hash", 1, 1 << 20, 10_000_000, 60_000, 0, [synth.CONTAINER], {})]
+        loaded = set()
         for name, per, rows, hc, step, hour, gbs, env in shapes:
             n = per * world
-            keys = [f"d8/{name}/{i}" for i in range(n)]
+            data = f"{per}/{rows}/{hc}/{hour}"   # the C5 shapes share their segments (generated and loaded once)
+            keys = [f"d8/{data}/{i}" for i in range(n)]
             shard = [i // per for i in range(n)]
             for i in range(n):   # only this rank's shard: every rank's engine dictionary differs
-                if shard[i] == rank:
-                    s = synth.make_segment(synth.segment_spec(i, rows=rows, hour=hour, highcard_n=hc))
+                if shard[i] == rank and keys[i] not in loaded:
+                    s = synth.make_segment(synth.segment_spec(i, rows=rows, hour=hour, highcard_n=hc, threads=2))
                     eng.put_segment_ptr(keys[i], s.ptr, s.size)
                     s.free()
+                    loaded.add(keys[i])
             segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
             req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), segs, "sum", gbs))
             first = eng.eval_pushdown_dist(req, keys, shard, 10)
@@ -236,8 +240,10 @@ def _worker8(rank, world, port, q):
             for _ in range(9 if name == "c5_1h" else 0):
                 agree.append(eng.eval_pushdown_dist(req, keys, shard, 10).stats["dims_ms"])
             if rank == 0:
-                results[name] = (req, res.rows(), dict(res.stats, agree_ms=[res.stats["dims_ms"]] + agree), first.stats)
-                assert first.rows() == res.rows()
+                results[name] = (req, result_columns(res), dict(res.stats, agree_ms=[res.stats["dims_ms"]] + agree),
+                                 first.stats)
+                assert np.array_equal(first.ts, res.ts) and np.array_equal(first.values.view(np.uint64),
+                                                                           res.values.view(np.uint64))
             else:
                 assert len(res) == 0
         dist.barrier()
@@ -252,29 +258,32 @@ def _worker8(rank, world, port, q):
 def test_dist_world8_host_transport_c4_c5_shapes():
     """8 ranks (one GPU, host transport over gloo), each holding only its shard's segments, so the unrestricted
     group dims (service / 10M-value container) go through the dictionary exchange; C5 at a 1m step runs the hash
-    table and its record exchange.  Rank 0's merged rows equal the oracle over every segment."""
+    table and its record exchange.  Rank 0's merged rows equal the CPU restatement (oracle/cpu, the bench's
+    validator: per-glob cells folded with query-api semantics) over every segment."""
     import torch.multiprocessing as mp
 
     from lakeside_amd import synth
+    from oracle import cpu as lkcpu
     from oracle import dataexpr as dx
+    from tests.parity import result_columns
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = mp.start_processes(_worker8, args=(8, _free_port(), q), nprocs=8, join=False, start_method="spawn")
     results = q.get(timeout=800)
     procs.join()
-    for name, (req, rows, stats, first) in results.items():
+    datasets = {}
+    for name, (req, cols, stats, first) in results.items():
         pr = dx.parse_pushdown(req)
         per = 2 if name == "c4" else 1
         n = per * 8
         hour = None if name == "c4" else 0
         hc = 0 if name == "c4" else 10_000_000
-        blobs = []
-        for i in range(n):
-            s = synth.make_segment(synth.segment_spec(i, rows=1 << 20, hour=hour, highcard_n=hc))
-            blobs.append(s.bytes())
-            s.free()
-        want = dx.evaluate_merged(pr, [f"k{i}" for i in range(n)], 10, sources=blobs)
-        assert_rows_equal(rows, want, "sum", f"world 8 {name}")
+        if (per, hc) not in datasets:   # the C5 shapes share their segments
+            datasets[(per, hc)] = [synth.make_segment(synth.segment_spec(i, rows=1 << 20, hour=hour, highcard_n=hc))
+                                   for i in range(n)]
+        segs = datasets[(per, hc)]
+        table = lkcpu.evaluate_cell_table(pr, 10, [(g.ptr, g.size) for g in segs], 8)
+        lkcpu.assert_columns_equal(cols, lkcpu.merge_cell_table(table, "sum", True), "sum", f"world 8 {name}")
         if name == "c5_1m_hash":
             assert stats["table"] == "hash", stats
         if name == "c5_1h":   # 10M dense cells: key-range all-to-all + per-rank finalize (SURVEY §8(e)); each
@@ -293,6 +302,9 @@ def test_dist_world8_host_transport_c4_c5_shapes():
             assert med < 10.0, ag
             print(f"{name}: dims agreement first {first['dims_ms']:.1f} ms, reused median {med:.3f} ms "
                   f"(max {ag[-1]:.3f} of {len(ag)} calls); eval {stats['total_ms']:.1f} ms", flush=True)
+    for segs in datasets.values():
+        for g in segs:
+            g.free()
 
 
 def _worker_err(rank, world, port):
@@ -515,6 +527,62 @@ def test_dist_numeric_leaves_world2(tmp_path):
     from tests.test_gpu_numeric import _files
     paths, _ = _files(tmp_path)
     mp.spawn(_worker_numeric, args=(2, _free_port(), paths), nprocs=2, join=True)
+
+
+def _worker_metrics_sketch(rank, world, port, paths, segs):
+    """Metrics `p<NN>` / `ces` through the distributed path (host transport, world 2): each glob's per-glob MAX cells
+    are reduced on rank 0 before the sketches are built (a glob's files sit on both ranks under the modulo shard);
+    merged rows equal the oracle's over every file."""
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+
+    from lakeside_amd import synth
+    from lakeside_amd.evaluator import Engine
+    from oracle import dataexpr as dx, hll
+    from tests.test_gpu_features import _pct_rows_equal
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    eng = Engine(0)
+    try:
+        eng.comm_init_host(world, rank)
+        for filt, agg, gbs in [(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "p95", []),
+                               (synth.leaf(synth.NAME, "!=", "metric_03"), "p50", [synth.SERVICE]),
+                               (synth.leaf(synth.NAME, "eq", "metric_01"), "ces", [synth.SERVICE])]:
+            req = json.dumps(synth.pushdown(filt, segs, agg, gbs, dataset="metrics"))
+            try:
+                res = eng.eval_pushdown_dist(req, paths, None, 2)
+            except Exception as e:   # both ranks' failures in the log (spawn reports only one)
+                print(f"rank {rank}: {agg} failed: {e}", flush=True)
+                raise
+            if rank == 0:
+                pr = dx.parse_pushdown(req)
+                if agg == "ces":
+                    want = dx.merge_ces(dx.evaluate_ces_per_glob(pr, 2, paths))
+                    assert [(int(t), float(v)) for t, v in zip(res.ts, res.values)] == \
+                        [(ts, hll.estimate(ks)) for ts, ks in want], "dist metrics ces"
+                else:
+                    want = dx.merge_percentile(pr, dx.evaluate_percentile_per_glob(pr, 2, paths))
+                    got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r)) for r in range(len(res))]
+                    _pct_rows_equal(got, want, float(agg[1:]) / 100.0, f"dist metrics {agg}")
+            else:
+                assert len(res) == 0
+        dist.barrier()
+    finally:
+        eng.close()
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_dist_metrics_percentile_and_ces_world2(tmp_path):
+    import torch.multiprocessing as mp
+
+    from tests.test_gpu_features import _metrics_segments
+
+    class _Files:   # the files only: each rank's engine loads its shard
+        def load_segment(self, path):
+            pass
+    paths, _, segs = _metrics_segments(_Files(), tmp_path, [(0, True), (1, True), (0, False), (1, True)])
+    mp.spawn(_worker_metrics_sketch, args=(2, _free_port(), paths, segs), nprocs=2, join=True)
 
 
 # ---------------------------------------------------------------------------------------------------------

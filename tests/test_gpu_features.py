@@ -232,6 +232,50 @@ def test_cardinality_estimates(engine):
             [(ts, hll.estimate(ks)) for ts, ks in dx.merge_ces(want)], (gbs, agg)
 
 
+def test_metrics_percentiles_and_cardinality(engine, tmp_path):
+    """Metrics `p<NN>` (VERDICT r5 missing #1): per glob MAX(rollup_<r>) per (raw ts, groupBys, name) (BaseExpr.scala:
+    379-383), each row's value (NULL -> 0.0) into the DDSketch of its (raw ts, key tags); metrics `ces`: every passing
+    row (`1.0 as value`, no rollup column read, 385-388) into the HLL of its raw timestamp.  On-grid and off-grid
+    segments (the 1 ms re-run), NULL rollup values and NULL group values; per glob and merged vs the oracle."""
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx, hll
+    keys, blobs, segs = _metrics_segments(engine, tmp_path, [(0, True), (1, True), (0, False)])
+    for filt, agg, gbs, rollup in [(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "p95", [], None),
+                                   (synth.leaf(synth.NAME, "!=", "metric_03"), "p50", [synth.SERVICE], "max"),
+                                   (synth.leaf(synth.SERVICE, "regex", "svc-00[0-3]"), "p99.9", [synth.SERVICE, synth.NAME], None)]:
+        q = float(agg[1:]) / 100.0
+        req_d = synth.pushdown(filt, segs, agg, gbs, dataset="metrics")
+        if rollup:
+            req_d["baseExpr"]["chart"]["rollup"] = rollup
+        req = json.dumps(req_d)
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_percentile_per_glob(pr, 2, keys, sources=blobs)
+        assert sum(len(w) for w in want) > 1000
+        res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        assert list(res.ts) == sorted(res.ts)
+        for gi in range(len(want)):
+            got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
+                   for r in range(len(res)) if int(res.globs[r]) == gi]
+            _pct_rows_equal(got, want[gi], q, f"metrics {agg} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        got = [(int(merged.ts[r]), merged.tags[r], float(merged.values[r]), merged.sketch(r)) for r in range(len(merged))]
+        _pct_rows_equal(got, dx.merge_percentile(pr, want), q, f"metrics {agg} merged")
+    for filt, gbs in [(synth.leaf(synth.NAME, "eq", "metric_01"), [synth.SERVICE]),
+                      (synth.leaf(synth.SERVICE, "exists"), [synth.NAME, synth.SERVICE]),
+                      (synth.leaf(synth.NAME, "in", "metric_02", "metric_03"), [])]:
+        req = json.dumps(synth.pushdown(filt, segs, "ces", gbs, dataset="metrics"))
+        pr = dx.parse_pushdown(req)
+        want = dx.evaluate_ces_per_glob(pr, 2, keys, sources=blobs)
+        res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        got = [[(int(res.ts[r]), float(res.values[r])) for r in range(len(res)) if int(res.globs[r]) == gi]
+               for gi in range(len(want))]
+        assert got == [[(ts, hll.estimate(ks)) for ts, ks in w] for w in want], gbs
+        assert sum(len(w) for w in want) > 100
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert [(int(t), float(v)) for t, v in zip(merged.ts, merged.values)] == \
+            [(ts, hll.estimate(ks)) for ts, ks in dx.merge_ces(want)], gbs
+
+
 def test_hbm_budget_lru_eviction():
     """HBM segment cache with a weight bound (lk_engine_create hbm_budget_bytes; the worker's weighted Caffeine
     cache, WorkerApi.scala:53-64): inserts past the budget evict the least recently used segments; a segment used

@@ -1,7 +1,8 @@
 // Synthetic sealed-segment writer (bench / test tooling, not product code).
 //
 // Writes an uncompressed Parquet file with the lakeside logs schema of SURVEY.md §8(d):
-//   _cardinalhq.timestamp INT64 PLAIN (sorted, evenly spread over [t0, t0 + span))
+//   _cardinalhq.timestamp INT64 PLAIN (sorted, evenly spread over [t0, t0 + span); with ts_shuffle the same
+//                         values permuted within each row group: no tile is sorted or pinned to one bucket)
 //   _cardinalhq.value     DOUBLE PLAIN ("exact": integers in [0,1000); "real": lognormal(0, 2))
 //   _cardinalhq.name               dict, 16 values  metric_00..metric_15
 //   resource.service.name          dict, 100 values svc-000..svc-099
@@ -34,6 +35,7 @@ typedef struct {
   double null_frac;       // NULL probability of tag and value cells
   uint32_t highcard_n;    // 0: no resource.container.id column
   int32_t threads;        // 0: one per row group (capped at 32)
+  int32_t ts_shuffle;     // 0: timestamps sorted; 1: the sorted timestamps permuted within each row group
 } lk_synth_spec;
 
 int lk_synth_segment(const lk_synth_spec* spec, uint8_t** out, size_t* out_len);
@@ -252,6 +254,12 @@ void build_rg(const lk_synth_spec& sp, const std::vector<ColSpec>& cols, uint64_
       }
     } else {
       ch.data_off = 0;
+      std::vector<uint64_t> perm;   // ts_shuffle: row i of the row group takes sorted timestamp perm[i]
+      if (cs.kind == TS && sp.ts_shuffle) {
+        perm.resize(nrows);
+        for (uint64_t i = 0; i < nrows; i++) perm[i] = i;
+        for (uint64_t i = nrows; i > 1; i--) std::swap(perm[i - 1], perm[rng.next() % i]);
+      }
       for (uint64_t p = 0; p < nrows; p += prow) {
         uint64_t pe = std::min<uint64_t>(nrows, p + prow);
         std::vector<uint8_t> page;
@@ -261,7 +269,7 @@ void build_rg(const lk_synth_spec& sp, const std::vector<ColSpec>& cols, uint64_
         uint8_t* dst = page.data() + base;
         size_t nv = 0;
         for (uint64_t i = p; i < pe; i++) {
-          uint64_t g = row0 + i;
+          uint64_t g = row0 + (perm.empty() ? i : perm[i]);
           if (cs.kind == TS) {
             int64_t t = sp.t0_ms + int64_t((unsigned __int128)g * uint64_t(sp.span_ms) / sp.rows);
             memcpy(dst + 8 * nv++, &t, 8);
