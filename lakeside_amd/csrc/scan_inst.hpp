@@ -34,7 +34,9 @@ static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
       case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true, HASH, true>), grid, block, 0, st, P); return;
       case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true, HASH, true>), grid, block, 0, st, P); return;
       case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true, HASH, true>), grid, block, 0, st, P); return;
-      default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH, true>), grid, block, 0, st, P); return;
+      case 6: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH, true>), grid, block, 0, st, P); return;
+      case 7: hipLaunchKernelGGL((scan_tiles<AGG, 7, true, HASH, true>), grid, block, 0, st, P); return;
+      default: hipLaunchKernelGGL((scan_tiles<AGG, 8, true, HASH, true>), grid, block, 0, st, P); return;
     }
     }
   }
@@ -44,7 +46,9 @@ static void launch_agg(const QParams& P, dim3 grid, hipStream_t st) {
     case 3: hipLaunchKernelGGL((scan_tiles<AGG, 3, true, HASH>), grid, block, 0, st, P); break;
     case 4: hipLaunchKernelGGL((scan_tiles<AGG, 4, true, HASH>), grid, block, 0, st, P); break;
     case 5: hipLaunchKernelGGL((scan_tiles<AGG, 5, true, HASH>), grid, block, 0, st, P); break;
-    default: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH>), grid, block, 0, st, P); break;
+    case 6: hipLaunchKernelGGL((scan_tiles<AGG, 6, true, HASH>), grid, block, 0, st, P); break;
+    case 7: hipLaunchKernelGGL((scan_tiles<AGG, 7, true, HASH>), grid, block, 0, st, P); break;
+    default: hipLaunchKernelGGL((scan_tiles<AGG, 8, true, HASH>), grid, block, 0, st, P); break;
   }
 }
 
