@@ -15,10 +15,14 @@ TXLIB   = lakeside_amd/liblakeside_text.so
 
 HOST_SRCS = $(SRC)/numleaf.cpp $(SRC)/exemplar.cpp $(SRC)/jdtoa.cpp $(SRC)/ddsketch.cpp $(SRC)/hll.cpp $(SRC)/regex.cpp $(SRC)/codec.cpp $(SRC)/parquet.cpp $(SRC)/plan.cpp $(SRC)/loader.cpp $(SRC)/engine.cpp $(SRC)/eval.cpp $(SRC)/dims.cpp $(SRC)/comm.cpp $(SRC)/abi.cpp
 HOST_OBJS = $(patsubst $(SRC)/%.cpp,$(OBJDIR)/%.o,$(HOST_SRCS))
-HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(OBJDIR)/scan_sum.o $(OBJDIR)/scan_min.o $(OBJDIR)/scan_max.o $(OBJDIR)/scan_count.o
+# the fused scan kernels: one unit per (aggregate, kernel family, table mode) so they compile in parallel
+SCAN_LEAN  = $(foreach a,sum min max count,$(foreach m,d h,$(OBJDIR)/scan_$(a)_lean_$(m).o))
+SCAN_TILES = $(foreach a,sum min max count,$(foreach m,d h,$(OBJDIR)/scan_$(a)_tiles_$(m).o))
+HIP_OBJS  = $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_LEAN) $(SCAN_TILES)
 HDRS = $(wildcard $(SRC)/*.hpp) $(SRC)/unicode_tables.inc include/lakeside_gpu.h include/lakeside_regex.h
-# device code includes only these (host-only header edits do not rebuild the kernels)
-DEV_HDRS = $(SRC)/device_common.hpp $(SRC)/kernels.hpp $(SRC)/layout.hpp $(SRC)/scan_inst.hpp $(SRC)/scan_kernel.hpp $(SRC)/lean_kernel.hpp
+# device code includes only these (host-only header edits do not rebuild the kernels); lean_kernel.hpp only the
+# scan_lean units, scan_kernel.hpp only the scan units
+DEV_HDRS = $(SRC)/device_common.hpp $(SRC)/kernels.hpp $(SRC)/layout.hpp $(SRC)/scan_inst.hpp
 
 all: $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
 
@@ -29,6 +33,9 @@ $(OBJDIR)/%.o: $(SRC)/%.cpp $(HDRS)
 $(OBJDIR)/%.o: $(SRC)/%.hip $(DEV_HDRS)
 	@mkdir -p $(OBJDIR)
 	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(SCAN_TILES): $(SRC)/scan_kernel.hpp
+$(SCAN_LEAN): $(SRC)/scan_kernel.hpp $(SRC)/lean_kernel.hpp
 
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
 	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
@@ -48,7 +55,7 @@ $(SYNTH): tools/synth.cpp $(SRC)/thrift.hpp
 asm: $(SRC)/kernels.hip $(HDRS)
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) --cuda-device-only -S $< -o build/kernels.s
-	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(SRC)/scan_$$a.hip -o build/scan_$$a.s; done
+	for a in sum min max count; do for f in lean tiles; do $(HIPCC) $(HIPFLAGS) --cuda-device-only -S $(SRC)/scan_$${a}_$${f}_d.hip -o build/scan_$${a}_$${f}_d.s; done; done
 
 clean:
 	rm -rf build $(LIB) $(SYNTH) $(RELIB) $(TXLIB)
@@ -64,13 +71,14 @@ $(CPULIB): oracle/cpu/lkcpu.cpp
 all: $(CPULIB)
 
 # Kernel A/B builds (experiments): the library with the scan kernels built under EXP_FLAGS (e.g.
-# EXP_FLAGS=-DLK_LEAN_ROWS=4 EXP_NAME=rows4) -> lakeside_amd/exp/liblakeside_gpu_<EXP_NAME>.so, selected with LK_LIB_PATH.
+# EXP_FLAGS=-DLK_LEAN_ROWS=4 EXP_NAME=rows4; the scan_lean units only) -> lakeside_amd/exp/liblakeside_gpu_<EXP_NAME>.so,
+# selected with LK_LIB_PATH.
 EXP_FLAGS ?=
 EXP_NAME ?= x
-exp: $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o
+exp: $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES)
 	@mkdir -p build/exp/$(EXP_NAME) lakeside_amd/exp
-	for a in sum min max count; do $(HIPCC) $(HIPFLAGS) $(EXP_FLAGS) -c $(SRC)/scan_$$a.hip -o build/exp/$(EXP_NAME)/scan_$$a.o & done; wait
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_$(EXP_NAME).so $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o build/exp/$(EXP_NAME)/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+	for a in sum min max count; do for m in d h; do $(HIPCC) $(HIPFLAGS) $(EXP_FLAGS) -c $(SRC)/scan_$${a}_lean_$${m}.hip -o build/exp/$(EXP_NAME)/scan_$${a}_lean_$${m}.o & done; done; wait
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_$(EXP_NAME).so $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES) build/exp/$(EXP_NAME)/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
 .PHONY: exp
 
 # Host-only loader harness (no HIP): the Parquet walk, dictionary interning and staging copy of lakeside_amd/csrc/

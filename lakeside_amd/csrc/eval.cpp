@@ -240,13 +240,13 @@ enum Redo : unsigned { REDO_METRICS_RAW = 1u, REDO_MIN_APART = 2u };
 constexpr unsigned long long kTsRunsMinKeys = 1ull << 18;   // output key spaces this large (C5: 10M keys)
 constexpr uint64_t kTsRunsMaxBuckets = 1u << 16;            // bucket_pos entries (mapped pinned memory)
 
-void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F) {
+void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F, int threads) {
   if (!nrows) return;
   const uint32_t* bp = F.bucket_pos;
   const uint64_t nb = F.nbuckets;
   const size_t piece = size_t(1) << 19;
   const size_t npieces = (nrows + piece - 1) / piece;
-  parallel_for(npieces, int(std::min<size_t>(npieces, 8)), [&](size_t p) {
+  parallel_for(npieces, int(std::min<size_t>(npieces, size_t(threads))), [&](size_t p) {
     const size_t lo = p * piece, hi = std::min(nrows, lo + piece);
     // the bucket of row lo: the last bucket starting at or before it
     uint64_t b = uint64_t(std::upper_bound(bp, bp + nb, uint32_t(lo)) - bp);
@@ -264,12 +264,12 @@ void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F) {
 // order, so row r's key -- and from it the timestamp, group id and glob -- follow from the bits alone.  Pieces of 2^20
 // keys: counts, a prefix, then every piece expanded on its own thread.
 void expand_rows_from_keys(int64_t* ts, uint32_t* gid, uint32_t* glob, const unsigned long long* bits,
-                           const FParams& F, bool per_glob) {
+                           const FParams& F, bool per_glob, int threads_max) {
   const uint64_t words = (F.nkeys + 63) / 64;
   constexpr uint64_t kPiece = uint64_t(1) << 14;   // words per piece
   const size_t np = size_t((words + kPiece - 1) / kPiece);
   std::vector<size_t> base(np + 1, 0);
-  const int threads = int(std::min<size_t>(np, 8));
+  const int threads = int(std::min<size_t>(np, size_t(threads_max)));
   parallel_for(np, threads, [&](size_t p) {
     size_t c = 0;
     for (uint64_t w = p * kPiece; w < std::min(words, (p + 1) * kPiece); w++) c += size_t(__builtin_popcountll(bits[w]));
@@ -1831,7 +1831,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         if (Fs.bucket_pos) {   // timestamps expanded here while finalize_write's rows cross the host link
           HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
           HIP_TRY(hipEventSynchronize(X->ev_rows));
-          expand_ts_runs(res->ts, Fs.bucket_pos[nbuckets], Fs);
+          expand_ts_runs(res->ts, Fs.bucket_pos[nbuckets], Fs, E.load_thread_count());
           HIP_TRY(hipStreamSynchronize(st));
           memcpy(&plan_bytes, fl + 2, 8);
           return fl[0];
@@ -2369,9 +2369,11 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     }
     if (ts_runs) {   // timestamps expanded here while finalize_write's rows cross the host link
       HIP_TRY(hipEventSynchronize(X->ev_rows));
-      expand_ts_runs(res->ts, nrows_out, F);
+      expand_ts_runs(res->ts, nrows_out, F, E.load_thread_count());
     }
-    if (key_rows) expand_rows_from_keys(res->ts, res->gid, per_glob_rows ? res->glob : nullptr, F.key_bits, F, per_glob_rows);
+    if (key_rows)
+      expand_rows_from_keys(res->ts, res->gid, per_glob_rows ? res->glob : nullptr, F.key_bits, F, per_glob_rows,
+                            E.load_thread_count());
     HIP_TRY(hipStreamSynchronize(st));
   }
   const double copy_ms = ms_since(t_start);

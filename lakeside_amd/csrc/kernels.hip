@@ -23,6 +23,7 @@
 
 #include "device_common.hpp"
 #include "kernels.hpp"
+#include "scan_inst.hpp"   // launch_scan_agg (host dispatch; the kernels live in the scan_*.hip units)
 #include "layout.hpp"
 
 #include <hipcub/device/device_radix_sort.hpp>

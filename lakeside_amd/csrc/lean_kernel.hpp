@@ -136,25 +136,7 @@ struct LeanLds {
   uint32_t wlist[LISTED ? BLOCK / 64 : 1][LISTED ? LIST : 1];   // each wave's passing rows
 };
 
-// The tile qualifies for scan_lean with `nl` late string columns (uniform: scalar loads).  scan_tiles applies the
-// same test to skip it.  Late columns (query columns 3 .. 2 + nl) must hold no NULL over the tile (value index =
-// row) or be absent from the segment.
-__device__ __forceinline__ bool lean_tile(const QSeg* Sp, uint32_t t, uint32_t nl, uint32_t rows_only) {
-  if (!Sp->cols[0].present || !Sp->cols[2].present) return false;
-  if (!Sp->cols[1].present && !rows_only) return false;   // COUNT(*) reads no value column
-  const TileCol* a = Sp->cols[0].tcols + t;
-  const TileCol* c = Sp->cols[2].tcols + t;
-  if (Sp->cols[1].present && Sp->cols[1].tcols[t].has_nulls) return false;
-  if (a->has_nulls || c->has_nulls || c->kind != PAGE_DICT || c->dict_n > 64u || c->nruns == 0u ||
-      c->bw < 1u || c->bw > 6u)
-    return false;
-  for (uint32_t k = 0; k < nl; k++) {
-    if (!Sp->cols[3 + k].present) continue;
-    const TileCol* l = Sp->cols[3 + k].tcols + t;
-    if (l->has_nulls || l->kind != PAGE_DICT || l->nruns == 0u || l->bw > 32u) return false;
-  }
-  return true;
-}
+// (lean_tile, the test of a tile scan_lean takes, is in device_common.hpp: scan_tiles applies it too)
 
 // Run of value v among `n` staged runs (+ sentinel) through a 64-value-block table (blk[b]: run holding vbase + 64b).
 __device__ __forceinline__ int lean_find_run(const LRun* runs, const uint8_t* blk, uint32_t nb, uint32_t vbase,

@@ -1,0 +1,7 @@
+// scan_tiles instantiations for AGG_COUNT, hash-mode tables (see scan_inst.hpp).
+#define LK_INST_TILES
+#include "scan_inst.hpp"
+
+namespace lk {
+template void launch_tiles<AGG_COUNT, true>(const QParams& P, dim3 grid, hipStream_t st);
+}  // namespace lk

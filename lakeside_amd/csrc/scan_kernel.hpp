@@ -140,7 +140,9 @@ __device__ __forceinline__ void lds_merge(LT& L, const QParams& P, const Acc& a)
 
 }  // namespace lk
 
-#include "lean_kernel.hpp"   // scan_lean (uses lds_merge); lean_tile for the split
+#ifdef LK_INST_LEAN
+#include "lean_kernel.hpp"   // scan_lean (uses lds_merge); its units only (scan_inst.hpp)
+#endif
 
 namespace lk {
 
