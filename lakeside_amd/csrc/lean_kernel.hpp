@@ -106,7 +106,7 @@ struct LeanHash {           // hash mode: the LDS hash table (lds_merge's layout
   uint32_t hfull;
 };
 
-template <int NL>
+template <int NL, bool LISTED_>
 struct LeanLds {
   static constexpr int NLA = NL > 0 ? NL : 1;
   static constexpr uint32_t RW = lean_dir_words(NL);
@@ -132,7 +132,9 @@ struct LeanLds {
   uint32_t llut[NLA][NL > 0 ? LUT_CAP : 1];
   uint32_t ltruth[NL > 0 ? (1u << (2 * TT_MAX_LEAVES)) / 32 : 1];
   uint32_t lines_l[NLA][NL > 0 ? LEAN_LLINES : 1];     // plan bytes only: late stream lines gathered
-  static constexpr bool LISTED = NL > 0 || LK_LEAN_LIST0;   // (NL = 0: the value-gathering shapes use it)
+  // the shapes that list their passing rows (NL > 0, and NL = 0 with a value gather outside the dense shape) hold a
+  // per-wave ring; the COUNT and dense-code NL = 0 shapes, which never list, keep its 8 KB of LDS
+  static constexpr bool LISTED = LISTED_;
   uint32_t wlist[LISTED ? BLOCK / 64 : 1][LISTED ? LIST : 1];   // each wave's passing rows
 };
 
@@ -182,7 +184,7 @@ template <int AGG, bool HASH, int NL, bool EARLY = false>
 // NL = 0 with EARLY (P.late_chunk set by the host when the filter passes a quarter or more of the name values: the
 // dense query): the per-lane loop and row-major dense blocks at 5 waves per SIMD, the shape those tiles measured best in
 __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (NL == 0 ? LK_LEAN_WAVES1 : 4) : LEAN_WAVES(NL, AGG)))) void scan_lean(QParams P) {
-  using LT = LeanLds<NL>;
+  using LT = LeanLds<NL, (NL > 0 || (LK_LEAN_LIST0 && AGG != AGG_COUNT && !EARLY))>;
   __shared__ LT L;
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -771,7 +773,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
   // until a full trip of LEAN_TRIP rows -- LEAN_ROWS per lane, every lane busy, all their late-column loads and then
   // all their value loads in flight together -- is ready, across the tile's rounds; the rest drains at the tile's end.
   uint32_t lhead = 0, ltail = 0;   // wave-uniform list positions (mod LEAN_LIST)
-  uint32_t* const wl = L.wlist[tid >> 6];
+  uint32_t* const wl = L.wlist[LT::LISTED ? (tid >> 6) : 0];
   auto list_trip = [&](auto ec, uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
     constexpr bool ELIST = decltype(ec)::value;   // entries carry complete group terms (early_late)
     if (P.ablate & 0x20000u) {   // diagnostics only: listed rows dropped unprocessed (the trips' cost)
@@ -1031,7 +1033,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
         }
       }
       constexpr bool LIST0 = NL == 0 && LK_LEAN_LIST0 && AGG != AGG_COUNT && !EARLY;
-      if (NL == 0 && (!LIST0 || dense_codes)) {   // uniform
+      if (!LT::LISTED || (NL == 0 && (!LIST0 || dense_codes))) {   // uniform
         // passing rows: two per trip (their loads in flight together)
         while (m) {
           const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
@@ -1049,7 +1051,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
           uint32_t dd[2] = {d1, d2};
           rowsN(std::integral_constant<int, 2>{}, std::false_type{}, rr, aa, dd);
         }
-      } else {
+      } else if constexpr (LT::LISTED) {
         // Late columns: the wave's passing rows are appended to its LDS list (lane-major) and processed LEAN_TRIP at
         // a time (list_trip) -- a per-lane loop would run as many trips as the lane with the most passing rows, each
         // a chain of dependent late-column and value loads.
@@ -1178,7 +1180,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
         }
       }
     }
-    if constexpr (NL > 0 || (LK_LEAN_LIST0 && AGG != AGG_COUNT)) {
+    if constexpr (LT::LISTED) {
       while (ltail != lhead) list_trip(ec, min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
       wave_sync();
     }

@@ -325,24 +325,38 @@ void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32
     d.nvals = nvals;
     if (col.is_string) {
       uint32_t page_remap = 0, page_dict_n = dict_n;
-      if (st.encoding == pq::PLAIN) {
-        // PLAIN BYTE_ARRAY page (a writer's dictionary fallback, or no dictionary at all): the page gets its own
-        // dictionary -- its distinct values in first-seen order, interned with the chunk -- and its values are
-        // re-encoded as one bit-packed literal run of indices, so the kernels see a dictionary page.
+      if (st.encoding == pq::PLAIN || st.encoding == pq::DELTA_LENGTH_BYTE_ARRAY || st.encoding == pq::DELTA_BYTE_ARRAY) {
+        // PLAIN BYTE_ARRAY page (a writer's dictionary fallback, or no dictionary at all), or its DELTA_LENGTH_BYTE_ARRAY
+        // / DELTA_BYTE_ARRAY forms (decoded here; the rebuilt DELTA_BYTE_ARRAY values are held with the chunk): the
+        // page gets its own dictionary -- its distinct values in first-seen order, interned with the chunk -- and its
+        // values are re-encoded as one bit-packed literal run of indices, so the kernels see a dictionary page.
+        std::vector<pq::ByteView> vals;
+        if (st.encoding == pq::PLAIN) {
+          vals.reserve(nvals);
+          size_t p = 0;
+          for (uint32_t i = 0; i < nvals; i++) {
+            if (p + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY page in " + col.name);
+            uint32_t L;
+            memcpy(&L, st.vals + p, 4);
+            p += 4;
+            if (p + L > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY value in " + col.name);
+            vals.push_back(pq::ByteView{st.vals + p, L});
+            p += L;
+          }
+        } else if (st.encoding == pq::DELTA_LENGTH_BYTE_ARRAY) {
+          pq::delta_length_decode(st.vals, st.vals_len, nvals, vals);
+        } else {
+          C.plain.push_back(std::make_unique<std::vector<uint8_t>>());
+          pq::delta_byte_array_decode(st.vals, st.vals_len, nvals, *C.plain.back(), vals);
+        }
         std::unordered_map<std::string_view, uint32_t> local;
         std::vector<uint32_t> idx(nvals);
         page_remap = uint32_t(C.dict.size());
-        size_t p = 0;
         for (uint32_t i = 0; i < nvals; i++) {
-          if (p + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY page in " + col.name);
-          uint32_t L;
-          memcpy(&L, st.vals + p, 4);
-          p += 4;
-          if (p + L > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: truncated PLAIN BYTE_ARRAY value in " + col.name);
-          auto ins = local.emplace(std::string_view(reinterpret_cast<const char*>(st.vals + p), L), uint32_t(local.size()));
+          auto ins = local.emplace(std::string_view(reinterpret_cast<const char*>(vals[i].p), vals[i].len),
+                                   uint32_t(local.size()));
           if (ins.second) C.dict.emplace_back(ins.first->first);
           idx[i] = ins.first->second;
-          p += L;
         }
         page_dict_n = uint32_t(local.size());
         int pbw = 1;
@@ -410,6 +424,43 @@ void walk_column_chunk(const uint8_t* F, size_t size, const HostCol& col, uint32
           if (idx[i] >= dict_n) throw PlanError(LK_ERR_IO, "parquet: dictionary index out of range in " + col.name);
           memcpy(out.data() + size_t(i) * width, ndict.data() + size_t(idx[i]) * width, width);
         }
+        st.vals = out.data();
+        st.vals_len = out.size();
+      } else if (st.encoding == pq::DELTA_BINARY_PACKED && (col.ptype == pq::INT32 || col.ptype == pq::INT64)) {
+        // DELTA_BINARY_PACKED integers (e.g. a writer's sorted timestamps): materialized to PLAIN here
+        std::vector<int64_t> v(nvals);
+        pq::delta_binary_decode(st.vals, st.vals_len, nvals, col.ptype == pq::INT32 ? 32 : 64, v.data());
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>(size_t(nvals) * width));
+        std::vector<uint8_t>& out = *C.plain.back();
+        for (uint32_t i = 0; i < nvals; i++) {
+          if (width == 8) {
+            memcpy(out.data() + size_t(i) * 8, &v[i], 8);
+          } else {
+            const int32_t x = int32_t(v[i]);
+            memcpy(out.data() + size_t(i) * 4, &x, 4);
+          }
+        }
+        st.vals = out.data();
+        st.vals_len = out.size();
+      } else if (st.encoding == pq::BYTE_STREAM_SPLIT && width) {
+        // BYTE_STREAM_SPLIT (FLOAT / DOUBLE, and INT32 / INT64 in format 2.11): the byte streams interleaved back
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>(size_t(nvals) * width));
+        pq::byte_stream_split_decode(st.vals, st.vals_len, nvals, width, C.plain.back()->data());
+        st.vals = C.plain.back()->data();
+        st.vals_len = C.plain.back()->size();
+      } else if (st.encoding == pq::RLE && width == 0) {
+        // RLE BOOLEAN values (data page v2 writers): a 4-byte length, then the hybrid stream at bit width 1 -> the
+        // PLAIN bit-packed layout (LSB first)
+        if (st.vals_len < 4) throw PlanError(LK_ERR_IO, "parquet: truncated RLE BOOLEAN page in " + col.name);
+        uint32_t L;
+        memcpy(&L, st.vals, 4);
+        if (size_t(L) + 4 > st.vals_len) throw PlanError(LK_ERR_IO, "parquet: bad RLE BOOLEAN length in " + col.name);
+        std::vector<uint32_t> b(nvals);
+        pq::hybrid_decode(st.vals + 4, L, 1, nvals, b.data());
+        C.plain.push_back(std::make_unique<std::vector<uint8_t>>((size_t(nvals) + 7) / 8, 0));
+        std::vector<uint8_t>& out = *C.plain.back();
+        for (uint32_t i = 0; i < nvals; i++)
+          if (b[i]) out[i >> 3] |= uint8_t(1u << (i & 7));
         st.vals = out.data();
         st.vals_len = out.size();
       } else if (st.encoding != pq::PLAIN) {

@@ -269,5 +269,126 @@ uint32_t hybrid_literal_max(const uint8_t* d, size_t avail, int bw, uint32_t cou
   return mx;
 }
 
+
+// ---- value encodings materialized at load (parquet-format Encodings.md) ----
+namespace {
+struct Reader {
+  const uint8_t* p;
+  const uint8_t* end;
+  uint64_t uleb() {
+    uint64_t v = 0;
+    for (int sh = 0; sh < 64; sh += 7) {
+      if (p >= end) throw std::runtime_error("parquet: truncated DELTA header");
+      const uint8_t b = *p++;
+      v |= uint64_t(b & 0x7f) << sh;
+      if (!(b & 0x80)) return v;
+    }
+    throw std::runtime_error("parquet: bad varint in a DELTA stream");
+  }
+  int64_t zigzag() {
+    const uint64_t u = uleb();
+    return int64_t(u >> 1) ^ -int64_t(u & 1);
+  }
+};
+}  // namespace
+
+size_t delta_binary_decode(const uint8_t* p, size_t len, size_t n, int bits, int64_t* out) {
+  Reader r{p, p + len};
+  const uint64_t block = r.uleb(), nmini = r.uleb(), total = r.uleb();
+  int64_t prev = r.zigzag();
+  if (block == 0 || block % 128 || nmini == 0 || block % nmini || (block / nmini) % 32)
+    throw std::runtime_error("parquet: bad DELTA_BINARY_PACKED block layout");
+  if (total < n) throw std::runtime_error("parquet: DELTA_BINARY_PACKED page holds fewer values than its rows");
+  const uint64_t per_mini = block / nmini;
+  const uint64_t mask = bits == 32 ? 0xffffffffull : ~0ull;
+  auto wrap = [&](uint64_t v) -> int64_t {   // the column's width: INT32 sign-extends its low 32 bits
+    return bits == 32 ? int64_t(int32_t(uint32_t(v & mask))) : int64_t(v);
+  };
+  size_t i = 0;
+  if (n) out[i++] = wrap(uint64_t(prev));
+  while (i < n) {
+    const uint64_t min_delta = uint64_t(r.zigzag());
+    if (uint64_t(r.end - r.p) < nmini) throw std::runtime_error("parquet: truncated DELTA_BINARY_PACKED block");
+    const uint8_t* widths = r.p;
+    r.p += nmini;
+    for (uint64_t m = 0; m < nmini && i < n; m++) {
+      const int w = widths[m];
+      if (w > 64) throw std::runtime_error("parquet: bad DELTA_BINARY_PACKED bit width");
+      const uint64_t bytes = per_mini * uint64_t(w) / 8;
+      if (uint64_t(r.end - r.p) < bytes) throw std::runtime_error("parquet: truncated DELTA_BINARY_PACKED miniblock");
+      const uint8_t* d = r.p;
+      for (uint64_t k = 0; k < per_mini && i < n; k++) {
+        uint64_t v = 0;
+        if (w) {   // LSB-first, bit k * w .. k * w + w - 1
+          const uint64_t bit = k * uint64_t(w);
+          unsigned __int128 acc = 0;
+          const uint64_t b0 = bit >> 3, nb = (uint64_t(bit & 7) + uint64_t(w) + 7) / 8;
+          for (uint64_t j = 0; j < nb; j++) acc |= (unsigned __int128)d[b0 + j] << (8 * j);
+          v = uint64_t(acc >> (bit & 7));
+          if (w < 64) v &= (uint64_t(1) << w) - 1;
+        }
+        prev = int64_t(uint64_t(prev) + min_delta + v);   // two's-complement wrap, then the column's width
+        prev = wrap(uint64_t(prev));
+        out[i++] = prev;
+      }
+      r.p += bytes;
+    }
+  }
+  return size_t(r.p - p);
+}
+
+size_t delta_length_decode(const uint8_t* p, size_t len, size_t n, std::vector<ByteView>& views) {
+  std::vector<int64_t> lens(n);
+  size_t pos = n ? delta_binary_decode(p, len, n, 32, lens.data()) : 0;
+  if (!n) {   // an empty page still carries a (value-less) header
+    Reader r{p, p + len};
+    if (len) {
+      r.uleb(), r.uleb(), r.uleb(), r.zigzag();
+      pos = size_t(r.p - p);
+    }
+  }
+  views.clear();
+  views.reserve(n);
+  for (size_t i = 0; i < n; i++) {
+    if (lens[i] < 0 || uint64_t(lens[i]) > len - pos) throw std::runtime_error("parquet: truncated DELTA_LENGTH_BYTE_ARRAY");
+    views.push_back(ByteView{p + pos, uint32_t(lens[i])});
+    pos += size_t(lens[i]);
+  }
+  return pos;
+}
+
+void delta_byte_array_decode(const uint8_t* p, size_t len, size_t n, std::vector<uint8_t>& store,
+                             std::vector<ByteView>& views) {
+  std::vector<int64_t> pre(n);
+  const size_t used = n ? delta_binary_decode(p, len, n, 32, pre.data()) : 0;
+  std::vector<ByteView> suf;
+  delta_length_decode(p + used, len - used, n, suf);
+  size_t total = 0, last = 0;
+  for (size_t i = 0; i < n; i++) {
+    if (pre[i] < 0 || uint64_t(pre[i]) > last) throw std::runtime_error("parquet: bad DELTA_BYTE_ARRAY prefix length");
+    last = size_t(pre[i]) + suf[i].len;
+    total += last;
+  }
+  store.clear();
+  store.reserve(total);
+  views.clear();
+  views.reserve(n);
+  for (size_t i = 0; i < n; i++) {   // (reserved: no reallocation, so earlier views stay valid)
+    const size_t at = store.size(), pl = size_t(pre[i]);   // pre[0] == 0 (checked above)
+    store.resize(at + pl + suf[i].len);
+    if (pl) memcpy(store.data() + at, views[i - 1].p, pl);
+    if (suf[i].len) memcpy(store.data() + at + pl, suf[i].p, suf[i].len);
+    views.push_back(ByteView{store.data() + at, uint32_t(pl + suf[i].len)});
+  }
+}
+
+void byte_stream_split_decode(const uint8_t* p, size_t len, size_t n, size_t width, uint8_t* out) {
+  if (len < n * width) throw std::runtime_error("parquet: truncated BYTE_STREAM_SPLIT page");
+  for (size_t k = 0; k < width; k++) {
+    const uint8_t* s = p + k * n;
+    for (size_t i = 0; i < n; i++) out[i * width + k] = s[i];
+  }
+}
+
 }  // namespace pq
 }  // namespace lk

