@@ -148,6 +148,20 @@ struct Engine {
   // hardware threads, at most 16) and the pinned staging area its upload goes through (under dev_mu).
   int load_threads = 0;
   int load_thread_count() const;
+  // Result-path host work (large results' rows expanded on the host while their values cross the link): a persistent
+  // pool of load_thread_count() threads, created on first use; a call that finds it busy spawns its own threads.
+  std::unique_ptr<WorkerPool> result_pool;
+  std::mutex result_pool_mu;
+  template <class F>
+  void host_parallel(size_t n, F&& fn) {
+    WorkerPool* p;
+    {
+      std::lock_guard<std::mutex> g(result_pool_mu);
+      if (!result_pool) result_pool = std::make_unique<WorkerPool>(load_thread_count());
+      p = result_pool.get();
+    }
+    if (!p->try_run(n, fn)) parallel_for(n, p->threads(), fn);
+  }
   void* load_pinned = nullptr;
   size_t load_pinned_cap = 0;
   hipStream_t load_stream = nullptr;

@@ -240,13 +240,13 @@ enum Redo : unsigned { REDO_METRICS_RAW = 1u, REDO_MIN_APART = 2u };
 constexpr unsigned long long kTsRunsMinKeys = 1ull << 18;   // output key spaces this large (C5: 10M keys)
 constexpr uint64_t kTsRunsMaxBuckets = 1u << 16;            // bucket_pos entries (mapped pinned memory)
 
-void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F, int threads) {
+void expand_ts_runs(Engine& E, int64_t* ts, size_t nrows, const FParams& F) {
   if (!nrows) return;
   const uint32_t* bp = F.bucket_pos;
   const uint64_t nb = F.nbuckets;
   const size_t piece = size_t(1) << 19;
   const size_t npieces = (nrows + piece - 1) / piece;
-  parallel_for(npieces, int(std::min<size_t>(npieces, size_t(threads))), [&](size_t p) {
+  E.host_parallel(npieces, [&](size_t p) {
     const size_t lo = p * piece, hi = std::min(nrows, lo + piece);
     // the bucket of row lo: the last bucket starting at or before it
     uint64_t b = uint64_t(std::upper_bound(bp, bp + nb, uint32_t(lo)) - bp);
@@ -263,21 +263,20 @@ void expand_ts_runs(int64_t* ts, size_t nrows, const FParams& F, int threads) {
 // Rows of a large result from its output keys' existence bits (FParams::key_bits): rows are the existing keys in key
 // order, so row r's key -- and from it the timestamp, group id and glob -- follow from the bits alone.  Pieces of 2^20
 // keys: counts, a prefix, then every piece expanded on its own thread.
-void expand_rows_from_keys(int64_t* ts, uint32_t* gid, uint32_t* glob, const unsigned long long* bits,
-                           const FParams& F, bool per_glob, int threads_max) {
+void expand_rows_from_keys(Engine& E, int64_t* ts, uint32_t* gid, uint32_t* glob, const unsigned long long* bits,
+                           const FParams& F, bool per_glob) {
   const uint64_t words = (F.nkeys + 63) / 64;
   constexpr uint64_t kPiece = uint64_t(1) << 14;   // words per piece
   const size_t np = size_t((words + kPiece - 1) / kPiece);
   std::vector<size_t> base(np + 1, 0);
-  const int threads = int(std::min<size_t>(np, size_t(threads_max)));
-  parallel_for(np, threads, [&](size_t p) {
+  E.host_parallel(np, [&](size_t p) {
     size_t c = 0;
     for (uint64_t w = p * kPiece; w < std::min(words, (p + 1) * kPiece); w++) c += size_t(__builtin_popcountll(bits[w]));
     base[p + 1] = c;
   });
   for (size_t p = 0; p < np; p++) base[p + 1] += base[p];
   const uint64_t ng = F.ngroups, ns = F.nglob_slots ? F.nglob_slots : 1;
-  parallel_for(np, threads, [&](size_t p) {
+  E.host_parallel(np, [&](size_t p) {
     size_t r = base[p];
     for (uint64_t w = p * kPiece; w < std::min(words, (p + 1) * kPiece); w++) {
       unsigned long long x = bits[w];
@@ -508,8 +507,8 @@ static int evaluate_mixed_steps(Engine& E, const std::string& json, const Reques
 // Metrics percentiles (VERDICT r5 missing #1).  Each glob's SQL is
 //   SELECT ts, MAX(rollup_<rollup|sum>) AS value, name, <groupBys> ... GROUP BY ts, <groupBys>, name
 // (BaseExpr.scala:379-383), and the worker's PushDownAggregatorStage feeds every row's value (NULL -> 0.0, JDBC
-// getDouble) into the DDSketch of its (raw timestamp, key tags) -- the groupBys' tags, or {"name": v} without
-// groupBys (PushDownAggregatorStage.scala:56-60, 69-81, 188-197); query-api merges the sketches per (timestamp, tags)
+// getDouble) into the DDSketch of its (raw timestamp, key tags) -- the groupBys' tags, or {"_cardinalhq.name": ""}
+// without groupBys (PushDownAggregatorStage.scala:56-60, 69-81, 188-197); query-api merges the sketches per (timestamp, tags)
 // (TimeGroupedSketchAggregator.scala:34-37).  Here the per-glob MAX rows come from the GPU scan (the metrics MAX
 // path with per-glob cells, every rank's partial table folded on rank 0 when distributed) and the host builds the
 // sketches from those rows -- O(output rows), as the logs path assembles its sketches from the kernel's bins.
@@ -551,10 +550,9 @@ static int evaluate_metrics_pct(Engine& E, const std::string& json, const Reques
         if (kv.first == k) return &kv.second;
       return nullptr;
     };
-    Tags kt;   // getGroupByKeyTags
+    Tags kt;   // getGroupByKeyTags: no groupBys -> {"_cardinalhq.name": ""} (the name tag is labelled `name`)
     if (by_name) {
-      const std::string* nm = get("name");
-      kt.emplace_back("name", nm ? *nm : std::string());
+      kt.emplace_back(kName, std::string());
     } else {
       for (auto& g : R.group_bys)
         if (const std::string* v = get(g))
@@ -562,12 +560,9 @@ static int evaluate_metrics_pct(Engine& E, const std::string& json, const Reques
       std::sort(kt.begin(), kt.end());
     }
     const uint32_t glob = per_glob_rows ? r.glob[i] : 0u;
-    // merged without groupBys: one sketch per timestamp whose tags are one input's (here: the smallest name)
-    Tags key = (!per_glob_rows && by_name) ? Tags{} : kt;
-    auto ins = at.emplace(std::make_tuple(r.ts[i], glob, key), rows.size());
+    auto ins = at.emplace(std::make_tuple(r.ts[i], glob, kt), rows.size());
     if (ins.second) rows.push_back(Row{r.ts[i], glob, kt, dd::Sketch{}});
     Row& o = rows[ins.first->second];
-    if (!per_glob_rows && by_name && kt[0].second < o.tags[0].second) o.tags = kt;
     // DDSketch.accept throws on NaN / an untrackable magnitude: the worker's stream fails (Commons.scala:331-335)
     if (!o.sk.accept(r.val[i])) throw PlanError(LK_ERR_ARG, "DDSketch: value outside the trackable range");
   }
@@ -1497,9 +1492,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   const size_t o_bpos = reserve(ts_runs_ok ? (size_t(nbuckets) + 1) * 4 : 0);
   // host side only (mapped): the existence bit of every output key of a large grouped result (FParams::key_bits)
   const uint64_t okeys = per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups);
-  // opt-in (LK_KEY_ROWS=1): measured slower on C5 (eval 2.28 vs 2.13 ms) -- the host's 68 MB of row writes take
-  // longer than the 23 MB of group ids they keep off the host link
-  const bool key_rows_ok = !collapse && okeys >= kTsRunsMinKeys && getenv("LK_KEY_ROWS") && *getenv("LK_KEY_ROWS") == '1';
+  // default since r06 (LK_NO_KEY_ROWS=1 for A/B): with the row expansion on the job's whole thread share (a persistent
+  // pool) it runs while the values cross the host link -- C5 eval 2.64 -> 1.93 ms (profiles/r06_ab_c5_*); r05's
+  // 8-thread expansion measured slower (2.28 vs 2.13 ms)
+  const bool key_rows_ok = !collapse && okeys >= kTsRunsMinKeys && !getenv("LK_NO_KEY_ROWS");
   const size_t o_kbits = reserve(key_rows_ok ? size_t((okeys + 2047) / 2048) * 2048 / 8 : 0);
   // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)
   uint8_t* hbuf = nullptr;
@@ -1831,7 +1827,7 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         if (Fs.bucket_pos) {   // timestamps expanded here while finalize_write's rows cross the host link
           HIP_TRY(hipMemcpyAsync(fl, P.flags, 16, hipMemcpyDeviceToHost, st));
           HIP_TRY(hipEventSynchronize(X->ev_rows));
-          expand_ts_runs(res->ts, Fs.bucket_pos[nbuckets], Fs, E.load_thread_count());
+          expand_ts_runs(E, res->ts, Fs.bucket_pos[nbuckets], Fs);
           HIP_TRY(hipStreamSynchronize(st));
           memcpy(&plan_bytes, fl + 2, 8);
           return fl[0];
@@ -2060,16 +2056,14 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   uint32_t* d_counts = nullptr;
   void* sws = nullptr;
   unsigned long long nocc = 0;
-  // Percentiles: one DDSketch per (glob, step, group-key tags) -- the groupBys' values, or {"name": v} without
-  // groupBys (PushDownAggregatorStage.getGroupByKeyTags, 188-197); NULL / "null" / "" values drop out of the tags
-  // (Commons.scala:433).  Merged: per (step, tags), or per step without groupBys (SimpleSketchMerger: one sketch,
-  // tags of one input -- here the smallest name).
+  // Percentiles: one DDSketch per (glob, step, group-key tags) -- the groupBys' values, or {"_cardinalhq.name": ""}
+  // without groupBys (PushDownAggregatorStage.getGroupByKeyTags, 188-197: see below); NULL / "null" / "" values drop
+  // out of the tags (Commons.scala:433).  Merged: per (step, tags).
   struct SkRow {
     int64_t ts;
     uint32_t glob;
     unsigned long long gid;
     dd::Sketch sk;
-    std::string name;   // merged without groupBys: the name of `gid` (the smallest seen)
   };
   std::vector<SkRow> sk_rows;
   struct CesRow {
@@ -2168,10 +2162,17 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
         StrCol& sc = strs[si];
         if (!sc.is_dim || !sc.stride) continue;
         const bool drop = si == 0 && !by_name && !name_grouped;   // name is no key tag when groupBys exist
+        if (drop) continue;   // the name is no key tag (its column is hidden): no group term
+        if (si == 0 && by_name) {
+          // no groupBys: getGroupByKeyTags reads `datapoint.tags.getOrElse(NAME, "")` with NAME = "_cardinalhq.name"
+          // (PushDownAggregatorStage.scala:188-197, Commons.scala:45), but the row's name tag is labelled `name` (the
+          // SQL's `"_cardinalhq.name" as name`): every row's key tags are {"_cardinalhq.name": ""} -- one sketch per
+          // step, every name in it: no group term (the tag column reads "" for every row: tcols[0] below).
+          continue;
+        }
         GlobalDict& gd = E.dict(sc.name);
         std::lock_guard<std::mutex> g(gd.mu);
         std::unordered_map<uint32_t, bool> nl;
-        if (drop) continue;   // the name is no key tag (its column is hidden): no group term
         for (size_t i = 0; i < nocc; i++) {
           uint32_t d = uint32_t((cellv[i] % ngroups) / sc.stride % sc.ndim);
           if (d != sc.dim_null) {
@@ -2182,34 +2183,15 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
           kg[i] += (unsigned long long)d * sc.stride;
         }
       }
-      // merged without groupBys: one sketch per step; its tags: the smallest name ("" for a NULL-like one)
-      std::vector<std::string> name_of;
-      if (!per_glob_rows && by_name) {
-        GlobalDict& gd = E.dict(kName);
-        std::lock_guard<std::mutex> g(gd.mu);
-        name_of.resize(nocc);
-        for (size_t i = 0; i < nocc; i++) {
-          const uint32_t d = uint32_t(kg[i] / strs[0].stride % strs[0].ndim);
-          if (d != strs[0].dim_null) name_of[i] = std::string(strs[0].dim_value(d, gd));
-        }
-      }
       std::map<std::tuple<uint64_t, uint32_t, unsigned long long>, size_t> at;   // (bucket, glob, key) -> row
       for (size_t i = 0; i < nocc; i++) {
         const unsigned long long cell = cellv[i];
         const uint64_t b = (cell / ngroups) % nbuckets;
         const uint32_t slot = uint32_t(cell / ngroups / nbuckets);
-        const unsigned long long key = (!per_glob_rows && by_name) ? 0ull : kg[i];
-        auto ins = at.emplace(std::make_tuple(b, per_glob_rows ? slot : 0u, key), sk_rows.size());
-        if (ins.second) {
-          sk_rows.push_back(SkRow{bucket_base + int64_t(b) * P.step, per_glob_rows ? slot : 0u, kg[i], dd::Sketch{},
-                                  name_of.empty() ? std::string() : name_of[i]});
-        }
-        SkRow& r = sk_rows[ins.first->second];
-        if (!name_of.empty() && kg[i] != r.gid && name_of[i] < r.name) {   // keep the smallest name's group term
-          r.gid = kg[i];
-          r.name = name_of[i];
-        }
-        r.sk.add_bin(uint32_t(keys[i] % DD_NBINS), double(cnts[i]));
+        auto ins = at.emplace(std::make_tuple(b, per_glob_rows ? slot : 0u, kg[i]), sk_rows.size());
+        if (ins.second)
+          sk_rows.push_back(SkRow{bucket_base + int64_t(b) * P.step, per_glob_rows ? slot : 0u, kg[i], dd::Sketch{}});
+        sk_rows[ins.first->second].sk.add_bin(uint32_t(keys[i] % DD_NBINS), double(cnts[i]));
       }
       std::vector<size_t> ord(sk_rows.size());
       for (size_t i = 0; i < ord.size(); i++) ord[i] = i;
@@ -2369,11 +2351,10 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
     }
     if (ts_runs) {   // timestamps expanded here while finalize_write's rows cross the host link
       HIP_TRY(hipEventSynchronize(X->ev_rows));
-      expand_ts_runs(res->ts, nrows_out, F, E.load_thread_count());
+      expand_ts_runs(E, res->ts, nrows_out, F);
     }
     if (key_rows)
-      expand_rows_from_keys(res->ts, res->gid, per_glob_rows ? res->glob : nullptr, F.key_bits, F, per_glob_rows,
-                            E.load_thread_count());
+      expand_rows_from_keys(E, res->ts, res->gid, per_glob_rows ? res->glob : nullptr, F.key_bits, F, per_glob_rows);
     HIP_TRY(hipStreamSynchronize(st));
   }
   const double copy_ms = ms_since(t_start);
@@ -2440,7 +2421,15 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
       m[d] = res->owned.back().c_str();
     }
   }
-  if (sketch && gbs.empty()) res->tcols[0].null_value = "";   // key tags {"name": ""} (getOrElse(NAME, ""))
+  if (sketch && gbs.empty()) {   // key tags {"_cardinalhq.name": ""} (getOrElse(NAME, ""): see the sketch rows above)
+    res->tag_names[0] = kName;
+    lk_result::TagCol& tc = res->tcols[0];
+    tc = lk_result::TagCol{};    // one dim id, whose text is ""
+    tc.ndim = 1;
+    tc.dim_null = 1;
+    res->owned.push_back(std::string());
+    tc.local.assign(1, res->owned.back().c_str());
+  }
   if (sketch && !gbs.empty()) res->tcols[0].hidden = true;     // key tags: the groupBys only
   if (ces)   // the HLL SketchInput carries no tags (Aggregator.scala:58)
     for (auto& tc : res->tcols) tc.hidden = true;

@@ -1077,10 +1077,13 @@ def is_percentile(agg: Optional[str]) -> bool:
 
 def _key_tags(pr: PushDownRequest, tags: Dict[str, str]) -> Dict[str, str]:
     """PushDownAggregatorStage.getGroupByKeyTags (PushDownAggregatorStage.scala:188-197) over the DataPoint's tags
-    (Commons.toDataPoint: NULL / "null" / "" dropped, Commons.scala:433)."""
+    (Commons.toDataPoint: NULL / "null" / "" dropped, Commons.scala:433).  Without groupBys it reads
+    `tags.getOrElse(NAME, "")` with NAME = "_cardinalhq.name" (Commons.scala:45), while the row's name tag is labelled
+    `name` (the SQL's `"_cardinalhq.name" as name`, BaseExpr.scala:397-399): the key tags are {"_cardinalhq.name": ""}
+    for every row -- one sketch per step."""
     gbs = pr.baseExpr.chart.groupBys
     if not gbs:
-        return {"name": tags.get("name", "")}
+        return {NAME: tags.get(NAME, "")}
     return {g: tags[g] for g in gbs if g in tags}
 
 
@@ -1114,19 +1117,16 @@ def evaluate_percentile_per_glob(pr: PushDownRequest, glob_size: int, paths: Seq
 
 
 def merge_percentile(pr: PushDownRequest, per_glob) -> List[Tuple[int, Dict[str, str], Any]]:
-    """query-api merge of DD sketches (TimeGroupedSketchAggregator.scala:34-37, 101-114): per (timestamp, tags) with
-    groupBys, else one sketch per timestamp whose tags are one input's (here: the smallest name)."""
+    """query-api merge of DD sketches (TimeGroupedSketchAggregator.scala:34-37, 101-114): per (timestamp, tags) (without
+    groupBys every key-tag map is {"_cardinalhq.name": ""}: one sketch per timestamp)."""
     from oracle import ddsketch
-    gbs = pr.baseExpr.chart.groupBys
     acc: Dict[Tuple, Tuple[Dict[str, str], Any]] = {}
     for rows in per_glob:
         for ts, kt, sk in rows:
-            key = (ts, tuple(sorted(kt.items()))) if gbs else (ts,)
+            key = (ts, tuple(sorted(kt.items())))
             if key not in acc:
                 acc[key] = (dict(kt), ddsketch.Sketch().merge(sk))
             else:
-                if not gbs and kt.get("name", "") < acc[key][0].get("name", ""):
-                    acc[key] = (dict(kt), acc[key][1])
                 acc[key][1].merge(sk)
     return [(k[0], acc[k][0], acc[k][1]) for k in sorted(acc)]
 

@@ -275,7 +275,7 @@ def test_merged_min_absorbs_all_nan_glob(engine, tmp_path):
 
 def _write_exotic(path, rng, hour):
     """clean columns + columns this engine does not decode: a struct, a list, an INT96 timestamp, a 16-byte
-    FIXED_LEN_BYTE_ARRAY, a DELTA_BINARY_PACKED int64 and a BROTLI-compressed double."""
+    FIXED_LEN_BYTE_ARRAY and a BROTLI-compressed double; and a DELTA_BINARY_PACKED int64 (decoded since r06)."""
     import pyarrow as pa
     import pyarrow.parquet as pq
     base = pq.read_table(_write(path, rng, hour))
@@ -299,9 +299,9 @@ def _write_exotic(path, rng, hour):
 
 def test_unloaded_columns_serve_other_queries(engine, tmp_path):
     """a file with columns this engine does not decode (nested struct / list, INT96,
-    FIXED_LEN_BYTE_ARRAY, DELTA_BINARY_PACKED, BROTLI) still serves every query that does not reference them (GPU ==
-    oracle); a query that references one fails the call with LK_ERR_UNSUPPORTED (the caller falls back) instead of
-    silently emptying the glob."""
+    FIXED_LEN_BYTE_ARRAY, BROTLI) still serves every query that does not reference them (GPU == oracle); a query that
+    references one fails the call with LK_ERR_UNSUPPORTED (the caller falls back) instead of silently emptying the
+    glob.  The DELTA_BINARY_PACKED column is decoded at load (r06): a numeric leaf on it equals the oracle."""
     from lakeside_amd import LK_MERGED, synth
     from lakeside_amd._lib import LK_ERR_UNSUPPORTED, LakesideError
     rng = np.random.default_rng(7)
@@ -309,9 +309,13 @@ def test_unloaded_columns_serve_other_queries(engine, tmp_path):
     req = synth.pushdown(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), _segs(2), "sum", [synth.SERVICE])
     cells, stats = _compare(engine, req, paths, 1, "sum", "exotic columns unreferenced")
     assert stats["failed_globs"] == 0 and cells[0] and cells[1], stats
+    delta = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_02"),
+             "q2": {"k": "delta_col", "v": ["500"], "op": "gt", "dataType": "number"}}
+    cells, stats = _compare(engine, synth.pushdown(delta, _segs(2), "max", [synth.SERVICE]), paths, 1, "max",
+                            "DELTA_BINARY_PACKED leaf")
+    assert cells[0] and cells[1], stats
     for col, leaf in [("uuid", synth.leaf("uuid", "eq", "x")), ("attrs", synth.leaf("attrs", "eq", "x")),
                       ("tags", synth.leaf("tags", "eq", "x")),
-                      ("delta_col", {"k": "delta_col", "v": ["5"], "op": "gt", "dataType": "number"}),
                       ("brot", {"k": "brot", "v": ["0.5"], "op": "lt", "dataType": "number"}),
                       ("ts96", {"k": "ts96", "v": ["5"], "op": "gt", "dataType": "number"})]:
         filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"), "q2": leaf}

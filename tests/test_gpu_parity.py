@@ -237,10 +237,15 @@ def test_window_cuts_tiles(engine):
     _synth_case(engine, 1, 1 << 21, 0, 0.0, filt, "count", [], step=3600000, window=(60000, 0))
 
 
-def test_c5_shape_high_cardinality_group_by(engine):
+@pytest.mark.parametrize("rows_mode", ["key_rows", "ts_runs"])
+def test_c5_shape_high_cardinality_group_by(engine, rows_mode, monkeypatch):
     """C5 shape: a high-cardinality group key (resource.container.id, 300k-value dictionary, ~2^18 distinct per
-    row group) over segments of one hour, 1h step: groups far beyond the LDS table spill to the global table."""
+    row group) over segments of one hour, 1h step: groups far beyond the LDS table spill to the global table.  Large
+    results cross the host link as values + key bits (default since r06) or values + group ids with the timestamps
+    expanded on the host (LK_NO_KEY_ROWS=1)."""
     from lakeside_amd import synth
+    if rows_mode == "ts_runs":
+        monkeypatch.setenv("LK_NO_KEY_ROWS", "1")
     filt = synth.leaf(synth.NAME, "eq", "metric_07")
     res = _synth_case(engine, 2, 1 << 20, 0, 0.0, filt, "sum", [synth.CONTAINER], step=3600000, highcard_n=300000,
                       hour=0)
@@ -252,11 +257,11 @@ def test_c5_shape_high_cardinality_group_by(engine):
     _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
 
 
-def test_large_result_rows_from_key_bits(engine, monkeypatch):
-    """LK_KEY_ROWS=1 (opt-in): a large grouped result's rows carry only their values over the host link; timestamps,
-    group ids and globs come from finalize_count's per-key existence bits -- per glob and merged, one and 60 buckets."""
+def test_large_result_rows_from_key_bits(engine):
+    """Key-bit rows (default since r06): a large grouped result's rows carry only their values over the host link;
+    timestamps, group ids and globs come from finalize_count's per-key existence bits -- per glob and merged, one and
+    60 buckets."""
     from lakeside_amd import synth
-    monkeypatch.setenv("LK_KEY_ROWS", "1")
     filt = synth.leaf(synth.NAME, "eq", "metric_07")
     _synth_case(engine, 2, 1 << 20, 0, 0.0, filt, "sum", [synth.CONTAINER], step=3600000, highcard_n=300000, hour=0)
     _synth_case(engine, 1, 1 << 20, 0, 0.0, filt, "count", [synth.CONTAINER], step=60000, highcard_n=20000, hour=0)
