@@ -38,7 +38,7 @@ $(SCAN_TILES): $(SRC)/scan_kernel.hpp
 $(SCAN_LEAN): $(SRC)/scan_kernel.hpp $(SRC)/lean_kernel.hpp
 
 $(LIB): $(HOST_OBJS) $(HIP_OBJS)
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o $@ $^ -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -l:libbrotlidec.so.1 -Wl,-rpath,$(ROCM)/lib
 
 # host-only RE2-semantics matcher (CPU differential tests against RE2; the evaluator links regex.cpp itself)
 $(RELIB): $(SRC)/regex.cpp $(SRC)/regex_capi.cpp $(SRC)/regex.hpp $(SRC)/unicode_tables.inc include/lakeside_regex.h
@@ -78,7 +78,7 @@ EXP_NAME ?= x
 exp: $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES)
 	@mkdir -p build/exp/$(EXP_NAME) lakeside_amd/exp
 	for a in sum min max count; do for m in d h; do $(HIPCC) $(HIPFLAGS) $(EXP_FLAGS) -c $(SRC)/scan_$${a}_lean_$${m}.hip -o build/exp/$(EXP_NAME)/scan_$${a}_lean_$${m}.o & done; done; wait
-	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_$(EXP_NAME).so $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES) build/exp/$(EXP_NAME)/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -Wl,-rpath,$(ROCM)/lib
+	$(HIPCC) -shared --offload-arch=$(ARCH) -o lakeside_amd/exp/liblakeside_gpu_$(EXP_NAME).so $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES) build/exp/$(EXP_NAME)/scan_*.o -L$(ROCM)/lib -lrccl -lz -l:libzstd.so.1 -l:liblz4.so.1 -l:libbrotlidec.so.1 -Wl,-rpath,$(ROCM)/lib
 .PHONY: exp
 
 # Host-only loader harness (no HIP): the Parquet walk, dictionary interning and staging copy of lakeside_amd/csrc/
@@ -86,7 +86,7 @@ exp: $(HOST_OBJS) $(OBJDIR)/kernels.o $(OBJDIR)/ex_kernels.o $(SCAN_TILES)
 LOADCHK_SRCS = tools/load_check.cpp $(SRC)/loader.cpp $(SRC)/parquet.cpp $(SRC)/codec.cpp $(SRC)/plan.cpp
 LOADCHK_DEPS = $(LOADCHK_SRCS) $(SRC)/loader.hpp $(SRC)/segment.hpp $(SRC)/parquet.hpp $(SRC)/codec.hpp $(SRC)/layout.hpp $(SRC)/plan.hpp $(SRC)/thrift.hpp
 LOADCHK_FLAGS = -std=c++17 -g -pthread -Wall -Wextra -Wno-unused-parameter
-LOADCHK_LIBS = -lz -l:libzstd.so.1 -l:liblz4.so.1
+LOADCHK_LIBS = -lz -l:libzstd.so.1 -l:liblz4.so.1 -l:libbrotlidec.so.1
 build/load_check: $(LOADCHK_DEPS)
 	@mkdir -p build
 	g++ -O2 $(LOADCHK_FLAGS) -o $@ $(LOADCHK_SRCS) $(LOADCHK_LIBS)

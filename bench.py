@@ -548,11 +548,13 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
 
     def run():
         evaluate()   # warm (page-in, thread pool)
+        log(f"rank {rank}: cpu baseline warm run done")   # (progress: a C5 shard takes ~45 s per run)
         times, table = [], None
-        for _ in range(3):
+        for i in range(3):
             t = []
             table = evaluate(timing=t)
             times.append(t[0])
+            log(f"rank {rank}: cpu baseline run {i + 1}/3: {t[0]:.3f} s")
         return sorted(times)[1], table
 
     if concurrent:
@@ -566,6 +568,7 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
         f"({_cpu_model()}, {os.cpu_count()} CPUs visible)")
     full = n == len(segs)
     if world > 1:   # every rank's shard time and cells -> rank 0
+        log(f"rank {rank}: sending the shard's cells to rank 0")
         times = [None] * world
         dist.all_gather_object(times, (dt, full))
         parts = [None] * world if rank == 0 else None
@@ -589,6 +592,7 @@ def cpu_baseline_and_validate(args, q, local_req, segs, gpu_res, world=1, rank=0
         dts = [dt]
     validated = None
     if full:
+        log(f"rank {rank}: comparing the GPU rows with the CPU restatement")
         has_gb = bool(q["group_bys"])
         want = (list(table),) if tag or exemplar else lkcpu.merge_cell_table(table, agg, has_gb)
         try:

@@ -6,7 +6,8 @@
 //   GZIP (2)    — zlib inflate, gzip or zlib header auto-detected
 //   ZSTD (6)    — the system libzstd (runtime library only in this image: the two entry points are declared below)
 //   LZ4_RAW (7) — the system liblz4 block decoder; LZ4 (5, deprecated): Hadoop framing, else one raw block
-// LZO (3) and BROTLI (4) are rejected with LK_ERR_UNSUPPORTED.
+//   BROTLI (4)  — the system libbrotlidec one-shot decoder (r06)
+// LZO (3) is rejected with LK_ERR_UNSUPPORTED.
 #include "codec.hpp"
 
 #include <zlib.h>
@@ -23,6 +24,9 @@ size_t ZSTD_decompress(void* dst, size_t dst_capacity, const void* src, size_t c
 unsigned ZSTD_isError(size_t code);
 const char* ZSTD_getErrorName(size_t code);
 int LZ4_decompress_safe(const char* src, char* dst, int compressed_size, int dst_capacity);
+// libbrotlidec.so.1: BrotliDecoderResult BrotliDecoderDecompress(...); BROTLI_DECODER_RESULT_SUCCESS = 1
+int BrotliDecoderDecompress(size_t encoded_size, const uint8_t* encoded_buffer, size_t* decoded_size,
+                            uint8_t* decoded_buffer);
 }
 
 namespace lk {
@@ -141,6 +145,12 @@ void decompress(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t ca
       if (r < 0 || size_t(r) != cap) bad("LZ4", "decode failed");
       return;
     }
+    case CODEC_BROTLI: {
+      size_t out = cap;
+      if (BrotliDecoderDecompress(n, src, &out, dst) != 1) bad("BROTLI", "decode failed");
+      if (out != cap) bad("BROTLI", "short output");
+      return;
+    }
     default:
       throw PlanError(LK_ERR_UNSUPPORTED, "parquet: compression codec " + std::to_string(codec) + " is not supported");
   }
@@ -148,7 +158,7 @@ void decompress(int codec, const uint8_t* src, size_t n, uint8_t* dst, size_t ca
 
 bool codec_supported(int codec) {
   return codec == CODEC_UNCOMPRESSED || codec == CODEC_SNAPPY || codec == CODEC_GZIP || codec == CODEC_ZSTD ||
-         codec == CODEC_LZ4 || codec == CODEC_LZ4_RAW;
+         codec == CODEC_LZ4 || codec == CODEC_LZ4_RAW || codec == CODEC_BROTLI;
 }
 
 }  // namespace pq

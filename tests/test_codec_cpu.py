@@ -21,7 +21,8 @@ def checker(tmp_path_factory):
     out = str(tmp_path_factory.mktemp("codec") / "page_codec_check")
     subprocess.run(["g++", "-O1", "-std=c++17", "-I", SRC, "-I", "/opt/rocm/include", "-D__HIP_PLATFORM_AMD__",
                     os.path.join(ROOT, "tools", "page_codec_check.cpp"), os.path.join(SRC, "codec.cpp"),
-                    os.path.join(SRC, "parquet.cpp"), "-o", out, "-lz", "-l:libzstd.so.1", "-l:liblz4.so.1"],
+                    os.path.join(SRC, "parquet.cpp"), "-o", out, "-lz", "-l:libzstd.so.1", "-l:liblz4.so.1",
+                    "-l:libbrotlidec.so.1"],
                    check=True)
     return out
 
@@ -41,7 +42,7 @@ def _table():
 
 
 @pytest.mark.parametrize("version", ["1.0", "2.0"])
-@pytest.mark.parametrize("codec", ["snappy", "gzip", "zstd", "lz4"])
+@pytest.mark.parametrize("codec", ["snappy", "gzip", "zstd", "lz4", "brotli"])
 def test_pages_decompress_to_the_uncompressed_pages(checker, tmp_path, codec, version):
     import pyarrow.parquet as pq
     t = _table()

@@ -274,8 +274,8 @@ def test_merged_min_absorbs_all_nan_glob(engine, tmp_path):
 
 
 def _write_exotic(path, rng, hour):
-    """clean columns + columns this engine does not decode: a struct, a list, an INT96 timestamp, a 16-byte
-    FIXED_LEN_BYTE_ARRAY and a BROTLI-compressed double; and a DELTA_BINARY_PACKED int64 (decoded since r06)."""
+    """clean columns + columns this engine does not decode: a struct, a list, an INT96 timestamp and a 16-byte
+    FIXED_LEN_BYTE_ARRAY; and a DELTA_BINARY_PACKED int64 and a BROTLI-compressed double (both decoded since r06)."""
     import pyarrow as pa
     import pyarrow.parquet as pq
     base = pq.read_table(_write(path, rng, hour))
@@ -299,9 +299,10 @@ def _write_exotic(path, rng, hour):
 
 def test_unloaded_columns_serve_other_queries(engine, tmp_path):
     """a file with columns this engine does not decode (nested struct / list, INT96,
-    FIXED_LEN_BYTE_ARRAY, BROTLI) still serves every query that does not reference them (GPU == oracle); a query that
+    FIXED_LEN_BYTE_ARRAY) still serves every query that does not reference them (GPU == oracle); a query that
     references one fails the call with LK_ERR_UNSUPPORTED (the caller falls back) instead of silently emptying the
-    glob.  The DELTA_BINARY_PACKED column is decoded at load (r06): a numeric leaf on it equals the oracle."""
+    glob.  The DELTA_BINARY_PACKED and BROTLI columns are decoded at load (r06): numeric leaves on them equal the
+    oracle."""
     from lakeside_amd import LK_MERGED, synth
     from lakeside_amd._lib import LK_ERR_UNSUPPORTED, LakesideError
     rng = np.random.default_rng(7)
@@ -314,9 +315,12 @@ def test_unloaded_columns_serve_other_queries(engine, tmp_path):
     cells, stats = _compare(engine, synth.pushdown(delta, _segs(2), "max", [synth.SERVICE]), paths, 1, "max",
                             "DELTA_BINARY_PACKED leaf")
     assert cells[0] and cells[1], stats
+    brot = {"op": "and", "q1": synth.leaf(synth.NAME, "in", "metric_01", "metric_02"),
+            "q2": {"k": "brot", "v": ["0.5"], "op": "lt", "dataType": "number"}}
+    cells, stats = _compare(engine, synth.pushdown(brot, _segs(2), "sum", []), paths, 1, "sum", "BROTLI leaf")
+    assert cells[0] and cells[1], stats
     for col, leaf in [("uuid", synth.leaf("uuid", "eq", "x")), ("attrs", synth.leaf("attrs", "eq", "x")),
                       ("tags", synth.leaf("tags", "eq", "x")),
-                      ("brot", {"k": "brot", "v": ["0.5"], "op": "lt", "dataType": "number"}),
                       ("ts96", {"k": "ts96", "v": ["5"], "op": "gt", "dataType": "number"})]:
         filt = {"op": "and", "q1": synth.leaf(synth.NAME, "eq", "metric_01"), "q2": leaf}
         with pytest.raises(LakesideError) as ei:

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Fixtures for the loader harness (tools/load_check.cpp, `make sanitize`), written into the directory given:
-compressed pages (SNAPPY / GZIP / ZSTD / LZ4, data page v1 and v2, NULLs), a PLAIN BYTE_ARRAY dictionary fallback,
+compressed pages (SNAPPY / GZIP / ZSTD / LZ4 / BROTLI, data page v1 and v2, NULLs), a PLAIN BYTE_ARRAY dictionary fallback,
 numeric dictionary pages, a large string dictionary (the parallel interning path: > 2^16 chunk-dictionary values per
 column), and a truncated file (a corrupt-file error).  The golden segments (tests/golden/segments) are passed by the
 caller as they are.  Test infrastructure: needs pyarrow (this container), never run on the GPU box."""
@@ -32,7 +32,7 @@ def main(out):
     os.makedirs(out, exist_ok=True)
     t = table(60_000, 1)
     strings = ["_cardinalhq.name", "resource.service.name"]
-    for codec in ("snappy", "gzip", "zstd", "lz4"):
+    for codec in ("snappy", "gzip", "zstd", "lz4", "brotli"):
         for ver in ("1.0", "2.0"):
             pq.write_table(t, os.path.join(out, f"codec_{codec}_v{ver[0]}.parquet"), compression=codec,
                            use_dictionary=strings, data_page_version=ver, row_group_size=25_000, data_page_size=16_384,
