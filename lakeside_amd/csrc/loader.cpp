@@ -795,8 +795,13 @@ HostLoad load_host(const std::string& key, const uint8_t* F, size_t size, int th
     GlobalDict& gd = dict(col.name);
     std::lock_guard<std::mutex> g(gd.mu);
     std::vector<std::string_view>& sv = gd.sc_views;   // (reused across loads)
-    sv.clear();
-    for (size_t rg = 0; rg < nrg; rg++) sv.insert(sv.end(), chunks[ci * nrg + rg].dict.begin(), chunks[ci * nrg + rg].dict.end());
+    std::vector<size_t> at(nrg + 1, 0);
+    for (size_t rg = 0; rg < nrg; rg++) at[rg + 1] = at[rg] + chunks[ci * nrg + rg].dict.size();
+    sv.resize(at[nrg]);
+    parallel_for(nrg, t, [&](size_t rg) {   // the row groups' chunk dictionaries side by side (16M views: C5)
+      const auto& d = chunks[ci * nrg + rg].dict;
+      std::copy(d.begin(), d.end(), sv.begin() + std::ptrdiff_t(at[rg]));
+    });
     col.remap.resize(sv.size());
     if (t > 1) mark("  views");
     gd.intern_all(sv, col.remap.data(), t);
