@@ -80,6 +80,15 @@ def generate_sql(pr: PushDownRequest, start: int, end: int, step: int, nonexiste
     chart_field_filter = "true"                                               # 407-426 (no fieldName)
     if be.dataset == METRICS:
         rollup = chart.rollup or SUM
+        if len(agg) > 1 and agg[0] == "p":   # BaseExpr.scala:379-383: MAX of the rollup per (ts, groupBys, name)
+            return (f'SELECT "{TIMESTAMP}", MAX(rollup_{rollup}) as value,'
+                    f' "{NAME}" as name  {gb} FROM ({sub}) '
+                    f" WHERE {chart_field_filter}"
+                    f' AND {fsql} GROUP BY "{TIMESTAMP}" {gb}, name ORDER BY "{TIMESTAMP}" ASC')
+        if agg == "ces":                      # BaseExpr.scala:385-388: every passing row, 1.0, no rollup column
+            return (f'SELECT "{TIMESTAMP}", 1.0 as value, "{NAME}" as name  {gb} FROM ({sub}) '
+                    f" WHERE {chart_field_filter}"
+                    f' AND {fsql} ORDER BY "{TIMESTAMP}" ASC')
         return (f'SELECT "{TIMESTAMP}", {agg}(rollup_{rollup}) as value,'
                 f' "{NAME}" as name  {gb} FROM ({sub}) '
                 f" WHERE {chart_field_filter}"
@@ -182,8 +191,10 @@ def run_sql(pr: PushDownRequest, seg_idx: Sequence[int], paths: Sequence[str]):
     # SQLite reads an unknown double-quoted identifier as a string literal; DuckDB raises a Binder Error
     # that the worker turns into an empty glob (Commons.scala:249-253).  Mirror DuckDB.
     import re
-    idents = set(re.findall(r'"([^"]+)"', sql)) | {"rollup_" + (pr.baseExpr.chart.rollup or SUM)
-                                                   if pr.baseExpr.dataset == METRICS else VALUE}
+    metrics_ces = pr.baseExpr.dataset == METRICS and pr.baseExpr.chart.aggregation == "ces"
+    idents = set(re.findall(r'"([^"]+)"', sql)) | (set() if metrics_ces else
+                                                   {"rollup_" + (pr.baseExpr.chart.rollup or SUM)
+                                                    if pr.baseExpr.dataset == METRICS else VALUE})
     if not idents <= set(union):
         con.close()
         return []
