@@ -154,6 +154,8 @@ struct Engine {
   std::mutex result_pool_mu;
   template <class F>
   void host_parallel(size_t n, F&& fn) {
+    static const bool no_pool = getenv("LK_NO_POOL") != nullptr;   // A/B: threads spawned per call
+    if (no_pool) return parallel_for(n, load_thread_count(), fn);
     WorkerPool* p;
     {
       std::lock_guard<std::mutex> g(result_pool_mu);

@@ -57,8 +57,9 @@ void parallel_for(size_t n, int threads, F&& fn) {
 
 // Persistent worker threads for per-call host work on the result path (large results' rows expanded while their
 // values cross the host link): a std::thread spawn costs tens of microseconds, 16 of them per call ~0.3 ms of C5's
-// ~2 ms evaluation; a wake-up costs microseconds.  One job at a time: a caller that finds the pool busy (another
-// evaluation's expansion on another thread) gets false and runs its job with parallel_for instead.
+// ~2 ms evaluation; a wake-up costs microseconds.  The caller works too and waits only for the workers that joined the
+// job (a worker still asleep when the items run out never touches it), so a slow wake-up delays nothing.  One job at
+// a time: a caller that finds the pool busy (another evaluation's expansion) gets false and uses parallel_for.
 class WorkerPool {
  public:
   explicit WorkerPool(int threads) {
@@ -74,7 +75,7 @@ class WorkerPool {
   }
   int threads() const { return int(th_.size()) + 1; }
   // fn(0..n-1) on the pool's threads and the calling thread; false (nothing ran) when the pool is busy.  The first
-  // exception is rethrown after every worker has left the job.
+  // exception is rethrown once no worker is inside the job.
   template <class F>
   bool try_run(size_t n, F&& fn) {
     std::unique_lock<std::mutex> job(job_mu_, std::try_to_lock);
@@ -86,13 +87,14 @@ class WorkerPool {
       n_ = n;
       next_.store(0);
       err_ = nullptr;
-      active_ = int(th_.size());
+      open_ = true;
       gen_++;
     }
     cv_.notify_all();
     work();
     std::unique_lock<std::mutex> g(mu_);
-    done_cv_.wait(g, [&] { return active_ == 0; });
+    open_ = false;                                   // late wakers see a closed job and go back to sleep
+    done_cv_.wait(g, [&] { return busy_ == 0; });    // only the workers inside work()
     fn_ = nullptr;
     if (err_) std::rethrow_exception(err_);
     return true;
@@ -117,13 +119,14 @@ class WorkerPool {
     for (;;) {
       {
         std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(g, [&] { return stop_ || (open_ && gen_ != seen); });
         if (stop_) return;
         seen = gen_;
+        busy_++;
       }
       work();
       std::lock_guard<std::mutex> g(mu_);
-      if (--active_ == 0) done_cv_.notify_all();
+      if (--busy_ == 0) done_cv_.notify_all();
     }
   }
   std::mutex job_mu_;   // held by the submitting caller for the job's duration
@@ -132,7 +135,8 @@ class WorkerPool {
   std::function<void(size_t)>* fn_ = nullptr;
   size_t n_ = 0;
   std::atomic<size_t> next_{0};
-  int active_ = 0;
+  int busy_ = 0;
+  bool open_ = false;
   uint64_t gen_ = 0;
   bool stop_ = false;
   std::exception_ptr err_;
