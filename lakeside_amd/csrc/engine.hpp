@@ -148,21 +148,12 @@ struct Engine {
   // hardware threads, at most 16) and the pinned staging area its upload goes through (under dev_mu).
   int load_threads = 0;
   int load_thread_count() const;
-  // Result-path host work (large results' rows expanded on the host while their values cross the link): a persistent
-  // pool of load_thread_count() threads, created on first use; a call that finds it busy spawns its own threads.
-  std::unique_ptr<WorkerPool> result_pool;
-  std::mutex result_pool_mu;
+  // Result-path host work (large results' rows expanded on the host while their values cross the link): threads
+  // spawned per call, the job's whole thread share.  A persistent pool measured slower (C5 eval 2.66 vs 1.94 ms,
+  // profiles/r06_ab_c5_pool.json / _spawned_threads.json) and was removed.
   template <class F>
   void host_parallel(size_t n, F&& fn) {
-    static const bool no_pool = getenv("LK_NO_POOL") != nullptr;   // A/B: threads spawned per call
-    if (no_pool) return parallel_for(n, load_thread_count(), fn);
-    WorkerPool* p;
-    {
-      std::lock_guard<std::mutex> g(result_pool_mu);
-      if (!result_pool) result_pool = std::make_unique<WorkerPool>(load_thread_count());
-      p = result_pool.get();
-    }
-    if (!p->try_run(n, fn)) parallel_for(n, p->threads(), fn);
+    parallel_for(n, load_thread_count(), fn);
   }
   void* load_pinned = nullptr;
   size_t load_pinned_cap = 0;

@@ -1492,9 +1492,9 @@ static int evaluate_once(Engine& E, const std::shared_ptr<const Request>& Rp, co
   const size_t o_bpos = reserve(ts_runs_ok ? (size_t(nbuckets) + 1) * 4 : 0);
   // host side only (mapped): the existence bit of every output key of a large grouped result (FParams::key_bits)
   const uint64_t okeys = per_glob_rows ? ncells : (collapse ? nbuckets : nbuckets * ngroups);
-  // default since r06 (LK_NO_KEY_ROWS=1 for A/B): with the row expansion on the job's whole thread share (a persistent
-  // pool) it runs while the values cross the host link -- C5 eval 2.64 -> 1.93 ms (profiles/r06_ab_c5_*); r05's
-  // 8-thread expansion measured slower (2.28 vs 2.13 ms)
+  // default since r06 (LK_NO_KEY_ROWS=1 for A/B): with the row expansion on the job's whole thread share it runs while
+  // the values cross the host link -- C5 eval 2.64 -> 1.93 ms (profiles/r06_ab_c5_*); r05's 8-thread expansion measured
+  // slower (2.28 vs 2.13 ms)
   const bool key_rows_ok = !collapse && okeys >= kTsRunsMinKeys && !getenv("LK_NO_KEY_ROWS");
   const size_t o_kbits = reserve(key_rows_ok ? size_t((okeys + 2047) / 2048) * 2048 / 8 : 0);
   // staging buffers: a rank-local failure here is agreed on after the scan stage (no scan runs on this rank)

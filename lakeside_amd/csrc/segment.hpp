@@ -3,7 +3,6 @@
 // (tools/load_check.cpp, `make sanitize`).
 #pragma once
 #include <atomic>
-#include <condition_variable>
 #include <cstdint>
 #include <exception>
 #include <functional>
@@ -54,94 +53,6 @@ void parallel_for(size_t n, int threads, F&& fn) {
   for (auto& th : pool) th.join();
   if (err) std::rethrow_exception(err);
 }
-
-// Persistent worker threads for per-call host work on the result path (large results' rows expanded while their
-// values cross the host link): a std::thread spawn costs tens of microseconds, 16 of them per call ~0.3 ms of C5's
-// ~2 ms evaluation; a wake-up costs microseconds.  The caller works too and waits only for the workers that joined the
-// job (a worker still asleep when the items run out never touches it), so a slow wake-up delays nothing.  One job at
-// a time: a caller that finds the pool busy (another evaluation's expansion) gets false and uses parallel_for.
-class WorkerPool {
- public:
-  explicit WorkerPool(int threads) {
-    for (int t = 1; t < threads; t++) th_.emplace_back([this] { loop(); });   // the caller is the last worker
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& t : th_) t.join();
-  }
-  int threads() const { return int(th_.size()) + 1; }
-  // fn(0..n-1) on the pool's threads and the calling thread; false (nothing ran) when the pool is busy.  The first
-  // exception is rethrown once no worker is inside the job.
-  template <class F>
-  bool try_run(size_t n, F&& fn) {
-    std::unique_lock<std::mutex> job(job_mu_, std::try_to_lock);
-    if (!job.owns_lock()) return false;
-    std::function<void(size_t)> f(std::forward<F>(fn));
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      fn_ = &f;
-      n_ = n;
-      next_.store(0);
-      err_ = nullptr;
-      open_ = true;
-      gen_++;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> g(mu_);
-    open_ = false;                                   // late wakers see a closed job and go back to sleep
-    done_cv_.wait(g, [&] { return busy_ == 0; });    // only the workers inside work()
-    fn_ = nullptr;
-    if (err_) std::rethrow_exception(err_);
-    return true;
-  }
-
- private:
-  void work() {
-    for (;;) {
-      const size_t i = next_.fetch_add(1);
-      if (i >= n_) return;
-      try {
-        (*fn_)(i);
-      } catch (...) {
-        std::lock_guard<std::mutex> g(err_mu_);
-        if (!err_) err_ = std::current_exception();
-        next_.store(n_);
-      }
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || (open_ && gen_ != seen); });
-        if (stop_) return;
-        seen = gen_;
-        busy_++;
-      }
-      work();
-      std::lock_guard<std::mutex> g(mu_);
-      if (--busy_ == 0) done_cv_.notify_all();
-    }
-  }
-  std::mutex job_mu_;   // held by the submitting caller for the job's duration
-  std::mutex mu_, err_mu_;
-  std::condition_variable cv_, done_cv_;
-  std::function<void(size_t)>* fn_ = nullptr;
-  size_t n_ = 0;
-  std::atomic<size_t> next_{0};
-  int busy_ = 0;
-  bool open_ = false;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-  std::exception_ptr err_;
-  std::vector<std::thread> th_;
-};
 
 // Append-only string array in fixed 64K-entry blocks behind a fixed block table: an element never moves, and
 // reading an element published before (under the owner's mutex) needs no lock, so results keep reading tag
