@@ -68,18 +68,45 @@ constexpr uint32_t LEAN_LIST = LK_LEAN_LIST;                           // per-wa
 #ifndef LK_LEAN_PF0
 #define LK_LEAN_PF0 (LK_LEAN_LIST0 ? 2 : 0)
 #endif
+#ifndef LK_LEAN_PF0E
+#define LK_LEAN_PF0E 0   // NL = 0 dense-code shape (EARLY): chunk loads in the round itself
+#endif
 #ifndef LK_LEAN_PF0C
 #define LK_LEAN_PF0C 2   // NL = 0 COUNT (no value gather): 0.857 -> 0.754 ms on `count` with 2 rounds in flight
 #endif
 #ifndef LK_LEAN_PF1
 #define LK_LEAN_PF1 1
 #endif
+// unrotated chunk ring (A/B: -DLK_LEAN_SLOTS=0, the rotated ring of r02-r06): see the main loop
+#ifndef LK_LEAN_SLOTS
+#define LK_LEAN_SLOTS 1
+#endif
+// deferred trips of the late-column shapes (opt-in A/B: -DLK_LEAN_DEFER=1): see list_trip.  The pending trip's
+// registers (rows, group terms, late words) live across the chunk rounds, so these shapes run a shallower chunk ring
+// (LK_LEAN_PF1D / LK_LEAN_PF2D) and the COUNT(*) one 4 waves per SIMD (LK_LEAN_WAVES1D).  Measured (r06, validated):
+// tag 0.970 -> 1.161 ms, C4 1.352 -> 1.357, C3 1.786 -> 1.784, with a 2-deep ring C4 1.409, C3 1.820 -- the other
+// waves on the SIMD already hide the trip's first round trip, and the shallower ring / fewer waves cost more than
+// the overlap buys (profiles/r06_ab_defer_*.json)
+#ifndef LK_LEAN_DEFER
+#define LK_LEAN_DEFER 0
+#endif
+#define LEAN_DEFER(NL, AGG) (LK_LEAN_DEFER && (NL) > 0)
+#ifndef LK_LEAN_PF1D
+#define LK_LEAN_PF1D 1
+#endif
+#ifndef LK_LEAN_PF2D
+#define LK_LEAN_PF2D 1
+#endif
+#ifndef LK_LEAN_WAVES1D
+#define LK_LEAN_WAVES1D 4
+#endif
 #ifndef LK_LEAN_PF2
 #define LK_LEAN_PF2 3
 #endif
 // waves per SIMD the kernel is built for (A/B: -DLK_LEAN_WAVES1 / -DLK_LEAN_WAVES2)
 #define LEAN_WAVES(NL, AGG) ((NL) == 0 ? ((AGG) == AGG_COUNT || !LK_LEAN_LIST0 ? LK_LEAN_WAVES1 : LK_LEAN_WAVES0V) \
-                                      : (NL) == 1 ? ((AGG) == AGG_COUNT ? LK_LEAN_WAVES1 : LK_LEAN_WAVES1V) : LK_LEAN_WAVES2)
+                                      : (NL) == 1 ? ((AGG) == AGG_COUNT ? (LEAN_DEFER(NL, AGG) ? LK_LEAN_WAVES1D : LK_LEAN_WAVES1) \
+                                                                        : LK_LEAN_WAVES1V) : LK_LEAN_WAVES2)
 constexpr int LEAN_ROWS = LK_LEAN_ROWS;                                // listed rows per lane per trip (A/B: -DLK_LEAN_ROWS)
 constexpr uint32_t LEAN_TRIP = 64u * LEAN_ROWS;                        // listed rows per trip
 // the per-wave list is a ring indexed with & (LEAN_LIST - 1) and drained LEAN_TRIP rows at a time
@@ -648,9 +675,38 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
     acc_add<AGG>(acc, true, v);
   };
 
-  // N rows per lane (rr[u] live when aa[u]) with group terms dd[u]: late columns (run lookup + packed word, all N
-  // rows' loads in flight together), late filter, timestamp / value gather, accumulate
-  auto rowsN = [&](auto ncst, auto ldc, const uint32_t* rr, const bool* aa, uint32_t* dd) __attribute__((always_inline)) {
+  // The late-column loads of N rows per lane (rr[u] live when aa[u]): run lookup + packed word lw[u][k], its bit
+  // offset / RLE code lm[u][k]; all N rows' loads in flight together
+  auto late_issue = [&](auto ncst, const uint32_t* rr, const bool* aa, auto& lw, auto& lm) __attribute__((always_inline)) {
+    constexpr int N = decltype(ncst)::value;
+#pragma unroll
+    for (int k = 0; k < NL; k++) {
+#pragma unroll
+      for (int u = 0; u < N; u++) {
+        lw[u][k] = v2u{0u, 0u};
+        lm[u][k] = 0u;
+      }
+      if (!((lpres >> k) & 1u)) continue;   // uniform
+#pragma unroll
+      for (int u = 0; u < N; u++) {
+        const uint32_t v = lvb[k] + rr[u];
+        const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
+        const LRun lr = L.lruns[k][ri];
+        const bool lt = (lr.off_lit & 0x80000000u) != 0u;
+        const uint32_t bit = (v - lr.start) * lbw[k];
+        const uint32_t byte = (lr.off_lit & 0x7fffffffu) + (bit >> 3);
+        lw[u][k] = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], (aa[u] && lt) ? (byte & ~3u) : OOB, 0, 0);
+        lm[u][k] = lt ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : lr.value;
+        if (count_plan && aa[u] && lt) {   // distinct 128-B lines of the late stream gathered
+          const uint32_t l = ((byte & ~3u) >> 7) - ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
+          if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
+        }
+      }
+    }
+  };
+  // N rows per lane (rr[u] live when aa[u]) with group terms dd[u] and their late-column words lw / lm (late_issue,
+  // issued by the caller): late filter, timestamp / value gather, accumulate
+  auto rowsN = [&](auto ncst, auto ldc, const uint32_t* rr, const bool* aa, uint32_t* dd, auto& lw, auto& lm) __attribute__((always_inline)) {
     constexpr int N = decltype(ncst)::value;
     constexpr bool LATE_DONE = decltype(ldc)::value;   // late columns decoded already (dd complete): values only
     bool p[N], ld[N];   // ld: rows whose timestamp / value loads were issued (plan bytes)
@@ -669,33 +725,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
       }
     };
     if constexpr (NL > 0 && !LATE_DONE) {
-      // with no late filter leaf every row passes, so the timestamp / value loads go out with the late-column loads
-      v2u lw[N][LT::NLA];
-      uint32_t lm[N][LT::NLA];
-#pragma unroll
-      for (int k = 0; k < NL; k++) {
-#pragma unroll
-        for (int u = 0; u < N; u++) {
-          lw[u][k] = v2u{0u, 0u};
-          lm[u][k] = 0u;
-        }
-        if (!((lpres >> k) & 1u)) continue;   // uniform
-#pragma unroll
-        for (int u = 0; u < N; u++) {
-          const uint32_t v = lvb[k] + rr[u];
-          const int ri = lnr[k] == 1u ? 0 : lean_find_run(L.lruns[k], L.lrblk[k], nblk, lvb[k], v);
-          const LRun lr = L.lruns[k][ri];
-          const bool lt = (lr.off_lit & 0x80000000u) != 0u;
-          const uint32_t bit = (v - lr.start) * lbw[k];
-          const uint32_t byte = (lr.off_lit & 0x7fffffffu) + (bit >> 3);
-          lw[u][k] = __builtin_amdgcn_raw_buffer_load_b64(lrs[k], (aa[u] && lt) ? (byte & ~3u) : OOB, 0, 0);
-          lm[u][k] = lt ? (0x80000000u | ((byte & 3u) * 8u + (bit & 7u))) : lr.value;
-          if (count_plan && aa[u] && lt) {   // distinct 128-B lines of the late stream gathered
-            const uint32_t l = ((byte & ~3u) >> 7) - ((L.lruns[k][0].off_lit & 0x7fffffffu) >> 7);
-            if (l < LEAN_LLINES * 32u) atomicOr(&L.lines_l[k][l >> 5], 1u << (l & 31u));
-          }
-        }
-      }
+      // with no late filter leaf every row passes, so the timestamp / value loads go out with the late-column words
       // speculative gather (P.spec_gather): with a late filter, every listed row's timestamp / value loads go out now,
       // with its late-column loads, instead of after the late filter -- one dependent memory round trip less per trip
       // for the loads of the rows the filter then drops
@@ -774,14 +804,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
   // all their value loads in flight together -- is ready, across the tile's rounds; the rest drains at the tile's end.
   uint32_t lhead = 0, ltail = 0;   // wave-uniform list positions (mod LEAN_LIST)
   uint32_t* const wl = L.wlist[LT::LISTED ? (tid >> 6) : 0];
+  // Deferred trips (LK_LEAN_DEFER, the late-column shapes outside early_late): a trip's late-column words are issued
+  // and the trip is finished (decode, late filter, value gather, accumulate) only at the next trip or the tile's end,
+  // so its first memory round trip overlaps the chunk rounds in between instead of being waited for on the spot.
+  // Needs the unrotated chunk ring (a rotated ring's latch waits for every load in flight, the trip's included).
+  uint32_t prr[LEAN_ROWS], pdd[LEAN_ROWS];
+  bool paa[LEAN_ROWS];
+  v2u plw[LEAN_ROWS][LT::NLA];
+  uint32_t plm[LEAN_ROWS][LT::NLA];
+  bool pend = false;   // (uniform) a deferred trip is in flight
   auto list_trip = [&](auto ec, uint32_t n) __attribute__((always_inline)) {   // the n (<= LEAN_TRIP) rows at lhead
     constexpr bool ELIST = decltype(ec)::value;   // entries carry complete group terms (early_late)
+    constexpr bool DEFER = LEAN_DEFER(NL, AGG) && !ELIST;
     if (P.ablate & 0x20000u) {   // diagnostics only: listed rows dropped unprocessed (the trips' cost)
       lhead += n;
       return;
     }
     uint32_t rr[LEAN_ROWS], dd[LEAN_ROWS];
     bool aa[LEAN_ROWS];
+    if constexpr (DEFER) {
+      if (pend) rowsN(std::integral_constant<int, LEAN_ROWS>{}, ec, prr, paa, pdd, plw, plm);   // the previous trip
+    }
 #pragma unroll
     for (int u = 0; u < LEAN_ROWS; u++) {
       const uint32_t i = uint32_t(lane) + 64u * uint32_t(u);
@@ -790,7 +833,21 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
       rr[u] = x & 0xffffu;
       dd[u] = ELIST ? (x >> 16) : (npass > 1 ? (L.lut[x >> 16] & DIM_MASK) * stride : dim_u);
     }
-    rowsN(std::integral_constant<int, LEAN_ROWS>{}, ec, rr, aa, dd);
+    if constexpr (DEFER) {
+      late_issue(std::integral_constant<int, LEAN_ROWS>{}, rr, aa, plw, plm);
+#pragma unroll
+      for (int u = 0; u < LEAN_ROWS; u++) {
+        prr[u] = rr[u];
+        paa[u] = aa[u];
+        pdd[u] = dd[u];
+      }
+      pend = true;
+    } else {
+      v2u lw[LEAN_ROWS][LT::NLA];
+      uint32_t lm[LEAN_ROWS][LT::NLA];
+      if constexpr (NL > 0 && !ELIST) late_issue(std::integral_constant<int, LEAN_ROWS>{}, rr, aa, lw, lm);
+      rowsN(std::integral_constant<int, LEAN_ROWS>{}, ec, rr, aa, dd, lw, lm);
+    }
     lhead += n;
   };
   auto wave_sync = [&]() __attribute__((always_inline)) {   // the wave's list writes / reads are ordered
@@ -819,8 +876,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
     // The packed codes of the next PF rounds are in flight while a round runs (a register ring; loads return in issue
     // order, so a round waits only for its own chunk): a round's own work is far shorter than a memory round trip, and
     // one load per lane in flight would leave the tile's stream latency-bound (PF = 0: loaded in the round itself).
-    constexpr int PF = NL == 0 ? (EARLY ? 0 : AGG == AGG_COUNT ? LK_LEAN_PF0C : LK_LEAN_PF0)
-                               : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : LK_LEAN_PF1V) : LK_LEAN_PF2);
+    constexpr int PF = NL == 0 ? (EARLY ? LK_LEAN_PF0E : AGG == AGG_COUNT ? LK_LEAN_PF0C : LK_LEAN_PF0)
+                               : (NL == 1 ? (AGG == AGG_COUNT ? LK_LEAN_PF1 : (LEAN_DEFER(NL, AGG) ? LK_LEAN_PF1D : LK_LEAN_PF1V))
+                                          : (LEAN_DEFER(NL, AGG) ? LK_LEAN_PF2D : LK_LEAN_PF2));
     auto chunk_load = [&](uint32_t qq) __attribute__((always_inline)) {
       const bool lv = qq < total;
       const LeanRun Rn = L.runs[lv ? L.ctab[qq] : 0u];
@@ -870,7 +928,17 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
       }
     };
     if constexpr (ECH) late_load(uint32_t(tid));
-    for (uint32_t q0 = 0; q0 < total; q0 += BLOCK) {   // uniform trip count
+    // Ring slots (LK_LEAN_SLOTS, r06): outside the early_late bodies round j consumes slot j % PF and refills it right
+    // after the slot's last use, and the rounds run PF at a time (the loop below), so each slot keeps its registers.  A
+    // rotated ring (x = xr[0]; xr[i] = xr[i + 1]) copies the newest load's registers at the loop latch, and that copy
+    // waits for the load (s_waitcnt vmcnt(0): the counter retires in order) -- one exposed memory round trip per round
+    // however deep the ring, which is what left the COUNT shapes latency-bound (`count` 0.733 -> 0.476 ms with the
+    // load-free COUNT rows below).  The late-column shapes keep the rotated ring: their list trips wait on their own
+    // loads, which drains the ring either way (tag 0.969 / 0.973 ms, C4 1.351 / 1.351), and C3's three unrolled rounds
+    // spill (1.80 -> 1.86 ms); C2 measured the same both ways (1.105 ms) and keeps the slots.
+    constexpr bool ROT = PF > 0 && (ECH || (NL > 0 && !LEAN_DEFER(NL, AGG)) || !LK_LEAN_SLOTS);
+    auto round = [&](uint32_t q0, auto slc) __attribute__((always_inline)) {
+      constexpr int S = decltype(slc)::value;   // the ring slot this round consumes (unrotated ring)
       const uint32_t q = q0 + uint32_t(tid);
       const bool live = q < total;
       const LeanRun R = L.runs[live ? L.ctab[q] : 0u];
@@ -884,11 +952,13 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
       const uint32_t byte = (R.off_lit & 0x7fffffffu) + 2u * BW * k;
       v4u x;
       LWin lcur[LT::NLA];
-      if constexpr (PF > 0) {
+      if constexpr (ROT) {
         x = xr[0];
 #pragma unroll
         for (int i = 0; i + 1 < PF; i++) xr[i] = xr[i + 1];
         xr[PF - 1] = chunk_load(q + uint32_t(PF) * BLOCK);
+      } else if constexpr (PF > 0) {
+        x = xr[S];   // refilled below, after its last use
       } else {
         x = __builtin_amdgcn_raw_buffer_load_b128(rs2, (live && lit) ? (byte & ~3u) : OOB, 0, 0);
       }
@@ -901,6 +971,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
       uint32_t w0 = __builtin_amdgcn_alignbit(x.y, x.x, sh);
       uint32_t w1 = __builtin_amdgcn_alignbit(x.z, x.y, sh);
       uint32_t w2 = __builtin_amdgcn_alignbit(x.w, x.z, sh);
+      if constexpr (PF > 0 && !ROT) xr[S] = chunk_load(q + uint32_t(PF) * BLOCK);   // x is dead: the slot's next chunk
       if (!lit) {   // RLE run: every field holds the run's code
         if constexpr (POW2) {
           w0 = w1 = rval * REP;
@@ -938,7 +1009,11 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
         m = f & valid;
       }
       const uint32_t rbase = v0 - vb2;   // tile row of value v0
-      if (NL == 0 && dense_codes) {   // uniform
+      // (not built into the unrotated-ring COUNT(*) shape: its rows gather nothing to coalesce unless the timestamps are
+      // unsorted, and the block's registers would spill inside the round -- a spill reload waits like any load; the
+      // host sends dense filters to the EARLY shape, which keeps the block)
+      constexpr bool DENSE_BLK = NL == 0 && !(AGG == AGG_COUNT && !EARLY && LK_LEAN_SLOTS);
+      if (DENSE_BLK && dense_codes) {   // uniform
         // Dense block: the wave's 64 chunks are 1024 row-contiguous rows and most chunks pass several rows.  The
         // per-lane loop below would have each load instruction touch 64 different 128-B lines (8 B used of each,
         // the other 120 B re-fetched by later trips -- evicted from L2 in between when every row passes), so the
@@ -1033,7 +1108,27 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
         }
       }
       constexpr bool LIST0 = NL == 0 && LK_LEAN_LIST0 && AGG != AGG_COUNT && !EARLY;
-      if (!LT::LISTED || (NL == 0 && (!LIST0 || dense_codes))) {   // uniform
+      if (AGG == AGG_COUNT && NL == 0 && LK_LEAN_SLOTS && !ts_gather && !P.nvl) {   // uniform
+        // COUNT(*) with every row's bucket from the zone map or the split: no per-row load, so no loop here carries
+        // one (a wait at its head would drain the chunk ring too).  One passing code and no split boundary inside the
+        // chunk: the chunk's rows are one register-cell add of their popcount.
+        const uint32_t n = uint32_t(__popcll(m));
+        const uint32_t c0 = split ? split_class(rbase) : 1u, c15 = split ? split_class(rbase + 15u) : 1u;
+        if (n && npass == 1 && c0 == c15) {
+          if (c0 != 0u && (!split || c0 < nsb)) {   // inside the window
+            row(0, 0.0, dim_u, rbase + (uint32_t(__builtin_ctzll(m)) >> shs));
+            acc.rows += n - 1u;
+            acc.cnt += n - 1u;
+          }
+        } else {
+          while (m) {
+            const uint32_t e = uint32_t(__builtin_ctzll(m)) >> shs;
+            m &= m - 1ull;
+            const uint32_t d = npass > 1 ? (L.lut[lit ? lean_code<BW>(w0, w1, w2, e) : rval] & DIM_MASK) * stride : dim_u;
+            row(0, 0.0, d, rbase + e);
+          }
+        }
+      } else if (!LT::LISTED || (NL == 0 && (!LIST0 || dense_codes))) {   // uniform
         // passing rows: two per trip (their loads in flight together)
         while (m) {
           const uint32_t e1 = uint32_t(__builtin_ctzll(m)) >> shs;
@@ -1049,7 +1144,9 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
           const uint32_t rr[2] = {rbase + e1, rbase + e2};
           const bool aa[2] = {true, two};
           uint32_t dd[2] = {d1, d2};
-          rowsN(std::integral_constant<int, 2>{}, std::false_type{}, rr, aa, dd);
+          v2u lw[2][LT::NLA];   // (NL = 0 here: no late columns)
+          uint32_t lm[2][LT::NLA];
+          rowsN(std::integral_constant<int, 2>{}, std::false_type{}, rr, aa, dd, lw, lm);
         }
       } else if constexpr (LT::LISTED) {
         // Late columns: the wave's passing rows are appended to its LDS list (lane-major) and processed LEAN_TRIP at
@@ -1136,7 +1233,7 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
               atomicAdd(rv + x, 1ull);
               if (rrows_on) atomicAdd(rrows + x, 1ull);
             }
-            continue;   // (uniform) the next round of chunks
+            return;   // (uniform) the next round of chunks
           }
         }
         if (P.ablate & 0x10000u) fm = 0;   // diagnostics only: no row listed (the chunk filter's cost alone)
@@ -1179,9 +1276,25 @@ __global__ __launch_bounds__(BLOCK) __attribute__((amdgpu_waves_per_eu(EARLY ? (
           wave_sync();   // the trips' entries are rewritten by later appends
         }
       }
+    };
+    if constexpr (ROT || PF <= 1) {
+      for (uint32_t q0 = 0; q0 < total; q0 += BLOCK) round(q0, std::integral_constant<int, 0>{});   // uniform trip count
+    } else {
+      for (uint32_t q0 = 0; q0 < total; q0 += uint32_t(PF) * BLOCK) {   // uniform: PF rounds, slots 0 .. PF - 1
+        round(q0, std::integral_constant<int, 0>{});
+        if (q0 + BLOCK < total) round(q0 + BLOCK, std::integral_constant<int, 1>{});
+        if constexpr (PF > 2) {
+          if (q0 + 2u * BLOCK < total) round(q0 + 2u * BLOCK, std::integral_constant<int, 2>{});
+        }
+        static_assert(PF <= 3, "ring slots: rounds unrolled up to 3");
+      }
     }
     if constexpr (LT::LISTED) {
       while (ltail != lhead) list_trip(ec, min(LEAN_TRIP, ltail - lhead));   // the tile's last rows
+      if constexpr (LEAN_DEFER(NL, AGG) && !ECH) {
+        if (pend) rowsN(std::integral_constant<int, LEAN_ROWS>{}, ec, prr, paa, pdd, plw, plm);   // the last trip
+        pend = false;
+      }
       wave_sync();
     }
   };
