@@ -594,7 +594,7 @@ def test_dist_metrics_percentile_and_ces_world2(tmp_path):
     class _Files:   # the files only: each rank's engine loads its shard
         def load_segment(self, path):
             pass
-    paths, _, segs = _metrics_segments(_Files(), tmp_path, [(0, True), (1, True), (0, False), (1, True)])
+    paths, _, segs = _metrics_segments(_Files(), tmp_path, [(0, True), (1, True), (0, False), (1, True)], n=60_000)
     mp.spawn(_worker_metrics_sketch, args=(2, _free_port(), paths, segs), nprocs=2, join=True)
 
 

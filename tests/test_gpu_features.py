@@ -11,7 +11,7 @@ from tests.parity import assert_rows_equal
 pytestmark = pytest.mark.gpu
 
 
-def _metrics_segments(engine, tmp_path, specs):
+def _metrics_segments(engine, tmp_path, specs, n=150_000):
     """Metrics segments (rollup_sum / rollup_max value columns) written by pyarrow; specs = [(hour, aligned)]:
     aligned timestamps sit on the 60 s step grid, unaligned ones on arbitrary milliseconds."""
     import pyarrow as pa
@@ -21,7 +21,6 @@ def _metrics_segments(engine, tmp_path, specs):
     rng = np.random.default_rng(77)
     keys, blobs, segs = [], [], []
     for i, (hour, aligned) in enumerate(specs):
-        n = 150_000
         t0 = synth.T0 + hour * synth.HOUR
         ts = t0 + (60_000 * rng.integers(0, 60, n) if aligned else rng.integers(0, synth.HOUR, n))
         vals = rng.integers(0, 1000, n).astype(np.float64)
@@ -37,7 +36,7 @@ def _metrics_segments(engine, tmp_path, specs):
         strings = [synth.NAME, synth.SERVICE]
         pq.write_table(t, path, compression="NONE", use_dictionary=strings,
                        column_encoding={c: "PLAIN" for c in t.column_names if c not in strings},
-                       row_group_size=50_000, data_page_size=65536)
+                       row_group_size=n // 3, data_page_size=65536)
         engine.load_segment(path)
         keys.append(path)
         blobs.append(open(path, "rb").read())
@@ -239,7 +238,7 @@ def test_metrics_percentiles_and_cardinality(engine, tmp_path):
     segments (the 1 ms re-run), NULL rollup values and NULL group values; per glob and merged vs the oracle."""
     from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
     from oracle import dataexpr as dx, hll
-    keys, blobs, segs = _metrics_segments(engine, tmp_path, [(0, True), (1, True), (0, False)])
+    keys, blobs, segs = _metrics_segments(engine, tmp_path, [(0, True), (1, True), (0, False)], n=60_000)
     for filt, agg, gbs, rollup in [(synth.leaf(synth.NAME, "in", "metric_01", "metric_02"), "p95", [], None),
                                    (synth.leaf(synth.NAME, "!=", "metric_03"), "p50", [synth.SERVICE], "max"),
                                    (synth.leaf(synth.SERVICE, "regex", "svc-00[0-3]"), "p99.9", [synth.SERVICE, synth.NAME], None)]:
@@ -253,10 +252,11 @@ def test_metrics_percentiles_and_cardinality(engine, tmp_path):
         assert sum(len(w) for w in want) > 1000
         res = engine.eval_pushdown(req, keys, 2, LK_PER_GLOB_ROWS)
         assert list(res.ts) == sorted(res.ts)
+        per = [[] for _ in want]   # one pass over the rows, bucketed by glob
+        for r, g in enumerate(np.asarray(res.globs).tolist()):
+            per[g].append((int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r)))
         for gi in range(len(want)):
-            got = [(int(res.ts[r]), res.tags[r], float(res.values[r]), res.sketch(r))
-                   for r in range(len(res)) if int(res.globs[r]) == gi]
-            _pct_rows_equal(got, want[gi], q, f"metrics {agg} glob {gi}")
+            _pct_rows_equal(per[gi], want[gi], q, f"metrics {agg} glob {gi}")
         merged = engine.eval_pushdown(req, keys, 2, LK_MERGED)
         got = [(int(merged.ts[r]), merged.tags[r], float(merged.values[r]), merged.sketch(r)) for r in range(len(merged))]
         _pct_rows_equal(got, dx.merge_percentile(pr, want), q, f"metrics {agg} merged")
