@@ -73,3 +73,46 @@ def result_columns(res):
             fallback[r] = tag_key(m)
     key = join_tag_columns(names, cols, fallback) if names else fallback
     return np.array(res.ts, dtype=np.int64), np.array(res.values, dtype=np.float64), key
+
+
+def check_columns(engine, req, keys, blobs, glob_size, flags=("per_glob", "merged")):
+    """GPU rows of a request (per glob and / or merged) vs the C++ restatement (oracle/cpu, the bench's full-size
+    validator; itself checked against oracle/dataexpr and the golden rows in tests/test_oracle_cpu.py), compared
+    column-wise with numpy: the bar of assert_rows_equal without a Python object per row, for results of 10^5-10^6
+    rows.  Returns {"per_glob": Result, "merged": Result} for the flags run."""
+    import os
+
+    import numpy as np
+
+    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS
+    from oracle import cpu as lkcpu
+    from oracle import dataexpr as dx
+    pr = dx.parse_pushdown(req)
+    agg = pr.baseExpr.chart.aggregation
+    table = lkcpu.evaluate_cell_table(pr, glob_size, blobs, min(16, os.cpu_count() or 1))
+    out = {}
+    if "per_glob" in flags:
+        res = engine.eval_pushdown(req, keys, glob_size, LK_PER_GLOB_ROWS)
+        ts, val, key = result_columns(res)
+        globs = np.asarray(res.globs)
+        assert len(ts) == len(table), f"per-glob rows {len(ts)} vs expected {len(table)}"
+        for g in range(int(table.glob.max()) + 1 if len(table) else 0):
+            sel = table.glob == g
+            cnt = table.count[sel]
+            if agg == dx.COUNT:
+                want = cnt.astype(np.float64)
+            elif agg in (dx.SUM, dx.AVG):   # CpuCell.agg_value: hi + lo is the double-double's rounded sum
+                s = table.hi[sel] + table.lo[sel]
+                want = np.where(cnt > 0, s if agg == dx.SUM else s / np.maximum(cnt, 1), 0.0)
+            else:
+                want = np.where(cnt > 0, (table.vmin if agg == dx.MIN else table.vmax)[sel], 0.0)
+            m = globs == g
+            lkcpu.assert_columns_equal((ts[m], val[m], key[m]), (table.ts[sel], want, table.key[sel]), agg,
+                                       f"glob {g}")
+        out["per_glob"] = res
+    if "merged" in flags:
+        res = engine.eval_pushdown(req, keys, glob_size, LK_MERGED)
+        lkcpu.assert_columns_equal(result_columns(res), lkcpu.merge_cell_table(table, agg, bool(pr.baseExpr.chart.groupBys)),
+                                   agg, "merged")
+        out["merged"] = res
+    return out

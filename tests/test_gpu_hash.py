@@ -143,42 +143,11 @@ def _check(engine, keys, blobs, filt, agg, gbs, step, hour, glob_size=10, flags=
 
 
 def _check_columns(engine, keys, blobs, filt, agg, gbs, step, hour, glob_size=10, flags=("per_glob", "merged")):
-    """_check for results of ~10^5-10^6 rows, compared column-wise (numpy) against the C++ restatement
-    (oracle/cpu, the bench's full-size validator, itself checked against oracle/dataexpr in tests/test_oracle_cpu.py):
-    the same cells and bar as _check without a Python object per row."""
-    from lakeside_amd import LK_MERGED, LK_PER_GLOB_ROWS, synth
-    from oracle import cpu as lkcpu
-    from oracle import dataexpr as dx
-    from tests.parity import result_columns
+    """_check for results of ~10^5-10^6 rows, compared column-wise against the C++ restatement (tests/parity.py)."""
+    from lakeside_amd import synth
+    from tests.parity import check_columns
     segs = [synth.segment_request(i, step=step, hour=hour) for i in range(len(keys))]
-    req = json.dumps(synth.pushdown(filt, segs, agg, gbs))
-    pr = dx.parse_pushdown(req)
-    table = lkcpu.evaluate_cell_table(pr, glob_size, blobs, min(16, os.cpu_count() or 1))
-    out = {}
-    if "per_glob" in flags:
-        res = engine.eval_pushdown(req, keys, glob_size, LK_PER_GLOB_ROWS)
-        ts, val, key = result_columns(res)
-        globs = np.asarray(res.globs)
-        assert len(ts) == len(table), f"per-glob rows {len(ts)} vs expected {len(table)}"
-        for g in range(int(table.glob.max()) + 1 if len(table) else 0):
-            sel = table.glob == g
-            cnt = table.count[sel]
-            if agg == dx.COUNT:
-                want = cnt.astype(np.float64)
-            elif agg in (dx.SUM, dx.AVG):
-                s = table.hi[sel] + table.lo[sel]
-                want = np.where(cnt > 0, s if agg == dx.SUM else s / np.maximum(cnt, 1), 0.0)
-            else:
-                want = np.where(cnt > 0, (table.vmin if agg == dx.MIN else table.vmax)[sel], 0.0)
-            m = globs == g
-            lkcpu.assert_columns_equal((ts[m], val[m], key[m]), (table.ts[sel], want, table.key[sel]), agg,
-                                       f"glob {g}")
-        out["per_glob"] = res
-    if "merged" in flags:
-        res = engine.eval_pushdown(req, keys, glob_size, LK_MERGED)
-        lkcpu.assert_columns_equal(result_columns(res), lkcpu.merge_cell_table(table, agg, bool(gbs)), agg, "merged")
-        out["merged"] = res
-    return out
+    return check_columns(engine, json.dumps(synth.pushdown(filt, segs, agg, gbs)), keys, blobs, glob_size, flags)
 
 
 @pytest.mark.timeout(600)
